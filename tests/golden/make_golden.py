@@ -1,0 +1,180 @@
+"""Generate the committed golden fixtures by running the REFERENCE itself (build container only).
+
+Run:  PYTHONDONTWRITEBYTECODE=1 python tests/golden/make_golden.py [/root/reference]
+
+The reference (possoj/Spacecraft-Pose-Estimation-Framework) is imported read-only from its checkout with
+in-memory stubs for the packages absent here (brevitas, torchvision: class-definition use only; cv2:
+module-level import only). Nothing is written into the reference tree and no reference source or
+bytecode is copied into this repository -- only input/output vectors land in ``tests/golden/*.npz``.
+
+Fixtures (all small):
+  fwd_64x64_b2.npz, fwd_240x384_b1.npz, fwd_512x512_b1.npz
+      seeded uint8 NHWC frames -> reference ModelWrapper(MobileNetV2, URSONetHead) float32 outputs
+      (ori logits, pos, 1280-d pooled features) with the seeded synthetic weights of
+      spef_amd.weights.synthetic_state_dict(seed=1001) (digest stored to pin the generator).
+  decode_ori.npz   random + planted orientation logits -> reference SPEUtils.last_activ + decode.
+  decode_pos.npz   random position logits (POS: classification) -> reference last_activ + decode.
+  encode.npz       reference OrientationSoftClassification.encode / PositionSoftClassification.encode.
+  keypoints.npz    reference KeyPoints.create_keypoints2d for the 1,800 valid.json poses.
+  score.npz        reference SPEUtils.get_score on perturbed poses.
+"""
+from __future__ import annotations
+
+import importlib.abc
+import importlib.machinery
+import json
+import os
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, os.path.join(REPO, 'spacecraft-pose-estimation-framework_amd'))
+
+
+def _install_stubs():
+    class _Meta(type):
+        def __getattr__(c, n):
+            if n.startswith('__'):
+                raise AttributeError(n)
+            return n
+
+    class _Any(types.ModuleType):
+        def __getattr__(s, n):
+            if n.startswith('__'):
+                raise AttributeError(n)
+            c = _Meta(n, (object,), {})
+            setattr(s, n, c)
+            return c
+
+    class _Finder(importlib.abc.MetaPathFinder, importlib.abc.Loader):
+        def find_spec(s, f, p, t=None):
+            if f.split('.')[0] in ('brevitas', 'torchvision'):
+                return importlib.machinery.ModuleSpec(f, s, is_package=True)
+
+        def create_module(s, spec):
+            return _Any(spec.name)
+
+        def exec_module(s, m):
+            m.__path__ = []
+
+    sys.meta_path.insert(0, _Finder())
+    sys.modules['cv2'] = types.ModuleType('cv2')
+
+
+def frames_u8(b, h, w, seed):
+    """Seeded SPEED-like frames: dark background, sensor noise, a bright textured blob."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    yy, xx = np.mgrid[0:h, 0:w]
+    out = np.empty((b, h, w, 3), np.uint8)
+    for i in range(b):
+        cy, cx = rng.uniform(0.3, 0.7) * h, rng.uniform(0.3, 0.7) * w
+        r = rng.uniform(0.1, 0.3) * min(h, w)
+        blob = 180 * np.exp(-(((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * r * r)))
+        tex = 40 * np.sin(xx / rng.uniform(2, 6)) * np.cos(yy / rng.uniform(2, 6))
+        g = np.clip(blob + tex * (blob > 20) + rng.normal(0, 2.0, (h, w)) + 8, 0, 255).astype(np.uint8)
+        out[i] = g[..., None]            # grayscale replicated to RGB (src/data/utils.py:215)
+    return out
+
+
+def main(ref_root='/root/reference'):
+    _install_stubs()
+    sys.dont_write_bytecode = True
+    sys.path.insert(0, ref_root)
+    import torch
+    from src.modeling.backbone.mobilenet_v2 import MobileNetV2
+    from src.modeling.head.ursonet import URSONetHead
+    from src.modeling.common.pytorch_layers import ModelWrapper
+    from src.spe.spe_utils import SPEUtils
+    from src.spe.keypoints_utils import KeyPoints
+    from src.data.datasets.speed import Camera
+    from spef_amd.weights import synthetic_state_dict, state_dict_digest
+    from spef_amd.arch import mobilenet_v2
+
+    torch.set_num_threads(8)
+    seed = 1001
+
+    # ---------------------------------------------------------------- forward fixtures
+    sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=seed)
+    model = ModelWrapper(MobileNetV2(3, 1280, True, True), URSONetHead(1280, 1728, 3, True, 0.2))
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    model.eval()
+    feats = {}
+    model.head.register_forward_hook(lambda m, i, o: feats.__setitem__('f', i[0].mean([2, 3]).detach()))
+    for (h, w, b, s) in ((64, 64, 2, 11), (240, 384, 1, 12), (512, 512, 1, 13)):
+        fr = frames_u8(b, h, w, s)
+        x = torch.from_numpy(fr).permute(0, 3, 1, 2).float().div(255)     # ToTensor()
+        with torch.no_grad():
+            ori, pos = model(x)
+        np.savez_compressed(os.path.join(HERE, f'fwd_{h}x{w}_b{b}.npz'), frames=fr, ori=ori.numpy(),
+                            pos=pos.numpy(), pooled=feats['f'].numpy(), seed=seed,
+                            digest=state_dict_digest(sd))
+        print('fwd', h, w, b, float(ori.abs().max()), float(pos.abs().max()))
+
+    # ---------------------------------------------------------------- decode fixtures
+    cam = Camera()
+    kp_path = os.path.join(ref_root, 'models', '3d_models', 'tangoPoints.mat')
+    su = SPEUtils(cam, 'classification', 12, 3, False, 'classification', 10, 100, kp_path)
+    valid = json.load(open(os.path.join(ref_root, 'src/data/datasets/speed_split/valid.json')))
+    q_true = np.array([v['q_vbs2tango'] for v in valid], np.float32)
+    t_true = np.array([v['r_Vo2To_vbs_true'] for v in valid], np.float32)
+
+    rng = np.random.Generator(np.random.PCG64(seed))
+    rand_logits = (rng.standard_normal((64, 1728)) * 2.0).astype(np.float32)
+    pose = su.last_activ({'ori_soft': rand_logits.copy(), 'pos_soft': np.zeros((64, 1000), np.float32)})
+    rand_soft = pose['ori_soft'].copy()
+    rand_q, _ = su.orientation.decode_batch(rand_soft)
+
+    # planted logits: log(encode(q_true)) * T (softmax of which is encode(q)^T renormalised)
+    temps = np.array([1.0, 0.5, 0.2], np.float32)
+    n_pl = 256
+    planted = np.zeros((len(temps), n_pl, 1728), np.float32)
+    planted_q = np.full((len(temps), n_pl, 4), np.nan, np.float32)
+    # np.linalg.inv(a) at classification_utils.py:142 raises LinAlgError when `a` is singular (mass on <= 3
+    # bins); the reference discards h_inv (spe_utils.py:97) but still raises. Such rows are recorded as NaN.
+    planted_raised = np.zeros((len(temps), n_pl), bool)
+    for ti, T in enumerate(temps):
+        enc = np.stack([su.orientation.encode(q_true[i]) for i in range(n_pl)])
+        lg = (np.log(np.maximum(enc, 1e-30)) / T).astype(np.float32)
+        lg = np.maximum(lg, np.float32(-80.0 / T))
+        planted[ti] = lg
+        p = su.last_activ({'ori_soft': lg.copy(), 'pos_soft': np.zeros((n_pl, 1000), np.float32)})
+        for i in range(n_pl):
+            try:
+                planted_q[ti, i], _ = su.orientation.decode(p['ori_soft'][i])
+            except np.linalg.LinAlgError:
+                planted_raised[ti, i] = True
+    np.savez_compressed(os.path.join(HERE, 'decode_ori.npz'), rand_logits=rand_logits,
+                        rand_soft=rand_soft[:16], rand_q=rand_q, temps=temps,
+                        planted_logits=planted[:, :32], planted_q=planted_q, planted_raised=planted_raised, q_true=q_true, t_true=t_true,
+                        hist=su.orientation.histogram, redundant=su.orientation.redundant_flags)
+
+    pos_logits = (rng.standard_normal((64, 1000)) * 2.0).astype(np.float32)
+    p = su.last_activ({'ori_soft': np.zeros((64, 1728), np.float32), 'pos_soft': pos_logits.copy()})
+    pos_dec = su.position.decode_batch(p['pos_soft'])
+    enc_pos = np.stack([su.position.encode(t_true[i]) for i in range(32)])
+    np.savez_compressed(os.path.join(HERE, 'decode_pos.npz'), logits=pos_logits, soft=p['pos_soft'][:8],
+                        pos=pos_dec, grid=su.position.histogram, enc_t=t_true[:32], enc=enc_pos)
+
+    enc_ori = np.stack([su.orientation.encode(q_true[i]) for i in range(16)])
+    np.savez_compressed(os.path.join(HERE, 'encode.npz'), q=q_true[:16], enc=enc_ori)
+
+    kp = KeyPoints(cam, kp_path)
+    k2d = np.stack([kp.create_keypoints2d(q_true[i], t_true[i]) for i in range(len(valid))])
+    np.savez_compressed(os.path.join(HERE, 'keypoints.npz'), q=q_true, t=t_true, kp2d=k2d,
+                        kp3d=kp.keypoints3d, K=cam.K, nu=cam.nu, nv=cam.nv)
+
+    # score on perturbed predictions
+    qp = q_true[:64] + rng.normal(0, 0.02, (64, 4)).astype(np.float32)
+    qp /= np.linalg.norm(qp, axis=1, keepdims=True)
+    tp = t_true[:64] + rng.normal(0, 0.1, (64, 3)).astype(np.float32)
+    sc = SPEUtils.get_score({'ori': q_true[:64], 'pos': t_true[:64]}, {'ori': qp, 'pos': tp})
+    np.savez_compressed(os.path.join(HERE, 'score.npz'), q_true=q_true[:64], t_true=t_true[:64], q_pred=qp,
+                        t_pred=tp, **{k: np.float64(v) for k, v in sc.items()})
+    print('decode fixtures written')
+
+
+if __name__ == '__main__':
+    main(*sys.argv[1:])

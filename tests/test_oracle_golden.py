@@ -1,0 +1,90 @@
+"""Pin the CPU oracle against the reference's own outputs (tests/golden/*.npz, made by make_golden.py)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import decode_ref as D
+from oracle import model_ref as M
+from spef_amd.arch import mobilenet_v2
+from spef_amd.weights import state_dict_digest, synthetic_state_dict
+
+
+@pytest.fixture(scope='module')
+def sd():
+    return synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=1001)
+
+
+def test_weight_generator_digest(sd, golden):
+    assert str(golden('fwd_64x64_b2.npz')['digest']) == state_dict_digest(sd)
+
+
+@pytest.mark.parametrize('name', ['fwd_64x64_b2.npz', 'fwd_240x384_b1.npz', 'fwd_512x512_b1.npz'])
+def test_forward_matches_reference(sd, golden, name):
+    g = golden(name)
+    torch.set_num_threads(8)
+    ori, pos = M.forward(M.u8_nhwc_to_nchw_f32(g['frames']), sd)
+    # same ops, same order, same torch build: expected bit-identical; 1e-6 allows thread-count reassociation
+    np.testing.assert_allclose(ori.numpy(), g['ori'], rtol=0, atol=1e-6)
+    np.testing.assert_allclose(pos.numpy(), g['pos'], rtol=0, atol=1e-6)
+
+
+def test_histograms_match_reference(golden):
+    g = golden('decode_ori.npz')
+    h, red = D.orientation_histogram(12, False)
+    np.testing.assert_array_equal(red, g['redundant'])
+    np.testing.assert_allclose(h, g['hist'], rtol=0, atol=1e-15)
+    gp = golden('decode_pos.npz')
+    np.testing.assert_allclose(D.position_histogram(10), gp['grid'], rtol=0, atol=1e-12)
+
+
+def test_encode_matches_reference(golden):
+    g = golden('encode.npz')
+    h, red = D.orientation_histogram(12, False)
+    enc = np.stack([D.encode_orientation(q, h, red) for q in g['q']])
+    np.testing.assert_allclose(enc, g['enc'], rtol=1e-6, atol=1e-9)
+    gp = golden('decode_pos.npz')
+    grid = D.position_histogram(10)
+    encp = np.stack([D.encode_position(t, grid) for t in gp['enc_t']])
+    np.testing.assert_allclose(encp, gp['enc'], rtol=1e-6, atol=1e-9)
+
+
+def test_softmax_and_orientation_decode_random(golden):
+    g = golden('decode_ori.npz')
+    p = D.softmax_f32(g['rand_logits'])
+    np.testing.assert_allclose(p[:16], g['rand_soft'], rtol=1e-6, atol=0)
+    q = D.decode_orientation_batch(p, g['hist'])
+    assert D.angle_deg_stable(q, g['rand_q']).max() < 1e-4
+
+
+def test_orientation_decode_planted(golden):
+    g = golden('decode_ori.npz')
+    h, red = D.orientation_histogram(12, False)
+    for ti, T in enumerate(g['temps']):
+        n = g['planted_q'].shape[1]
+        enc = np.stack([D.encode_orientation(q, h, red) for q in g['q_true'][:n]])
+        lg = np.maximum((np.log(np.maximum(enc, 1e-30)) / T).astype(np.float32), np.float32(-80.0 / T))
+        np.testing.assert_array_equal(lg[:32], g['planted_logits'][ti])
+        q = D.decode_orientation_batch(D.softmax_f32(lg), h)
+        ok = ~g['planted_raised'][ti]
+        assert D.angle_deg_stable(q[ok], g['planted_q'][ti][ok]).max() < 1e-4
+
+
+def test_position_decode(golden):
+    g = golden('decode_pos.npz')
+    p = D.softmax_f32(g['logits'])
+    np.testing.assert_allclose(p[:8], g['soft'], rtol=1e-6)
+    np.testing.assert_allclose(D.decode_position_batch(p, g['grid']), g['pos'], rtol=1e-6, atol=1e-6)
+
+
+def test_keypoint_projection(golden):
+    g = golden('keypoints.npz')
+    k = np.stack([D.create_keypoints2d(g['q'][i], g['t'][i], g['kp3d']) for i in range(g['q'].shape[0])])
+    np.testing.assert_allclose(k, g['kp2d'], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(D.SPEED_K, g['K'])
+
+
+def test_score(golden):
+    g = golden('score.npz')
+    s = D.get_score(g['q_true'], g['t_true'], g['q_pred'], g['t_pred'])
+    for k, v in s.items():
+        np.testing.assert_allclose(v, g[k], rtol=1e-6)
