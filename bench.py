@@ -1,0 +1,203 @@
+"""SPEF MI355X benchmark: images/sec at 512x512, batch 64 per GPU (BASELINE.json metric).
+
+A "step" = one pass of the hot path over one batch: uint8 NHWC frames already resident in HBM ->
+MobileNet-V2 backbone -> URSONet head -> on-device decode (softmax + Markley orientation average, position
+regression), i.e. SPEMi355x.predict minus the host copies. Weights: seeded synthetic (spef_amd.weights),
+BN folded, fp16 storage / fp32 accumulate. Frames: synthetic SPEED-style (dark background + noise + bright
+target), generated once per rank from (seed, global frame index).
+
+Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per GPU,
+rank 0 packs the weight blob and RCCL-broadcasts it (torch.distributed 'nccl' = RCCL over xGMI); every rank
+then runs independent batches of 64 (frame-parallel, weak scaling, no data-path collective). Timing: barrier +
+device sync on both sides of exactly K steps, max over ranks; value = all ranks' images / that time.
+
+Rank 0 prints ONE JSON line (see DESIGN.md "Measurement" for every field).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, 'spacecraft-pose-estimation-framework_amd'))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+MFMA_PEAK_TFLOPS = 2500.0      # dense fp16/bf16 MFMA, no sparsity
+
+
+def synth_frames(b: int, h: int, w: int, first_index: int, seed: int = 1001):
+    """SPEED-style uint8 NHWC frames (grayscale replicated to RGB, src/data/utils.py:215)."""
+    import numpy as np
+    out = np.empty((b, h, w, 3), np.uint8)
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
+    for i in range(b):
+        rng = np.random.Generator(np.random.PCG64([seed, first_index + i]))
+        cy, cx = rng.uniform(0.25, 0.75) * h, rng.uniform(0.25, 0.75) * w
+        r = rng.uniform(0.05, 0.25) * min(h, w)
+        g = 200.0 * np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * r * r))
+        g += 30.0 * np.sin(xx / rng.uniform(2, 8)) * (g > 20)
+        g += rng.normal(8.0, 2.0, (h, w)).astype(np.float32)
+        out[i] = np.clip(g, 0, 255).astype(np.uint8)[..., None]
+    return out
+
+
+def cpu_baseline(args, sd):
+    """The CPU oracle (FP32 PyTorch restatement of the reference eval path: forward + softmax + Markley decode,
+    pinned to the reference by tests/golden) timed on this host's cores, on a bounded sample."""
+    import numpy as np
+    import torch
+    from oracle import decode_ref as D
+    from oracle import model_ref as M
+    threads = min(args.cpu_threads, os.cpu_count() or 1)
+    torch.set_num_threads(threads)
+    h, _ = D.orientation_histogram(12, False)
+    bs, nb = args.cpu_batch, args.cpu_batches
+    x = M.u8_nhwc_to_nchw_f32(synth_frames(bs, args.size, args.size, 10_000))
+    o, p = M.forward(x[:2], sd)                                        # warm-up
+    t0 = time.perf_counter()
+    for _ in range(nb):
+        o, p = M.forward(x, sd)
+        D.decode_orientation_batch(D.softmax_f32(o.numpy()), h)
+    dt = time.perf_counter() - t0
+    return {'value': round(bs * nb / dt, 3), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+            'sample': f'{nb} batches x {bs} synthetic {args.size}x{args.size} frames, FP32 torch CPU forward + '
+                      f'NumPy softmax/Markley decode (oracle/, pinned to the reference by tests/golden), '
+                      f'{threads} threads, {dt:.1f} s'}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--steps', type=int, default=30)
+    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--batch', type=int, default=64)
+    ap.add_argument('--size', type=int, default=512)
+    ap.add_argument('--dtype', default='fp16', choices=['fp16', 'bf16'])
+    ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--cpu-threads', type=int, default=16)
+    ap.add_argument('--cpu-batch', type=int, default=64)
+    ap.add_argument('--cpu-batches', type=int, default=3)
+    args = ap.parse_args()
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        os.environ.setdefault('MASTER_ADDR', '127.0.0.1')
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', rank=rank, world_size=world, device_id=torch.device(f'cuda:{local}'))
+    dev = torch.device(f'cuda:{local}')
+    torch.cuda.set_device(dev)
+
+    from spef_amd import blob as Bl
+    from spef_amd.arch import flops_per_image, mobilenet_v2
+    from spef_amd.engine import Engine
+    from spef_amd.spe.spe_utils import SPEUtils
+    from spef_amd.weights import synthetic_state_dict
+
+    sd = None
+    if rank == 0:
+        sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=1001)
+        blob = np.frombuffer(Bl.pack(sd, dtype=args.dtype), np.uint8)
+        nbytes = torch.tensor([blob.size], dtype=torch.int64, device=dev)
+    else:
+        nbytes = torch.zeros(1, dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.broadcast(nbytes, 0)
+    dblob = torch.empty(int(nbytes.item()), dtype=torch.uint8, device=dev)
+    if rank == 0:
+        dblob.copy_(torch.from_numpy(blob))
+    if world > 1:
+        dist.broadcast(dblob, 0)                     # RCCL weight broadcast over xGMI
+    eng = Engine(dblob, dev)
+    su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
+    eng.set_decode_tables(su.orientation.histogram, None)
+
+    B, S = args.batch, args.size
+    frames = torch.from_numpy(synth_frames(B, S, S, rank * B)).to(dev)
+    eng.reserve(B, S, S)
+    ori = torch.empty((B, eng.n_out0), dtype=torch.float32, device=dev)
+    pos = torch.empty((B, eng.n_out1), dtype=torch.float32, device=dev)
+
+    def step():
+        eng.forward(frames, ori, pos)
+        return eng.decode(1, 0, ori, pos, want_soft=True)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        out = step()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    assert not out['status'].any().item(), 'decode reported NaN'
+
+    # roofline leg: per-kernel HIP events on the engine's stream, K more steps
+    eng.profile_begin()
+    for _ in range(args.steps):
+        step()
+    prof = eng.profile_end()
+
+    if rank == 0:
+        total_img = B * args.steps * world
+        value = total_img / elapsed
+        dom_key = max(prof, key=lambda k: prof[k][1])
+        n, ms, byts, fl = prof[dom_key]
+        avg_s = ms / n / 1e3
+        ach_gbs = byts / n / avg_s / 1e9
+        ach_tfl = fl / n / avg_s / 1e12
+        fpi = flops_per_image(S, S)
+        step_ms = elapsed / args.steps * 1e3
+        rec = {
+            'metric': 'images/sec at 512x512 batch 64 per GPU (MobileNetV2+URSONet forward + on-device decode)',
+            'value': round(value, 2),
+            'unit': 'images/sec',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': round(step_ms, 4),
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': args.dtype,
+            'data': 'synthetic SPEED-style uint8 frames resident in HBM; seeded random weights (BN-calibrated)',
+            'config': {'workload': f'C3: full net + decode, {S}x{S}, batch {B} per GPU', 'global_batch': B * world,
+                       'image_size': S, 'parallelism': f'frame-parallel x{world} (RCCL weight bcast)'},
+            'roofline': {'bound': 'hbm', 'kernel': dom_key, 'achieved': round(ach_gbs, 1), 'peak': HBM_PEAK_GBS,
+                         'unit': 'GB/s', 'frac': round(ach_gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'avg_launch_us': round(avg_s * 1e6, 2), 'launches_per_step': n / args.steps,
+                         'kernel_mfma_tflops': round(ach_tfl, 2)},
+            'mfma_utilisation_whole_net': round(fpi * value / world / 1e12 / MFMA_PEAK_TFLOPS, 5),
+            'kernels': {k: {'launches_per_step': v[0] / args.steps, 'ms_per_step': round(v[1] / args.steps, 4),
+                            'GB/s': round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] > 0 else None}
+                        for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1])},
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            rec['cpu_baseline'] = cpu_baseline(args, sd)
+        print(json.dumps(rec), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

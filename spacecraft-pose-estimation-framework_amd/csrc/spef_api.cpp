@@ -1,0 +1,551 @@
+// C ABI (include/spef.h) and the layer executor of the SPEF MI355X target.
+//
+// The executor walks the blob's op list (stem -> 17 inverted residuals -> last 1x1 -> head) over four
+// NHWC activation buffers sized at spef_reserve time, launching one kernel per conv (unfused v1 schedule).
+#include "../../include/spef.h"
+
+#include <hip/hip_runtime.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "spef_blob.hpp"
+#include "spef_kernels.hpp"
+
+using namespace spef;
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+#define HIP_TRY(expr)                                                                                  \
+  do {                                                                                                 \
+    hipError_t e_ = (expr);                                                                            \
+    if (e_ != hipSuccess) return fail(SPEF_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+  } while (0)
+
+struct spef_ctx {
+  int device = 0;
+  BlobHeader hdr{};
+  std::vector<OpDesc> ops;
+  uint8_t* d_data = nullptr;  // device copy of the blob's data section
+  size_t data_bytes = 0;
+  bool loaded = false;
+  // workspace
+  int ws_B = 0, ws_H = 0, ws_W = 0;
+  size_t buf_bytes = 0;
+  void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
+  float* pooled = nullptr;  // [B][1280] fp32
+  // decode tables
+  double* d_ori_bins = nullptr;
+  int n_ori_bins = 0;
+  double* d_pos_grid = nullptr;
+  int n_pos_bins = 0;
+  // per-launch HIP-event profiling (bench.py roofline leg)
+  bool profiling = false;
+  struct Rec {
+    std::string key;
+    hipEvent_t a, b;
+    double bytes, flops;
+  };
+  std::vector<Rec> recs;
+  std::vector<hipEvent_t> pool;
+  size_t pool_next = 0;
+};
+
+namespace {
+
+struct Dev {  // RAII device guard
+  int prev = -1;
+  explicit Dev(int d) {
+    hipGetDevice(&prev);
+    if (prev != d) hipSetDevice(d);
+  }
+  ~Dev() {
+    if (prev >= 0) hipSetDevice(prev);
+  }
+};
+
+inline int conv_out(int h, int s) { return (h + 2 - 3) / s + 1; }
+
+hipEvent_t next_event(spef_ctx* c) {
+  if (c->pool_next >= c->pool.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    c->pool.push_back(e);
+  }
+  return c->pool[c->pool_next++];
+}
+
+// Launch `fn` (returns hipError_t); when profiling, bracket it with events tagged by kernel key and its
+// algorithmic bytes / flops (what roofline.achieved is priced in).
+template <typename F>
+hipError_t prof_launch(spef_ctx* c, hipStream_t s, const char* key, double bytes, double flops, F&& fn) {
+  if (!c->profiling) return fn();
+  hipEvent_t a = next_event(c), b = next_event(c);
+  if (!a || !b) return hipErrorOutOfMemory;
+  hipEventRecord(a, s);
+  hipError_t e = fn();
+  hipEventRecord(b, s);
+  c->recs.push_back({key, a, b, bytes, flops});
+  return e;
+}
+
+const char* pw_key(int dt, int epi, int N) {
+  // mirrors pw_dispatch's tile choice so keys name the kernel instantiation rocprof reports
+  static thread_local std::string k;
+  const int n16 = ((N + 15) & ~15) / 16;
+  int nt = 1, mt = 4;
+  if (n16 == 1) { nt = 1; mt = 4; }
+  else if (n16 == 2) { nt = 2; mt = 4; }
+  else if (n16 == 4) { nt = 4; mt = 4; }
+  else if (n16 % 6 == 0) { nt = 6; mt = 2; }
+  else if (n16 % 5 == 0) { nt = 5; mt = 2; }
+  else if (n16 % 4 == 0) { nt = 4; mt = 4; }
+  else if (n16 % 3 == 0) { nt = 3; mt = 4; }
+  else if (n16 % 2 == 0) { nt = 2; mt = 4; }
+  k = std::string("pw_kernel<") + (dt == DT_F16 ? "F16" : "BF16") + "," + std::to_string(nt) + "," +
+      std::to_string(mt) + "," + std::to_string(epi) + ">";
+  return k.c_str();
+}
+
+template <typename T>
+inline const T* ptr(const spef_ctx* c, uint64_t off) {
+  return off == kAbsent ? nullptr : reinterpret_cast<const T*>(c->d_data + off);
+}
+
+size_t elem_size(const spef_ctx* c) { return 2; }  // fp16 / bf16 activations
+
+// algorithmic HBM bytes of one pointwise launch: read X, write Y (+ read residual), weights + bias once
+double pw_bytes(int64_t M, uint32_t K, uint32_t N, bool res) {
+  const double kp = (K + 31) & ~31u, np_ = (N + 15) & ~15u;
+  return (double)M * K * 2 + (double)M * N * 2 * (res ? 2 : 1) + np_ * kp * 2 + np_ * 4;
+}
+
+// Max activation elements per image over the backbone schedule for an H x W input.
+int64_t max_act_elems(const spef_ctx* c, int H, int W, int* fh, int* fw) {
+  int64_t mx = 0;
+  int h = H, w = W;
+  for (const OpDesc& op : c->ops) {
+    if (op.kind == OP_STEM) {
+      h = conv_out(h, 2);
+      w = conv_out(w, 2);
+      mx = std::max<int64_t>(mx, (int64_t)h * w * op.cout);
+    } else if (op.kind == OP_IRB) {
+      mx = std::max<int64_t>(mx, (int64_t)h * w * op.hidden);  // expand output
+      const int oh = conv_out(h, op.stride), ow = conv_out(w, op.stride);
+      mx = std::max<int64_t>(mx, (int64_t)oh * ow * op.hidden);
+      mx = std::max<int64_t>(mx, (int64_t)oh * ow * op.cout);
+      h = oh;
+      w = ow;
+    } else if (op.kind == OP_LAST) {
+      mx = std::max<int64_t>(mx, (int64_t)h * w * op.cout);  // unfused last conv (spef_backbone)
+    }
+  }
+  if (fh) *fh = h;
+  if (fw) *fw = w;
+  return mx;
+}
+
+int check_ready(spef_ctx* c, int B, int H, int W) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  if (!c->loaded) return fail(SPEF_ERR_STATE, "weights not loaded (spef_load_weights)");
+  if (B <= 0 || H < 32 || W < 32) return fail(SPEF_ERR_ARG, "bad input shape");
+  if (B > c->ws_B || (int64_t)H * W > (int64_t)c->ws_H * c->ws_W || H != c->ws_H || W != c->ws_W)
+    return fail(SPEF_ERR_STATE, "workspace not reserved for this shape (spef_reserve)");
+  return SPEF_OK;
+}
+
+// Runs the backbone. mode: 0 = full (pool into c->pooled), 1 = stop after op `stop` and leave the
+// activation in *out_buf, 2 = unfused last conv (feature map in *out_buf).
+int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W, hipStream_t s, int mode,
+                 int stop, void** out_buf, int* oc, int* oh, int* ow) {
+  const int dt = (int)c->hdr.dtype;
+  void* cur = nullptr;
+  int h = H, w = W, ch = 3;
+  int op_index = 0;
+  auto pick = [&](std::initializer_list<void*> busy) -> void* {
+    for (void* b : c->buf) {
+      bool used = false;
+      for (void* u : busy) used |= (u == b);
+      if (!used) return b;
+    }
+    return nullptr;
+  };
+  for (const OpDesc& op : c->ops) {
+    if (op.kind == OP_STEM) {
+      const int OH = conv_out(h, 2), OW = conv_out(w, 2);
+      void* y = c->buf[0];
+      const double px = (double)B * OH * OW;
+      const double in_b = (double)B * h * w * 3 * (layout == IN_U8_NHWC ? 1 : 4);
+      HIP_TRY(prof_launch(c, s, layout == IN_U8_NHWC ? "stem_kernel<u8>" : "stem_kernel<f32>",
+                          in_b + px * 32 * 2, px * 2 * 27 * 32, [&] {
+        return launch_stem(dt, layout, input, ptr<float>(c, op.w0), ptr<float>(c, op.b0), y, B, h, w, OH, OW, s);
+      }));
+      cur = y;
+      h = OH;
+      w = OW;
+      ch = (int)op.cout;
+    } else if (op.kind == OP_IRB) {
+      const int64_t M = (int64_t)B * h * w;
+      void* x = cur;
+      void* h1 = x;
+      if (op.expand != 1) {
+        h1 = pick({x});
+        HIP_TRY(prof_launch(c, s, pw_key(dt, EPI_RELU, op.hidden), pw_bytes(M, op.cin, op.hidden, false),
+                            2.0 * M * op.cin * op.hidden, [&] {
+          return launch_pw(dt, EPI_RELU, x, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, h1, M, (int)op.cin,
+                           (int)op.hidden, s);
+        }));
+      }
+      const int OH = conv_out(h, (int)op.stride), OW = conv_out(w, (int)op.stride);
+      void* h2 = pick({x, h1});
+      const double opx = (double)B * OH * OW;
+      HIP_TRY(prof_launch(c, s, op.stride == 1 ? "dw_kernel<1>" : "dw_kernel<2>",
+                          ((double)B * h * w + opx) * op.hidden * 2 + 40.0 * op.hidden, opx * op.hidden * 18.0, [&] {
+        return launch_dw(dt, h1, ptr<float>(c, op.w1), ptr<float>(c, op.b1), h2, B, h, w, (int)op.hidden,
+                         (int)op.stride, OH, OW, s);
+      }));
+      const bool res = op.flags & 1u;
+      void* y = res ? pick({x, h2}) : pick({h2});
+      const int64_t M2 = (int64_t)B * OH * OW;
+      HIP_TRY(prof_launch(c, s, pw_key(dt, res ? EPI_RES : EPI_NONE, op.cout), pw_bytes(M2, op.hidden, op.cout, res),
+                          2.0 * M2 * op.hidden * op.cout, [&] {
+        return launch_pw(dt, res ? EPI_RES : EPI_NONE, h2, ptr<void>(c, op.w2), ptr<float>(c, op.b2),
+                         res ? x : nullptr, y, M2, (int)op.hidden, (int)op.cout, s);
+      }));
+      cur = y;
+      h = OH;
+      w = OW;
+      ch = (int)op.cout;
+    } else if (op.kind == OP_LAST) {
+      if (mode == 0) {
+        const double M3 = (double)B * h * w;
+        HIP_TRY(prof_launch(c, s, "pw_pool_kernel<4>",
+                            M3 * op.cin * 2 + (double)op.cout * (op.cin * 2 + 4) + (double)B * op.cout * 4,
+                            2.0 * M3 * op.cin * op.cout, [&] {
+          return launch_pw_pool(dt, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), c->pooled, B, h * w,
+                                (int)op.cin, (int)op.cout, s);
+        }));
+      } else if (mode == 2) {
+        void* y = pick({cur});
+        HIP_TRY(launch_pw(dt, EPI_RELU, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, y,
+                          (int64_t)B * h * w, (int)op.cin, (int)op.cout, s));
+        cur = y;
+        ch = (int)op.cout;
+      }
+      break;
+    }
+    if (mode == 1 && op_index == stop) break;
+    ++op_index;
+  }
+  if (out_buf) *out_buf = cur;
+  if (oc) *oc = ch;
+  if (oh) *oh = h;
+  if (ow) *ow = w;
+  return SPEF_OK;
+}
+
+void free_workspace(spef_ctx* c) {
+  for (void*& b : c->buf) {
+    if (b) hipFree(b);
+    b = nullptr;
+  }
+  if (c->pooled) hipFree(c->pooled);
+  c->pooled = nullptr;
+  c->ws_B = c->ws_H = c->ws_W = 0;
+  c->buf_bytes = 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int spef_abi_version(void) { return SPEF_ABI_VERSION; }
+
+const char* spef_last_error(void) { return g_err.c_str(); }
+
+int spef_init(int device, spef_ctx** out) {
+  if (!out) return fail(SPEF_ERR_ARG, "out is null");
+  int n = 0;
+  HIP_TRY(hipGetDeviceCount(&n));
+  if (device < 0 || device >= n) return fail(SPEF_ERR_ARG, "device index out of range");
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, device));
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(SPEF_ERR_ARG, std::string("SPEF kernels are built for gfx950 only, device is ") + prop.gcnArchName);
+  spef_ctx* c = new spef_ctx();
+  c->device = device;
+  *out = c;
+  return SPEF_OK;
+}
+
+int spef_destroy(spef_ctx* c) {
+  if (!c) return SPEF_OK;
+  Dev d(c->device);
+  free_workspace(c);
+  if (c->d_data) hipFree(c->d_data);
+  if (c->d_ori_bins) hipFree(c->d_ori_bins);
+  if (c->d_pos_grid) hipFree(c->d_pos_grid);
+  for (hipEvent_t e : c->pool) hipEventDestroy(e);
+  delete c;
+  return SPEF_OK;
+}
+
+static int parse_blob(spef_ctx* c, const uint8_t* head_bytes, size_t bytes) {
+  if (bytes < sizeof(BlobHeader)) return fail(SPEF_ERR_BLOB, "blob too small");
+  BlobHeader h;
+  memcpy(&h, head_bytes, sizeof(h));
+  if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_BLOB, "bad blob magic");
+  if (h.version != kBlobVersion) return fail(SPEF_ERR_BLOB, "unsupported blob version");
+  if (h.dtype != DT_F16 && h.dtype != DT_BF16) return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
+  if (h.ops_off + (uint64_t)h.n_ops * sizeof(OpDesc) > bytes || h.data_off + h.data_bytes > bytes)
+    return fail(SPEF_ERR_BLOB, "blob truncated");
+  std::vector<OpDesc> ops(h.n_ops);
+  memcpy(ops.data(), head_bytes + h.ops_off, h.n_ops * sizeof(OpDesc));
+  for (const OpDesc& op : ops) {
+    for (uint64_t off : {op.w0, op.b0, op.w1, op.b1, op.w2, op.b2})
+      if (off != kAbsent && (off >= h.data_bytes || (off & 15)))
+        return fail(SPEF_ERR_BLOB, "tensor offset out of range / misaligned");
+    if (op.kind == OP_IRB && (op.cin % 8 || op.cout % 8 || op.hidden % 8 || (op.stride != 1 && op.stride != 2)))
+      return fail(SPEF_ERR_BLOB, "unsupported inverted-residual geometry");
+  }
+  c->hdr = h;
+  c->ops = std::move(ops);
+  return SPEF_OK;
+}
+
+static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_device) {
+  if (!c || !blob) return fail(SPEF_ERR_ARG, "null argument");
+  Dev d(c->device);
+  std::vector<uint8_t> head;
+  const uint8_t* hb;
+  if (on_device) {
+    // header + op table live in the first bytes; fetch them to the host
+    BlobHeader h;
+    HIP_TRY(hipMemcpy(&h, blob, sizeof(h), hipMemcpyDeviceToHost));
+    const size_t meta = std::min<size_t>(bytes, (size_t)h.data_off);
+    head.resize(std::max<size_t>(meta, sizeof(h)));
+    HIP_TRY(hipMemcpy(head.data(), blob, head.size(), hipMemcpyDeviceToHost));
+    hb = head.data();
+    int rc = parse_blob(c, hb, bytes);
+    if (rc) return rc;
+  } else {
+    hb = (const uint8_t*)blob;
+    int rc = parse_blob(c, hb, bytes);
+    if (rc) return rc;
+  }
+  if (c->d_data) hipFree(c->d_data);
+  c->d_data = nullptr;
+  HIP_TRY(hipMalloc(&c->d_data, c->hdr.data_bytes));
+  const uint8_t* src = (const uint8_t*)blob + c->hdr.data_off;
+  HIP_TRY(hipMemcpy(c->d_data, src, c->hdr.data_bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+  c->data_bytes = c->hdr.data_bytes;
+  c->loaded = true;
+  free_workspace(c);
+  return SPEF_OK;
+}
+
+int spef_load_weights(spef_ctx* c, const void* blob, size_t bytes) { return load_common(c, blob, bytes, false); }
+
+int spef_load_weights_device(spef_ctx* c, const void* blob, size_t bytes) { return load_common(c, blob, bytes, true); }
+
+int spef_model_info(const spef_ctx* c, int* head, int* n_out0, int* n_out1, int* dtype, int* n_ops) {
+  if (!c || !c->loaded) return fail(SPEF_ERR_STATE, "weights not loaded");
+  if (head) *head = (int)c->hdr.head;
+  if (n_out0) *n_out0 = (int)c->hdr.n_out0;
+  if (n_out1) *n_out1 = (int)c->hdr.n_out1;
+  if (dtype) *dtype = (int)c->hdr.dtype;
+  if (n_ops) *n_ops = (int)c->ops.size();
+  return SPEF_OK;
+}
+
+int spef_reserve(spef_ctx* c, int B, int H, int W) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  if (!c->loaded) return fail(SPEF_ERR_STATE, "weights not loaded");
+  if (B <= 0 || H < 32 || W < 32) return fail(SPEF_ERR_ARG, "bad shape");
+  if (B <= c->ws_B && H == c->ws_H && W == c->ws_W) return SPEF_OK;
+  Dev d(c->device);
+  int fh = 0, fw = 0;
+  const int64_t per_img = max_act_elems(c, H, W, &fh, &fw);
+  if (c->hdr.head == HEAD_KEYPOINTS && (fh != (int)c->hdr.kp_fh || fw != (int)c->hdr.kp_fw))
+    return fail(SPEF_ERR_ARG, "keypoint head expects a fixed feature map size (keypoints.py:20)");
+  free_workspace(c);
+  const size_t bytes = (size_t)per_img * B * elem_size(c) + 256;
+  for (void*& b : c->buf) HIP_TRY(hipMalloc(&b, bytes));
+  HIP_TRY(hipMalloc(&c->pooled, (size_t)B * c->hdr.feat_c * sizeof(float)));
+  c->buf_bytes = bytes;
+  c->ws_B = B;
+  c->ws_H = H;
+  c->ws_W = W;
+  return SPEF_OK;
+}
+
+int spef_forward(spef_ctx* c, const void* input, int layout, int B, int H, int W, float* out0, float* out1,
+                 void* stream) {
+  int rc = check_ready(c, B, H, W);
+  if (rc) return rc;
+  if (!input || !out0) return fail(SPEF_ERR_ARG, "null input/output");
+  if (layout != SPEF_IN_U8_NHWC && layout != SPEF_IN_F32_NCHW) return fail(SPEF_ERR_ARG, "bad layout");
+  Dev d(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  if (c->hdr.head == HEAD_URSONET) {
+    if (!out1 && c->hdr.n_out1) return fail(SPEF_ERR_ARG, "null position output");
+    rc = run_backbone(c, input, layout, B, H, W, s, 0, -1, nullptr, nullptr, nullptr, nullptr);
+    if (rc) return rc;
+    for (const OpDesc& op : c->ops)
+      if (op.kind == OP_FC)
+        HIP_TRY(prof_launch(c, s, "fc_kernel", ((double)B + op.cout) * op.cin * 4 + (double)B * op.cout * 4,
+                            2.0 * B * op.cin * op.cout, [&] {
+          return launch_fc(c->pooled, ptr<float>(c, op.w0), ptr<float>(c, op.b0), out0, (int)c->hdr.n_out0, out1,
+                           (int)c->hdr.n_out1, B, (int)c->hdr.feat_c, s);
+        }));
+    return SPEF_OK;
+  }
+  // keypoint head: flatten of the (unpooled) 1280 x fh x fw map, then one Linear
+  void* feat = nullptr;
+  int fc_ = 0, fh = 0, fw = 0;
+  rc = run_backbone(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw);
+  if (rc) return rc;
+  (void)feat;
+  return fail(SPEF_ERR_STATE, "keypoint head not implemented in this build");
+}
+
+int spef_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W, float* features, void* stream) {
+  int rc = check_ready(c, B, H, W);
+  if (rc) return rc;
+  if (!input || !features) return fail(SPEF_ERR_ARG, "null input/output");
+  Dev d(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  void* feat = nullptr;
+  int fc_ = 0, fh = 0, fw = 0;
+  rc = run_backbone(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw);
+  if (rc) return rc;
+  HIP_TRY(launch_to_f32((int)c->hdr.dtype, feat, features, (int64_t)B * fh * fw * fc_, s));
+  return SPEF_OK;
+}
+
+int spef_probe(spef_ctx* c, const void* input, int layout, int B, int H, int W, int stop_op, float* out, int* oc,
+               int* oh, int* ow, void* stream) {
+  int rc = check_ready(c, B, H, W);
+  if (rc) return rc;
+  if (!input || !out) return fail(SPEF_ERR_ARG, "null input/output");
+  Dev d(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  void* act = nullptr;
+  int ch = 0, h = 0, w = 0;
+  rc = run_backbone(c, input, layout, B, H, W, s, 1, stop_op, &act, &ch, &h, &w);
+  if (rc) return rc;
+  HIP_TRY(launch_to_f32((int)c->hdr.dtype, act, out, (int64_t)B * h * w * ch, s));
+  if (oc) *oc = ch;
+  if (oh) *oh = h;
+  if (ow) *ow = w;
+  return SPEF_OK;
+}
+
+int spef_set_decode_tables(spef_ctx* c, const double* ori_bins, int n_ori_bins, const double* pos_grid,
+                           int n_pos_bins) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  Dev d(c->device);
+  if (c->d_ori_bins) hipFree(c->d_ori_bins);
+  if (c->d_pos_grid) hipFree(c->d_pos_grid);
+  c->d_ori_bins = nullptr;
+  c->d_pos_grid = nullptr;
+  c->n_ori_bins = c->n_pos_bins = 0;
+  if (ori_bins && n_ori_bins > 0) {
+    HIP_TRY(hipMalloc(&c->d_ori_bins, sizeof(double) * 4 * n_ori_bins));
+    HIP_TRY(hipMemcpy(c->d_ori_bins, ori_bins, sizeof(double) * 4 * n_ori_bins, hipMemcpyHostToDevice));
+    c->n_ori_bins = n_ori_bins;
+  }
+  if (pos_grid && n_pos_bins > 0) {
+    HIP_TRY(hipMalloc(&c->d_pos_grid, sizeof(double) * 3 * n_pos_bins));
+    HIP_TRY(hipMemcpy(c->d_pos_grid, pos_grid, sizeof(double) * 3 * n_pos_bins, hipMemcpyHostToDevice));
+    c->n_pos_bins = n_pos_bins;
+  }
+  return SPEF_OK;
+}
+
+int spef_decode(spef_ctx* c, int ori_mode, int pos_mode, const float* ori_raw, const float* pos_raw, int B,
+                float* ori_soft, float* quat, float* pos_soft, float* pos, int* status, void* stream) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  if (B <= 0 || !ori_raw || !quat || !pos_raw || !pos || !status) return fail(SPEF_ERR_ARG, "null argument");
+  Dev d(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemsetAsync(status, 0, sizeof(int) * B, s));
+  if (ori_mode == SPEF_CLASSIFICATION) {
+    if (!c->d_ori_bins) return fail(SPEF_ERR_STATE, "orientation bins not set (spef_set_decode_tables)");
+    HIP_TRY(launch_decode_ori(ori_raw, B, c->n_ori_bins, c->d_ori_bins, ori_soft, quat, status, s));
+  } else if (ori_mode == SPEF_REGRESSION) {
+    HIP_TRY(launch_normalize_ori(ori_raw, B, quat, s));
+  } else {
+    return fail(SPEF_ERR_ARG, "ori_mode must be regression or classification");
+  }
+  if (pos_mode == SPEF_CLASSIFICATION) {
+    if (!c->d_pos_grid) return fail(SPEF_ERR_STATE, "position grid not set (spef_set_decode_tables)");
+    HIP_TRY(launch_decode_pos(pos_raw, B, c->n_pos_bins, c->d_pos_grid, pos_soft, pos, status, s));
+  } else if (pos_mode == SPEF_REGRESSION) {
+    if (pos != pos_raw) HIP_TRY(hipMemcpyAsync(pos, pos_raw, sizeof(float) * 3 * B, hipMemcpyDeviceToDevice, s));
+  } else {
+    return fail(SPEF_ERR_ARG, "pos_mode must be regression or classification");
+  }
+  return SPEF_OK;
+}
+
+int spef_profile_begin(spef_ctx* c) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  c->recs.clear();
+  c->pool_next = 0;
+  c->profiling = true;
+  return SPEF_OK;
+}
+
+int spef_profile_end(spef_ctx* c, char* buf, size_t cap, size_t* needed) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  Dev d(c->device);
+  c->profiling = false;
+  // aggregate per kernel key: launches, total ms, algorithmic bytes, flops
+  struct Agg {
+    long n = 0;
+    double ms = 0, bytes = 0, flops = 0;
+  };
+  std::vector<std::pair<std::string, Agg>> agg;
+  for (auto& r : c->recs) {
+    HIP_TRY(hipEventSynchronize(r.b));
+    float ms = 0.f;
+    HIP_TRY(hipEventElapsedTime(&ms, r.a, r.b));
+    Agg* a = nullptr;
+    for (auto& kv : agg)
+      if (kv.first == r.key) a = &kv.second;
+    if (!a) {
+      agg.push_back({r.key, Agg{}});
+      a = &agg.back().second;
+    }
+    a->n += 1;
+    a->ms += ms;
+    a->bytes += r.bytes;
+    a->flops += r.flops;
+  }
+  std::string js = "{";
+  char tmp[512];
+  for (size_t i = 0; i < agg.size(); ++i) {
+    snprintf(tmp, sizeof(tmp), "%s\"%s\": [%ld, %.6f, %.1f, %.1f]", i ? ", " : "", agg[i].first.c_str(),
+             agg[i].second.n, agg[i].second.ms, agg[i].second.bytes, agg[i].second.flops);
+    js += tmp;
+  }
+  js += "}";
+  c->recs.clear();
+  c->pool_next = 0;
+  if (needed) *needed = js.size() + 1;
+  if (buf && cap > 0) {
+    const size_t n = std::min(cap - 1, js.size());
+    memcpy(buf, js.data(), n);
+    buf[n] = 0;
+    if (n < js.size()) return fail(SPEF_ERR_ARG, "profile buffer too small");
+  }
+  return SPEF_OK;
+}
+
+}  // extern "C"

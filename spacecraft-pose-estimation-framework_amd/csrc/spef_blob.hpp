@@ -1,0 +1,44 @@
+// Weight blob layout (little endian), written by spef_amd/blob.py -- keep the two in sync.
+//
+//   [BlobHeader 128 B][OpDesc 128 B x n_ops][pad to 256][data section: 256-B aligned tensors]
+//
+// Ops (reference module -> op):
+//   OP_STEM  ConvBnAct 3->32 s2 (mobilenet_v2.py:252-254)   w0 fp32 [27][32] (k=ky*9+kx*3+ci), b0 fp32 [32]
+//   OP_IRB   InvertedResidual (pytorch_layers.py:65-98)       w0/b0 expand 1x1: act [Np][Kp], fp32 [Np] (absent if t==1)
+//                                                             w1/b1 depthwise: fp32 [9][hidden], fp32 [hidden]
+//                                                             w2/b2 project 1x1: act [Np][Kp], fp32 [Np]
+//   OP_LAST  ConvBnAct 320->1280 1x1 (mobilenet_v2.py:264)    w0 act [Np][Kp], b0 fp32 [Np]
+//   OP_FC    URSONetHead ori|pos Linear (ursonet.py:17-25)    w0 fp32 [Np][1280] rows = ori then pos, b0 fp32 [Np]
+//   OP_FCKP  KeypointRegressionHead (keypoints.py:18-21)      w0 fp32 [Np][F] columns in NHWC flatten order
+// act = the activation storage type (fp16 or bf16); Kp = K rounded up to 32, Np = N rounded up to 16, padding 0.
+// BatchNorm (eps 1e-5) is folded: w' = w*g/sqrt(v+eps), b' = beta - mean*g/sqrt(v+eps).
+#pragma once
+#include <stdint.h>
+
+namespace spef {
+
+static const char kBlobMagic[8] = {'S', 'P', 'E', 'F', 'M', 'I', '3', '5'};
+static const uint32_t kBlobVersion = 1;
+static const uint64_t kAbsent = ~0ull;
+
+enum OpKind : uint32_t { OP_STEM = 1, OP_IRB = 2, OP_LAST = 3, OP_FC = 4, OP_FCKP = 5 };
+enum HeadKind : uint32_t { HEAD_URSONET = 0, HEAD_KEYPOINTS = 1 };
+
+#pragma pack(push, 1)
+struct BlobHeader {
+  char magic[8];
+  uint32_t version, dtype, head, n_ops;
+  uint32_t n_out0, n_out1, feat_c, kp_fh, kp_fw, pad0;
+  uint64_t ops_off, data_off, data_bytes;
+  uint8_t reserved[56];
+};
+struct OpDesc {
+  uint32_t kind, cin, cout, hidden, stride, expand, flags, pad0;
+  uint64_t w0, b0, w1, b1, w2, b2;
+  uint8_t reserved[48];
+};
+#pragma pack(pop)
+static_assert(sizeof(BlobHeader) == 128, "BlobHeader must be 128 bytes");
+static_assert(sizeof(OpDesc) == 128, "OpDesc must be 128 bytes");
+
+}  // namespace spef

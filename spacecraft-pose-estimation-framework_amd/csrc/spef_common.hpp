@@ -1,0 +1,73 @@
+// Shared device helpers for the SPEF MI355X (gfx950 / CDNA4) kernels.
+//
+// Storage types: activations are NHWC, fp16 (parity default) or bf16, 16-B aligned per pixel row
+// (every channel count on the path is a multiple of 8). Accumulation is always fp32 (MFMA f32 C/D).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace spef {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// Element-type traits: the MFMA used for a 16x16 output tile with K = 32 per instruction.
+// gfx950 lane map (cdna_hip_programming.md §3): A[i = l&15][k = 8(l>>4)+e], B[k = 8(l>>4)+e][j = l&15],
+// D[i = 4(l>>4)+r][j = l&15].
+struct F16 {
+  using T = _Float16;
+  using x8 = f16x8;
+  using x4 = f16x4;
+  static __device__ __forceinline__ f32x4 mfma(x8 a, x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+};
+struct BF16 {
+  using T = __bf16;
+  using x8 = bf16x8;
+  using x4 = bf16x4;
+  static __device__ __forceinline__ f32x4 mfma(x8 a, x8 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+};
+
+template <typename DT>
+__device__ __forceinline__ typename DT::x8 load8(const typename DT::T* p) {
+  return *reinterpret_cast<const typename DT::x8*>(p);
+}
+template <typename DT>
+__device__ __forceinline__ typename DT::x8 zero8() {
+  typename DT::x8 z;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) z[e] = (typename DT::T)0.0f;
+  return z;
+}
+
+// Bijective XCD-aware remap of a 1-D workgroup id (cdna_hip_programming.md §5, "XCD swizzle must be
+// bijective"): consecutive logical ids land on one XCD (blocks b and b+8 share an XCD under the
+// observed round-robin placement). Speed only -- correctness never depends on placement.
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t bid, uint32_t nwg) {
+  const uint32_t q = nwg >> 3, r = nwg & 7, xcd = bid & 7, off = bid >> 3;
+  return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + off;
+}
+
+__device__ __forceinline__ float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+__device__ __forceinline__ double warp_sum_d(double v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+}  // namespace spef

@@ -1,0 +1,46 @@
+// Host-side launchers of the SPEF HIP kernels (internal; the public C ABI is include/spef.h).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace spef {
+
+enum Dtype : int { DT_F16 = 1, DT_BF16 = 2 };
+enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2 };
+enum InLayout : int { IN_U8_NHWC = 0, IN_F32_NCHW = 1 };
+
+// Stem ConvBnAct 3->32, 3x3, stride 2, pad 1, BN folded, ReLU. W: fp32 [27][32] (k = ky*9+kx*3+ci).
+hipError_t launch_stem(int dtype, int in_layout, const void* in, const float* w, const float* bias, void* y,
+                       int B, int H, int W, int OH, int OW, hipStream_t s);
+
+// Pointwise 1x1 conv as C^T = W * X^T on MFMA: X [M][K] NHWC, Wt [Np][Kp] (zero padded), bias fp32 [Np],
+// optional residual R [M][N]; Y [M][N].
+hipError_t launch_pw(int dtype, int epi, const void* x, const void* wt, const float* bias, const void* r,
+                     void* y, int64_t M, int K, int N, hipStream_t s);
+
+// Depthwise 3x3 conv, pad 1, stride 1|2, BN folded, ReLU. W9: fp32 [9][C], bias fp32 [C].
+hipError_t launch_dw(int dtype, const void* x, const float* w9, const float* bias, void* y, int B, int H, int W,
+                     int C, int stride, int OH, int OW, hipStream_t s);
+
+// Last 1x1 conv (+BN, ReLU) fused with the global mean over HW: pooled fp32 [B][N].
+hipError_t launch_pw_pool(int dtype, const void* x, const void* wt, const float* bias, float* pooled, int B,
+                          int HW, int K, int N, hipStream_t s);
+
+// fp32 head GEMM (f32-input MFMA): out[b][i] = sum_k X[b][k] W[i][k] + bias[i], columns [0,n0) -> out0,
+// [n0, n0+n1) -> out1. W fp32 [Np][K], K % 16 == 0.
+hipError_t launch_fc(const float* x, const float* w, const float* bias, float* out0, int n0, float* out1, int n1,
+                     int B, int K, hipStream_t s);
+
+// Activation dtype -> fp32 NHWC copy (debug probes / backbone feature export).
+hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStream_t s);
+
+// Decode (src/spe/spe_utils.py:56-101): ori softmax + Markley average; pos softmax + soft-argmax.
+// status[b] |= 1 (NaN orientation moments), 2 (pos zero sum), 4 (NaN position).
+hipError_t launch_decode_ori(const float* logits, int B, int n_bins, const double* q_bins, float* soft,
+                             float* quat, int* status, hipStream_t s);
+hipError_t launch_normalize_ori(const float* raw, int B, float* quat, hipStream_t s);
+hipError_t launch_decode_pos(const float* logits, int B, int n_bins, const double* grid, float* soft,
+                             float* pos, int* status, hipStream_t s);
+
+}  // namespace spef

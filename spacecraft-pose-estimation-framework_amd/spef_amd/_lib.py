@@ -1,0 +1,74 @@
+"""ctypes binding of the C ABI in include/spef.h (libspef_mi355x.so, built in-tree by _build.py).
+
+There is no CPU fallback: if the library is missing or fails to load, importing the product path raises.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+from . import _build
+
+OK, ERR_ARG, ERR_HIP, ERR_BLOB, ERR_STATE, ERR_NUMERIC = range(6)
+IN_U8_NHWC, IN_F32_NCHW = 0, 1
+REGRESSION, CLASSIFICATION, KEYPOINTS = 0, 1, 2
+
+# name -> (restype, argtypes); keep in sync with include/spef.h (tests/test_abi.py checks the header)
+_vp, _i, _sz = C.c_void_p, C.c_int, C.c_size_t
+_ip = C.POINTER(C.c_int)
+SIGNATURES = {
+    'spef_abi_version': (_i, []),
+    'spef_last_error': (C.c_char_p, []),
+    'spef_init': (_i, [_i, C.POINTER(_vp)]),
+    'spef_destroy': (_i, [_vp]),
+    'spef_load_weights': (_i, [_vp, _vp, _sz]),
+    'spef_load_weights_device': (_i, [_vp, _vp, _sz]),
+    'spef_model_info': (_i, [_vp, _ip, _ip, _ip, _ip, _ip]),
+    'spef_reserve': (_i, [_vp, _i, _i, _i]),
+    'spef_forward': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
+    'spef_backbone': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
+    'spef_probe': (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _ip, _ip, _ip, _vp]),
+    'spef_set_decode_tables': (_i, [_vp, _vp, _i, _vp, _i]),
+    'spef_decode': (_i, [_vp, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'spef_profile_begin': (_i, [_vp]),
+    'spef_profile_end': (_i, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),
+}
+
+
+class SpefError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f'[spef error {code}] {msg}')
+        self.code = code
+
+
+_LIB = None
+
+
+def load(path: str | None = None) -> C.CDLL:
+    """Load (once) and return the HIP library; raises if it is absent -- never falls back."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    path = path or _build.lib_path()
+    if not os.path.exists(path):
+        raise ImportError(f'SPEF HIP library not built: {path} (run __graft_entry__.build() or '
+                          f'python -m spef_amd._build)')
+    lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
+    for name, (res, args) in SIGNATURES.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    if lib.spef_abi_version() != 1:
+        raise ImportError('SPEF ABI version mismatch')
+    _LIB = lib
+    return lib
+
+
+def check(rc: int) -> None:
+    if rc != OK:
+        msg = _LIB.spef_last_error().decode(errors='replace') if _LIB else ''
+        if rc == ERR_NUMERIC:
+            raise ValueError(msg)
+        if rc == ERR_ARG:
+            raise AssertionError(msg)
+        raise SpefError(rc, msg)

@@ -1,0 +1,168 @@
+"""BatchNorm folding and weight packing: reference ``state_dict`` -> SPEF MI355X weight blob.
+
+Input is the reference checkpoint layout (``save_model`` / ``load_state_dict``,
+``src/modeling/model.py:70-89, 261-266``; 316 keys for MobileNetV2 + URSONetHead). Output is the
+binary blob ``csrc/spef_blob.hpp`` documents -- keep the two in sync.
+
+Folding (eval-mode ``BatchNorm2d``, eps 1e-5, ``pytorch_layers.py:53-56``), done in float64:
+    s  = gamma / sqrt(running_var + eps)
+    w' = w * s[:, None, None, None]         b' = beta - running_mean * s
+Pointwise weights are stored [Np][Kp] in the activation dtype (fp16 default, bf16 variant), zero padded
+(Kp = K up to a multiple of 32, Np = N up to a multiple of 16) so the MFMA kernels never mask weight loads.
+Stem, depthwise, bias and head weights stay fp32.
+"""
+from __future__ import annotations
+
+import struct
+from typing import Dict, List, Optional
+
+import numpy as np
+
+from .arch import Arch, BN_EPS, ConvSpec, LAST_CHANNELS, mobilenet_v2
+
+MAGIC = b'SPEFMI35'
+VERSION = 1
+DTYPES = {'fp16': 1, 'bf16': 2}
+OP_STEM, OP_IRB, OP_LAST, OP_FC, OP_FCKP = 1, 2, 3, 4, 5
+HEAD_URSONET, HEAD_KEYPOINTS = 0, 1
+ABSENT = (1 << 64) - 1
+_HDR = struct.Struct('<8sIIII' + 'IIIIII' + 'QQQ' + '56s')
+_OP = struct.Struct('<IIIIIIII' + 'QQQQQQ' + '48s')
+assert _HDR.size == 128 and _OP.size == 128
+
+
+def _np(v) -> np.ndarray:
+    if hasattr(v, 'detach'):
+        v = v.detach().cpu().numpy()
+    return np.asarray(v)
+
+
+def fold_bn(sd: Dict, c: ConvSpec):
+    """-> (w' float64 [cout, cin/g, k, k], b' float64 [cout])."""
+    w = _np(sd[f'{c.prefix}.0.weight']).astype(np.float64)
+    g = _np(sd[f'{c.prefix}.1.weight']).astype(np.float64)
+    beta = _np(sd[f'{c.prefix}.1.bias']).astype(np.float64)
+    mean = _np(sd[f'{c.prefix}.1.running_mean']).astype(np.float64)
+    var = _np(sd[f'{c.prefix}.1.running_var']).astype(np.float64)
+    s = g / np.sqrt(var + BN_EPS)
+    return w * s[:, None, None, None], beta - mean * s
+
+
+def _to_act(a: np.ndarray, dtype: str) -> bytes:
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if dtype == 'fp16':
+        return a.astype(np.float16).tobytes()
+    # bf16: round-to-nearest-even on the fp32 bits (finite weights only)
+    u = a.view(np.uint32).astype(np.uint64)
+    r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
+    return r.tobytes()
+
+
+class _Data:
+    def __init__(self):
+        self.chunks: List[bytes] = []
+        self.size = 0
+
+    def add(self, b: bytes) -> int:
+        off = self.size
+        pad = (-len(b)) % 256
+        self.chunks.append(b + b'\0' * pad)
+        self.size += len(b) + pad
+        return off
+
+
+def _pw_tensor(w: np.ndarray, b: np.ndarray, dtype: str, data: _Data):
+    cout, cin = w.shape[0], w.shape[1]
+    kp, np_ = (cin + 31) // 32 * 32, (cout + 15) // 16 * 16
+    wp = np.zeros((np_, kp), np.float32)
+    wp[:cout, :cin] = w[:, :, 0, 0]
+    bp = np.zeros(np_, np.float32)
+    bp[:cout] = b
+    return data.add(_to_act(wp, dtype)), data.add(bp.tobytes())
+
+
+def _dw_tensor(w: np.ndarray, b: np.ndarray, data: _Data):
+    c = w.shape[0]
+    w9 = np.ascontiguousarray(w[:, 0].reshape(c, 9).T, dtype=np.float32)   # [9][C], tap = ky*3+kx
+    return data.add(w9.tobytes()), data.add(np.asarray(b, np.float32).tobytes())
+
+
+def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=(8, 12)) -> bytes:
+    """Fold BN and pack a reference-layout state_dict into a blob (bytes)."""
+    assert dtype in DTYPES, dtype
+    arch = arch or mobilenet_v2()
+    data = _Data()
+    ops = []
+
+    # stem: [27][32], k = ky*9 + kx*3 + ci
+    w, b = fold_bn(sd, arch.stem)
+    ws = np.ascontiguousarray(w.transpose(2, 3, 1, 0).reshape(27, arch.stem.cout), dtype=np.float32)
+    ops.append((OP_STEM, 3, arch.stem.cout, 0, 2, 1, 0,
+                data.add(ws.tobytes()), data.add(np.asarray(b, np.float32).tobytes()), ABSENT, ABSENT, ABSENT, ABSENT))
+
+    for blk in arch.blocks:
+        convs = list(blk.convs)
+        e = (ABSENT, ABSENT)
+        if blk.expand != 1:
+            e = _pw_tensor(*fold_bn(sd, convs.pop(0)), dtype, data)
+        d = _dw_tensor(*fold_bn(sd, convs[0]), data)
+        p = _pw_tensor(*fold_bn(sd, convs[1]), dtype, data)
+        ops.append((OP_IRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, 1 if blk.residual else 0,
+                    e[0], e[1], d[0], d[1], p[0], p[1]))
+
+    lw, lb = _pw_tensor(*fold_bn(sd, arch.last), dtype, data)
+    ops.append((OP_LAST, arch.last.cin, arch.last.cout, 0, 1, 1, 0, lw, lb, ABSENT, ABSENT, ABSENT, ABSENT))
+
+    if arch.head == 'ursonet':
+        wo, bo = _np(sd['head.ori.1.weight']), _np(sd['head.ori.1.bias'])
+        wpos, bpos = _np(sd['head.pos.0.weight']), _np(sd['head.pos.0.bias'])
+        n = wo.shape[0] + wpos.shape[0]
+        np_ = (n + 15) // 16 * 16
+        wf = np.zeros((np_, LAST_CHANNELS), np.float32)
+        wf[:wo.shape[0]] = wo
+        wf[wo.shape[0]:n] = wpos
+        bf = np.zeros(np_, np.float32)
+        bf[:wo.shape[0]] = bo
+        bf[wo.shape[0]:n] = bpos
+        ops.append((OP_FC, LAST_CHANNELS, n, 0, 1, 1, 0, data.add(wf.tobytes()), data.add(bf.tobytes()),
+                    ABSENT, ABSENT, ABSENT, ABSENT))
+        head, n0, n1, fh, fw = HEAD_URSONET, wo.shape[0], wpos.shape[0], 0, 0
+    else:
+        fh, fw = kp_feat_hw
+        wk, bk = _np(sd['head.layer.1.weight']), _np(sd['head.layer.1.bias'])
+        n = wk.shape[0]
+        assert wk.shape[1] == LAST_CHANNELS * fh * fw, 'keypoint head size / feature map mismatch'
+        # torch.flatten of NCHW (keypoints.py:25) -> our NHWC flatten order
+        wn = wk.reshape(n, LAST_CHANNELS, fh, fw).transpose(0, 2, 3, 1).reshape(n, -1)
+        np_ = (n + 15) // 16 * 16
+        wf = np.zeros((np_, wn.shape[1]), np.float32)
+        wf[:n] = wn
+        bf = np.zeros(np_, np.float32)
+        bf[:n] = bk
+        ops.append((OP_FCKP, wn.shape[1], n, 0, 1, 1, 0, data.add(wf.tobytes()), data.add(bf.tobytes()),
+                    ABSENT, ABSENT, ABSENT, ABSENT))
+        head, n0, n1 = HEAD_KEYPOINTS, n, 0
+
+    ops_off = _HDR.size
+    data_off = ops_off + _OP.size * len(ops)
+    data_off += (-data_off) % 256
+    hdr = _HDR.pack(MAGIC, VERSION, DTYPES[dtype], head, len(ops), n0, n1, LAST_CHANNELS, fh, fw, 0,
+                    ops_off, data_off, data.size, b'\0' * 56)
+    out = bytearray(hdr)
+    for o in ops:
+        out += _OP.pack(*o[:7], 0, *o[7:], b'\0' * 48)
+    out += b'\0' * (data_off - len(out))
+    for ch in data.chunks:
+        out += ch
+    return bytes(out)
+
+
+def describe(blob: bytes) -> dict:
+    """Parse a blob header + op table (for tests and tooling)."""
+    h = _HDR.unpack_from(blob, 0)
+    if h[0] != MAGIC:
+        raise ValueError('not a SPEF MI355X blob')
+    info = dict(version=h[1], dtype=h[2], head=h[3], n_ops=h[4], n_out0=h[5], n_out1=h[6], feat_c=h[7],
+                kp_fh=h[8], kp_fw=h[9], ops_off=h[11], data_off=h[12], data_bytes=h[13])
+    info['ops'] = [_OP.unpack_from(blob, info['ops_off'] + i * _OP.size)[:14] for i in range(info['n_ops'])]
+    return info

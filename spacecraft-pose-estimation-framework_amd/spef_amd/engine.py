@@ -1,0 +1,150 @@
+"""Device-side engine: one SPEF context (one GPU) driven through the C ABI.
+
+PyTorch-ROCm is plumbing here: it owns device memory (output tensors) and the current HIP stream;
+every computation is a HIP kernel in libspef_mi355x.so.
+"""
+from __future__ import annotations
+
+import ctypes as C
+from typing import Optional, Tuple
+
+import numpy as np
+import torch
+
+from . import _lib as L
+
+
+def _ptr(t: Optional[torch.Tensor]):
+    return None if t is None else C.c_void_p(t.data_ptr())
+
+
+def _stream(device: torch.device):
+    return C.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Engine:
+    """Loaded weights + workspace on one GPU.
+
+    ``forward`` maps NHWC uint8 frames (or the reference's NCHW float32 [0,1] tensor) to the raw head
+    outputs; ``decode`` applies SPEUtils.last_activ + decode on the device.
+    """
+
+    def __init__(self, blob: bytes | torch.Tensor, device: int | str | torch.device = 0):
+        self.lib = L.load()
+        self.device = torch.device(device if not isinstance(device, int) else f'cuda:{device}')
+        if self.device.type != 'cuda':
+            raise AssertionError('SPEMi355x runs on a HIP device only (no CPU fallback)')
+        idx = self.device.index or 0
+        h = C.c_void_p()
+        L.check(self.lib.spef_init(idx, C.byref(h)))
+        self.ctx = h
+        self.load(blob)
+        self._reserved = (0, 0, 0)
+        self._decode_tables = None
+
+    # ------------------------------------------------------------------ weights
+    def load(self, blob: bytes | torch.Tensor) -> None:
+        if isinstance(blob, torch.Tensor):
+            assert blob.is_cuda and blob.dtype == torch.uint8 and blob.is_contiguous()
+            L.check(self.lib.spef_load_weights_device(self.ctx, C.c_void_p(blob.data_ptr()), blob.numel()))
+        else:
+            buf = C.create_string_buffer(bytes(blob), len(blob))
+            L.check(self.lib.spef_load_weights(self.ctx, buf, len(blob)))
+        head, n0, n1, dt, nops = (C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_int())
+        L.check(self.lib.spef_model_info(self.ctx, C.byref(head), C.byref(n0), C.byref(n1), C.byref(dt),
+                                         C.byref(nops)))
+        self.head, self.n_out0, self.n_out1 = head.value, n0.value, n1.value
+        self.dtype = {1: 'fp16', 2: 'bf16'}[dt.value]
+        self.n_ops = nops.value
+        self._reserved = (0, 0, 0)
+
+    def reserve(self, B: int, H: int, W: int) -> None:
+        rb, rh, rw = self._reserved
+        if B <= rb and (H, W) == (rh, rw):
+            return
+        L.check(self.lib.spef_reserve(self.ctx, B, H, W))
+        self._reserved = (B, H, W)
+
+    def set_decode_tables(self, ori_bins: Optional[np.ndarray], pos_grid: Optional[np.ndarray]) -> None:
+        ob = None if ori_bins is None else np.ascontiguousarray(ori_bins, np.float64)
+        pg = None if pos_grid is None else np.ascontiguousarray(pos_grid, np.float64)
+        L.check(self.lib.spef_set_decode_tables(
+            self.ctx, None if ob is None else ob.ctypes.data_as(C.c_void_p), 0 if ob is None else ob.shape[0],
+            None if pg is None else pg.ctypes.data_as(C.c_void_p), 0 if pg is None else pg.shape[0]))
+        self._decode_tables = (ob, pg)
+
+    # ------------------------------------------------------------------ compute
+    @staticmethod
+    def _layout(x: torch.Tensor) -> Tuple[int, int, int, int]:
+        if x.dtype == torch.uint8:
+            assert x.dim() == 4 and x.shape[3] == 3, 'uint8 frames must be B x H x W x 3 (NHWC)'
+            return L.IN_U8_NHWC, x.shape[0], x.shape[1], x.shape[2]
+        assert x.dtype == torch.float32 and x.dim() == 4 and x.shape[1] == 3, 'expected B x 3 x H x W float32'
+        return L.IN_F32_NCHW, x.shape[0], x.shape[2], x.shape[3]
+
+    def forward(self, x: torch.Tensor, out0: Optional[torch.Tensor] = None, out1: Optional[torch.Tensor] = None):
+        assert x.device == self.device and x.is_contiguous()
+        layout, B, H, W = self._layout(x)
+        self.reserve(B, H, W)
+        if out0 is None:
+            out0 = torch.empty((B, self.n_out0), dtype=torch.float32, device=self.device)
+        if out1 is None and self.n_out1:
+            out1 = torch.empty((B, self.n_out1), dtype=torch.float32, device=self.device)
+        L.check(self.lib.spef_forward(self.ctx, _ptr(x), layout, B, H, W, _ptr(out0), _ptr(out1),
+                                      _stream(self.device)))
+        return out0, out1
+
+    def backbone(self, x: torch.Tensor) -> torch.Tensor:
+        layout, B, H, W = self._layout(x)
+        self.reserve(B, H, W)
+        fh, fw = H, W
+        for _ in range(5):
+            fh, fw = (fh - 1) // 2 + 1, (fw - 1) // 2 + 1
+        f = torch.empty((B, fh, fw, 1280), dtype=torch.float32, device=self.device)
+        L.check(self.lib.spef_backbone(self.ctx, _ptr(x), layout, B, H, W, _ptr(f), _stream(self.device)))
+        return f
+
+    def probe(self, x: torch.Tensor, stop_op: int) -> torch.Tensor:
+        layout, B, H, W = self._layout(x)
+        self.reserve(B, H, W)
+        out = torch.empty(B * H * W * 96 // 4 + 64, dtype=torch.float32, device=self.device)  # >= any act
+        c, h, w = C.c_int(), C.c_int(), C.c_int()
+        L.check(self.lib.spef_probe(self.ctx, _ptr(x), layout, B, H, W, stop_op, _ptr(out), C.byref(c), C.byref(h),
+                                    C.byref(w), _stream(self.device)))
+        return out[:B * h.value * w.value * c.value].view(B, h.value, w.value, c.value)
+
+    def decode(self, ori_mode: int, pos_mode: int, ori_raw: torch.Tensor, pos_raw: torch.Tensor,
+               want_soft: bool = True):
+        B = ori_raw.shape[0]
+        dev = self.device
+        quat = torch.empty((B, 4), dtype=torch.float32, device=dev)
+        pos = torch.empty((B, 3), dtype=torch.float32, device=dev)
+        status = torch.empty((B,), dtype=torch.int32, device=dev)
+        ori_soft = torch.empty_like(ori_raw) if (want_soft and ori_mode == L.CLASSIFICATION) else None
+        pos_soft = torch.empty_like(pos_raw) if (want_soft and pos_mode == L.CLASSIFICATION) else None
+        L.check(self.lib.spef_decode(self.ctx, ori_mode, pos_mode, _ptr(ori_raw), _ptr(pos_raw), B, _ptr(ori_soft),
+                                     _ptr(quat), _ptr(pos_soft), _ptr(pos), _ptr(status), _stream(dev)))
+        return {'ori': quat, 'pos': pos, 'ori_soft': ori_soft, 'pos_soft': pos_soft, 'status': status}
+
+    # ------------------------------------------------------------------ profiling
+    def profile_begin(self) -> None:
+        L.check(self.lib.spef_profile_begin(self.ctx))
+
+    def profile_end(self) -> dict:
+        """-> {kernel key: (launches, total_ms, algorithmic_bytes, algorithmic_flops)}."""
+        import json
+        need = C.c_size_t(0)
+        buf = C.create_string_buffer(1 << 16)
+        L.check(self.lib.spef_profile_end(self.ctx, buf, len(buf), C.byref(need)))
+        return {k: tuple(v) for k, v in json.loads(buf.value.decode()).items()}
+
+    def close(self) -> None:
+        if getattr(self, 'ctx', None):
+            self.lib.spef_destroy(self.ctx)
+            self.ctx = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -1,0 +1,110 @@
+"""``SPEMi355x`` -- the MI355X inference target behind the reference's "SPE model" interface.
+
+Drop-in for ``SPETorch`` (src/spe/spe_torch.py:12-124), ``SPETVMARM`` (src/tvm/spe_tvm.py:12) and
+``SPEJetson`` (src/nvidia/spe_nvidia.py:53): same ``predict(images) -> (pose, latency_ms)`` contract, same
+pose-dict keys, same exception types, so ``tools/evaluation.py:71`` and the ``deploy_*`` throughput loops
+(``num_predict``, deploy_nvidia.py:93) call it unchanged.
+
+Differences from SPETorch, all deliberate:
+  * forward AND decode run on the GPU (HIP kernels); the reference decodes on the host in NumPy
+    (spe_torch.py:73-74, classification_utils.py:163-164);
+  * latency is measured with HIP events after a device sync (the reference's ``time.time()`` around an
+    un-synchronised forward times only the launch, spe_torch.py:57-61);
+  * ``num_predict`` > 1 repeats the device work and reports the mean, like SPEJetson's server loop
+    (jetson_inference_server.py:129-141).
+"""
+from __future__ import annotations
+
+import gc
+from typing import Dict, Tuple, Union
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from .engine import Engine
+
+_MODES = {'regression': L.REGRESSION, 'classification': L.CLASSIFICATION, 'keypoints': L.KEYPOINTS}
+
+
+class SPEMi355x:
+    """Args:
+        model: a weight blob (bytes, from build_mi355x.py / ``spef_amd.blob.pack``), a path to one, or an
+            already-loaded ``Engine``.
+        device: HIP device (``cuda:N``).
+        spe_utils: the reference ``SPEUtils`` (or ``spef_amd.spe.spe_utils.SPEUtils``): provides ori/pos mode
+            and the decode histograms.
+    """
+
+    def __init__(self, model: Union[bytes, str, Engine], device: Union[str, torch.device], spe_utils) -> None:
+        self.spe_utils = spe_utils
+        self.device = torch.device(device)
+        self.engine = None
+        self.update_model(model, self.device)
+
+    # ------------------------------------------------------------------ lifecycle (spe_torch.py:78-124)
+    def update_model(self, model, device) -> None:
+        if self.engine is not None:
+            self.delete_model()
+        self.device = torch.device(device)
+        if isinstance(model, Engine):
+            self.engine = model
+        else:
+            if isinstance(model, str):
+                with open(model, 'rb') as f:
+                    model = f.read()
+            self.engine = Engine(model, self.device)
+        su = self.spe_utils
+        self.ori_mode, self.pos_mode = _MODES[su.ori_mode], _MODES[su.pos_mode]
+        if self.ori_mode == L.KEYPOINTS:
+            raise NotImplementedError('keypoint (EPnP) mode is not available in this build')
+        ori_bins = su.orientation.histogram if self.ori_mode == L.CLASSIFICATION else None
+        pos_grid = su.position.histogram if self.pos_mode == L.CLASSIFICATION else None
+        self.engine.set_decode_tables(ori_bins, pos_grid)
+        # the head widths in the blob must agree with the decode configuration (model.py:225-234)
+        want0 = su.orientation.n_bins if self.ori_mode == L.CLASSIFICATION else 4
+        want1 = su.position.n_bins if self.pos_mode == L.CLASSIFICATION else 3
+        assert (self.engine.n_out0, self.engine.n_out1) == (want0, want1), \
+            f'model head {(self.engine.n_out0, self.engine.n_out1)} != decode config {(want0, want1)}'
+
+    def delete_model(self) -> None:
+        if self.engine is not None:
+            self.engine.close()
+        self.engine = None
+        gc.collect()
+
+    def close(self) -> None:
+        self.delete_model()
+
+    # ------------------------------------------------------------------ inference
+    def _run(self, x: torch.Tensor):
+        raw0, raw1 = self.engine.forward(x)
+        return raw0, raw1, self.engine.decode(self.ori_mode, self.pos_mode, raw0, raw1)
+
+    def predict(self, images: torch.Tensor, num_predict: int = 1) -> Tuple[Dict, float]:
+        """images: NCHW float32 in [0,1] (the reference ``images['torch']``) or NHWC uint8 frames."""
+        assert self.engine is not None
+        x = images.to(self.device, non_blocking=True).contiguous()
+        torch.cuda.synchronize(self.device)
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(max(1, num_predict)):
+            raw0, raw1, dec = self._run(x)
+        end.record()
+        end.synchronize()
+        latency_ms = start.elapsed_time(end) / max(1, num_predict)
+
+        status = dec['status'].cpu().numpy()
+        if np.any(status & 1):
+            raise ValueError('Error during orientation decoding')                       # classification_utils.py:135
+        if np.any(status & 2):
+            raise ValueError('Encoded position vector sum is zero, cannot decode.')     # :254
+        if np.any(status & 4):
+            raise ValueError('Error during position decoding, NaN found in decoded position.')  # :263
+
+        pose = {'ori': dec['ori'].cpu().numpy(), 'pos': dec['pos'].cpu().numpy()}
+        if self.ori_mode == L.CLASSIFICATION:
+            pose['ori_soft'] = dec['ori_soft'].cpu().numpy()
+        if self.pos_mode == L.CLASSIFICATION:
+            pose['pos_soft'] = dec['pos_soft'].cpu().numpy()
+        return pose, latency_ms
