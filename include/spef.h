@@ -95,6 +95,11 @@ int spef_set_decode_tables(spef_ctx* ctx, const double* ori_bins, int n_ori_bins
 int spef_decode(spef_ctx* ctx, int ori_mode, int pos_mode, const float* ori_raw, const float* pos_raw, int B,
                 float* ori_soft, float* quat, float* pos_soft, float* pos, int* status, void* stream);
 
+/* Options. SPEF_OPT_FUSE_BLOCKS (default 1): run each inverted-residual block as one fused kernel
+ * (expand + depthwise + project on-chip) where its geometry is in the fused table; 0 = one kernel per conv. */
+enum spef_option { SPEF_OPT_FUSE_BLOCKS = 1 };
+int spef_set_option(spef_ctx* ctx, int option, int value);
+
 /* Per-launch HIP-event profiling of every kernel the context enqueues between begin and end (bench.py's
  * roofline leg). spef_profile_end synchronises, then writes a JSON object
  *   {"<kernel key>": [launches, total_ms, algorithmic_bytes, algorithmic_flops], ...}

@@ -44,6 +44,7 @@ struct spef_ctx {
   int n_ori_bins = 0;
   double* d_pos_grid = nullptr;
   int n_pos_bins = 0;
+  bool fuse = true;  // SPEF_OPT_FUSE_BLOCKS
   // per-launch HIP-event profiling (bench.py roofline leg)
   bool profiling = false;
   struct Rec {
@@ -191,36 +192,58 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       ch = (int)op.cout;
     } else if (op.kind == OP_IRB) {
       const int64_t M = (int64_t)B * h * w;
-      void* x = cur;
-      void* h1 = x;
-      if (op.expand != 1) {
-        h1 = pick({x});
-        HIP_TRY(prof_launch(c, s, pw_key(dt, EPI_RELU, op.hidden), pw_bytes(M, op.cin, op.hidden, false),
-                            2.0 * M * op.cin * op.hidden, [&] {
-          return launch_pw(dt, EPI_RELU, x, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, h1, M, (int)op.cin,
-                           (int)op.hidden, s);
-        }));
-      }
       const int OH = conv_out(h, (int)op.stride), OW = conv_out(w, (int)op.stride);
-      void* h2 = pick({x, h1});
-      const double opx = (double)B * OH * OW;
-      HIP_TRY(prof_launch(c, s, op.stride == 1 ? "dw_kernel<1>" : "dw_kernel<2>",
-                          ((double)B * h * w + opx) * op.hidden * 2 + 40.0 * op.hidden, opx * op.hidden * 18.0, [&] {
-        return launch_dw(dt, h1, ptr<float>(c, op.w1), ptr<float>(c, op.b1), h2, B, h, w, (int)op.hidden,
-                         (int)op.stride, OH, OW, s);
-      }));
       const bool res = op.flags & 1u;
-      void* y = res ? pick({x, h2}) : pick({h2});
-      const int64_t M2 = (int64_t)B * OH * OW;
-      HIP_TRY(prof_launch(c, s, pw_key(dt, res ? EPI_RES : EPI_NONE, op.cout), pw_bytes(M2, op.hidden, op.cout, res),
-                          2.0 * M2 * op.hidden * op.cout, [&] {
-        return launch_pw(dt, res ? EPI_RES : EPI_NONE, h2, ptr<void>(c, op.w2), ptr<float>(c, op.b2),
-                         res ? x : nullptr, y, M2, (int)op.hidden, (int)op.cout, s);
-      }));
-      cur = y;
-      h = OH;
-      w = OW;
-      ch = (int)op.cout;
+      const bool expand = op.expand != 1;
+      void* x = cur;
+      if (c->fuse && irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res)) {
+        void* y = pick({x});
+        const int64_t M2 = (int64_t)B * OH * OW;
+        const double flops = 2.0 * M * op.cin * op.hidden * (expand ? 1 : 0) + 18.0 * M2 * op.hidden +
+                             2.0 * M2 * op.hidden * op.cout;
+        const double bytes = (double)M * op.cin * 2 + (double)M2 * op.cout * 2 +
+                             (expand ? pw_bytes(0, op.cin, op.hidden, false) : 0) + 40.0 * op.hidden +
+                             pw_bytes(0, op.hidden, op.cout, false);
+        char key[96];
+        snprintf(key, sizeof(key), "irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
+        HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
+          return launch_irb(dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
+                            ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
+                            ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
+        }));
+        cur = y;
+        h = OH;
+        w = OW;
+        ch = (int)op.cout;
+      } else {
+        void* h1 = x;
+        if (expand) {
+          h1 = pick({x});
+          HIP_TRY(prof_launch(c, s, pw_key(dt, EPI_RELU, op.hidden), pw_bytes(M, op.cin, op.hidden, false),
+                              2.0 * M * op.cin * op.hidden, [&] {
+            return launch_pw(dt, EPI_RELU, x, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, h1, M,
+                             (int)op.cin, (int)op.hidden, s);
+          }));
+        }
+        void* h2 = pick({x, h1});
+        const double opx = (double)B * OH * OW;
+        HIP_TRY(prof_launch(c, s, op.stride == 1 ? "dw_kernel<1>" : "dw_kernel<2>",
+                            ((double)B * h * w + opx) * op.hidden * 2 + 40.0 * op.hidden, opx * op.hidden * 18.0, [&] {
+          return launch_dw(dt, h1, ptr<float>(c, op.w1), ptr<float>(c, op.b1), h2, B, h, w, (int)op.hidden,
+                           (int)op.stride, OH, OW, s);
+        }));
+        void* y = res ? pick({x, h2}) : pick({h2});
+        const int64_t M2 = (int64_t)B * OH * OW;
+        HIP_TRY(prof_launch(c, s, pw_key(dt, res ? EPI_RES : EPI_NONE, op.cout), pw_bytes(M2, op.hidden, op.cout, res),
+                            2.0 * M2 * op.hidden * op.cout, [&] {
+          return launch_pw(dt, res ? EPI_RES : EPI_NONE, h2, ptr<void>(c, op.w2), ptr<float>(c, op.b2),
+                           res ? x : nullptr, y, M2, (int)op.hidden, (int)op.cout, s);
+        }));
+        cur = y;
+        h = OH;
+        w = OW;
+        ch = (int)op.cout;
+      }
     } else if (op.kind == OP_LAST) {
       if (mode == 0) {
         const double M3 = (double)B * h * w;
@@ -492,6 +515,15 @@ int spef_decode(spef_ctx* c, int ori_mode, int pos_mode, const float* ori_raw, c
     return fail(SPEF_ERR_ARG, "pos_mode must be regression or classification");
   }
   return SPEF_OK;
+}
+
+int spef_set_option(spef_ctx* c, int option, int value) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  if (option == SPEF_OPT_FUSE_BLOCKS) {
+    c->fuse = value != 0;
+    return SPEF_OK;
+  }
+  return fail(SPEF_ERR_ARG, "unknown option");
 }
 
 int spef_profile_begin(spef_ctx* c) {

@@ -32,6 +32,12 @@ hipError_t launch_pw_pool(int dtype, const void* x, const void* wt, const float*
 hipError_t launch_fc(const float* x, const float* w, const float* bias, float* out0, int n0, float* out1, int n1,
                      int B, int K, hipStream_t s);
 
+// Fused InvertedResidual block (expand -> depthwise -> project [+x]) for the geometries in k_irb.hip's table.
+bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
+hipError_t launch_irb(int dtype, int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
+                      const void* we, const float* be, const float* wd, const float* bd, const void* wp,
+                      const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
+
 // Activation dtype -> fp32 NHWC copy (debug probes / backbone feature export).
 hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStream_t s);
 

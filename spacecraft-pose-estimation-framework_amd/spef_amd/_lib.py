@@ -12,6 +12,7 @@ from . import _build
 OK, ERR_ARG, ERR_HIP, ERR_BLOB, ERR_STATE, ERR_NUMERIC = range(6)
 IN_U8_NHWC, IN_F32_NCHW = 0, 1
 REGRESSION, CLASSIFICATION, KEYPOINTS = 0, 1, 2
+OPT_FUSE_BLOCKS = 1
 
 # name -> (restype, argtypes); keep in sync with include/spef.h (tests/test_abi.py checks the header)
 _vp, _i, _sz = C.c_void_p, C.c_int, C.c_size_t
@@ -30,6 +31,7 @@ SIGNATURES = {
     'spef_probe': (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _ip, _ip, _ip, _vp]),
     'spef_set_decode_tables': (_i, [_vp, _vp, _i, _vp, _i]),
     'spef_decode': (_i, [_vp, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'spef_set_option': (_i, [_vp, _i, _i]),
     'spef_profile_begin': (_i, [_vp]),
     'spef_profile_end': (_i, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),
 }

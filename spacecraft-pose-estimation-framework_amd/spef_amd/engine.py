@@ -126,6 +126,10 @@ class Engine:
                                      _ptr(quat), _ptr(pos_soft), _ptr(pos), _ptr(status), _stream(dev)))
         return {'ori': quat, 'pos': pos, 'ori_soft': ori_soft, 'pos_soft': pos_soft, 'status': status}
 
+    def set_fused(self, on: bool) -> None:
+        """Fused inverted-residual blocks (default) or one kernel per conv (reference schedule)."""
+        L.check(self.lib.spef_set_option(self.ctx, L.OPT_FUSE_BLOCKS, 1 if on else 0))
+
     # ------------------------------------------------------------------ profiling
     def profile_begin(self) -> None:
         L.check(self.lib.spef_profile_begin(self.ctx))

@@ -171,3 +171,24 @@ def test_predict_end_to_end():
     assert (np.abs(pose['pos'] - rp.numpy()) <= 1e-3 + 2e-3 * np.abs(rp.numpy())).all()
     assert pose['ori_soft'].shape == (4, 1728)
     tgt.close()
+
+
+@pytest.mark.parametrize('b,h,w', [(2, 512, 512), (3, 240, 384), (2, 100, 136), (1, 64, 64)])
+def test_fused_blocks_bit_identical_to_unfused(engine, b, h, w):
+    """The fused inverted-residual kernel rounds and accumulates exactly like the one-kernel-per-conv
+    schedule, so every block output (and the logits) must be bit-identical -- including partial edge tiles."""
+    fr = torch.from_numpy(_frames(b, h, w, 100 + h)).cuda()
+    try:
+        for op in range(1, 18):
+            engine.set_fused(False)
+            u = engine.probe(fr, op).cpu().numpy()
+            engine.set_fused(True)
+            f = engine.probe(fr, op).cpu().numpy()
+            assert np.array_equal(u, f), (op, np.abs(u - f).max())
+        engine.set_fused(False)
+        uo, up = [t.cpu().numpy() for t in engine.forward(fr)]
+        engine.set_fused(True)
+        fo, fp = [t.cpu().numpy() for t in engine.forward(fr)]
+        assert np.array_equal(uo, fo) and np.array_equal(up, fp)
+    finally:
+        engine.set_fused(True)

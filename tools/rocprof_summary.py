@@ -1,0 +1,65 @@
+"""Turn rocprofv3 outputs (gpurun_out/) into the committed summaries under profiles/.
+
+  python tools/rocprof_summary.py --tag r01 --stats gpurun_out/prof_r1 \
+      --fetch gpurun_out/pmc_fetch --write gpurun_out/pmc_write
+
+Writes profiles/<tag>_kernel_stats.csv (copy of rocprofv3 --stats) and profiles/<tag>_pmc_traffic.json:
+per kernel symbol, the mean HBM bytes per dispatch from separate FETCH_SIZE / WRITE_SIZE passes, corrected as
+MI355X_MICROARCH.md §HBM prescribes: bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024 (FETCH_SIZE is KB and on
+gfx950 reads half the bytes of a wide coalesced stream). Keys are short kernel names matching bench.py's keys.
+"""
+import argparse
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+from collections import defaultdict
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def short_name(full: str) -> str:
+    """'void spef::pw_kernel<spef::F16, 6, 2, 1>(...)' -> 'pw_kernel<F16,6,2,1>' (bench.py key form)."""
+    n = full.split('(')[0].replace('void ', '').replace('spef::', '').strip()
+    n = re.sub(r'\s+', '', n)
+    n = n.replace('stem_kernel<F16,0>', 'stem_kernel<u8>').replace('stem_kernel<F16,1>', 'stem_kernel<f32>')
+    n = n.replace('stem_kernel<BF16,0>', 'stem_kernel<u8>').replace('stem_kernel<BF16,1>', 'stem_kernel<f32>')
+    n = re.sub(r'dw_kernel<B?F16,(\d)>', r'dw_kernel<\1>', n)
+    n = re.sub(r'pw_pool_kernel<B?F16,(\d)>', r'pw_pool_kernel<\1>', n)
+    return n
+
+
+def per_kernel(counter_dir: str, counter: str):
+    f = glob.glob(os.path.join(counter_dir, '*counter_collection.csv'))[0]
+    acc = defaultdict(list)
+    for row in csv.DictReader(open(f)):
+        if row['Counter_Name'] == counter:
+            acc[short_name(row['Kernel_Name'])].append(float(row['Counter_Value']))
+    return {k: sum(v) / len(v) for k, v in acc.items()}, {k: len(v) for k, v in acc.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument('--tag', required=True)
+    ap.add_argument('--stats', required=True)
+    ap.add_argument('--fetch')
+    ap.add_argument('--write')
+    a = ap.parse_args()
+    out = os.path.join(ROOT, 'profiles')
+    os.makedirs(out, exist_ok=True)
+    st = glob.glob(os.path.join(a.stats, '*kernel_stats.csv'))[0]
+    shutil.copy(st, os.path.join(out, f'{a.tag}_kernel_stats.csv'))
+    if a.fetch and a.write:
+        fe, n = per_kernel(a.fetch, 'FETCH_SIZE')
+        wr, _ = per_kernel(a.write, 'WRITE_SIZE')
+        res = {k: {'hbm_bytes_per_launch': (2 * fe[k] + wr.get(k, 0.0)) * 1024, 'fetch_kb': fe[k],
+                   'write_kb': wr.get(k, 0.0), 'dispatches': n[k]} for k in fe}
+        json.dump({'correction': 'bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024 (MI355X_MICROARCH.md HBM)',
+                   'kernels': res}, open(os.path.join(out, f'{a.tag}_pmc_traffic.json'), 'w'), indent=1)
+    print('wrote profiles for', a.tag)
+
+
+if __name__ == '__main__':
+    main()
