@@ -1,0 +1,164 @@
+// Front kernel: stem ConvBnAct 3->32 3x3/s2 (mobilenet_v2.py:252-254) fused with inverted-residual block 1
+// (t=1: depthwise 3x3 32ch + BN + ReLU -> project 32->16 + BN; pytorch_layers.py:65-98), uint8 NHWC frames in.
+//
+// The 32-channel 256x256 stem map (the largest activation of the network) never reaches HBM: per 16x16 block-1
+// output tile the kernel stages the 37x37x3 input bytes in LDS, computes the 18x18 stem tile (+1 halo for the
+// depthwise) on MFMA, keeps it in LDS, and runs the block-1 depthwise + project from there.
+//
+// Stem on MFMA: K = 27 taps (ky, kx, ci) padded to 32, A = weights [32 ch][k], B = image patch [k][pixel].
+// uint8 pixels are exact in fp16/bf16; ToTensor's /255 is folded into the weights, which are split into
+// hi + lo halves (w = hi + lo, two MFMAs) so the stem keeps ~fp32 weight precision.
+#include "spef_common.hpp"
+#include "spef_kernels.hpp"
+
+namespace spef {
+
+template <typename DT, int TH, int TW, int NW>
+__global__ __launch_bounds__(NW * 64) void front_kernel(
+    const uint8_t* __restrict__ X, const float* __restrict__ ws, const float* __restrict__ bs,
+    const float* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
+    const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int SH_img, int SW_img,
+    int tiles_x, int tiles_y, uint32_t nwg) {
+  using T = typename DT::T;
+  using x8 = typename DT::x8;
+  using x4 = typename DT::x4;
+  constexpr int SH = TH + 2, SW = TW + 2;          // stem tile (block-1 output tile + depthwise halo)
+  constexpr int IH = 2 * SH + 1, IW = 2 * SW + 1;  // input tile
+  constexpr int IRS = (IW * 3 + 15) / 16 * 16;     // input LDS row stride (bytes)
+  constexpr int PS = SH * SW, PS16 = (PS + 15) / 16, PSP = PS16 * 16;
+  constexpr int XS = 40;                           // stem-map row stride (32 ch + 16 B)
+  constexpr int POUT16 = TH * TW / 16, QPW = POUT16 / NW;
+  static_assert(POUT16 % NW == 0, "tile split");
+  __shared__ __attribute__((aligned(16))) uint8_t In[IH * IRS];
+  __shared__ __attribute__((aligned(16))) T Xs[PSP * XS];
+  __shared__ __attribute__((aligned(16))) float Sl[9 * 32 + 32];
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int tx = (int)(L % (uint32_t)tiles_x);
+  L /= (uint32_t)tiles_x;
+  const int ty = (int)(L % (uint32_t)tiles_y);
+  const int b = (int)(L / (uint32_t)tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * TW;            // block-1 output (= stem output) coordinates
+  const int sy0 = oy0 - 1, sx0 = ox0 - 1;            // stem tile origin
+  const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;    // input tile origin
+
+  // ---- 1. input bytes -> LDS (zero outside the image = the stem's padding)
+  {
+    const uint8_t* Xb = X + (size_t)b * H * W * 3;
+    for (int u = tid; u < IH * IW * 3; u += NW * 64) {
+      const int r = u / (IW * 3), cb = u - r * (IW * 3);
+      const int iy = iy0 + r, ix = ix0 + cb / 3;
+      uint8_t v = 0;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = Xb[((size_t)iy * W + ix0) * 3 + cb];
+      In[r * IRS + cb] = v;
+    }
+    for (int u = tid; u < 9 * 32 + 32; u += NW * 64) Sl[u] = u < 9 * 32 ? Wd[(u >> 5) * 32 + (u & 31)] : bd[u - 9 * 32];
+  }
+  // stem weight fragments (fp32 [27][32] -> /255 -> hi + lo), channel tiles t = 0, 1
+  x8 ahi[2], alo[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * kg + e;
+      const float w = k < 27 ? ws[k * 32 + 16 * t + r16] / 255.0f : 0.0f;
+      const T hi = (T)w;
+      ahi[t][e] = hi;
+      alo[t][e] = (T)(w - (float)hi);
+    }
+  const float4 sb0 = *reinterpret_cast<const float4*>(bs + 4 * kg);
+  const float4 sb1 = *reinterpret_cast<const float4*>(bs + 16 + 4 * kg);
+  // per-lane tap offsets inside the input tile for k = 8kg + e: (k / 9) * IRS + k % 9
+  int koff[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int k = 8 * kg + e;
+    koff[e] = k < 27 ? (k / 9) * IRS + (k % 9) : -1;
+  }
+  __syncthreads();
+
+  // ---- 2. stem tile on MFMA -> Xs (fp16/bf16, ReLU; zero outside the stem map = block-1 depthwise padding)
+  for (int pt = wave; pt < PS16; pt += NW) {
+    const int p = pt * 16 + r16;
+    const int spy = p / SW, spx = p - (p / SW) * SW;
+    const int base = (2 * spy) * IRS + 2 * spx * 3;
+    x8 bx;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bx[e] = (koff[e] >= 0 && p < PS) ? (T)(float)In[base + koff[e]] : (T)0.0f;
+    f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+    e0 = DT::mfma(ahi[0], bx, e0);
+    e0 = DT::mfma(alo[0], bx, e0);
+    e1 = DT::mfma(ahi[1], bx, e1);
+    e1 = DT::mfma(alo[1], bx, e1);
+    const int gy = sy0 + spy, gx = sx0 + spx;
+    const bool pv = p < PS && gy >= 0 && gy < SH_img && gx >= 0 && gx < SW_img;
+    x4 o0, o1;
+    o0[0] = (T)(pv ? fmaxf(e0[0] + sb0.x, 0.f) : 0.f);
+    o0[1] = (T)(pv ? fmaxf(e0[1] + sb0.y, 0.f) : 0.f);
+    o0[2] = (T)(pv ? fmaxf(e0[2] + sb0.z, 0.f) : 0.f);
+    o0[3] = (T)(pv ? fmaxf(e0[3] + sb0.w, 0.f) : 0.f);
+    o1[0] = (T)(pv ? fmaxf(e1[0] + sb1.x, 0.f) : 0.f);
+    o1[1] = (T)(pv ? fmaxf(e1[1] + sb1.y, 0.f) : 0.f);
+    o1[2] = (T)(pv ? fmaxf(e1[2] + sb1.z, 0.f) : 0.f);
+    o1[3] = (T)(pv ? fmaxf(e1[3] + sb1.w, 0.f) : 0.f);
+    *reinterpret_cast<x4*>(Xs + p * XS + 4 * kg) = o0;
+    *reinterpret_cast<x4*>(Xs + p * XS + 16 + 4 * kg) = o1;
+  }
+  __syncthreads();
+
+  // ---- 3. block 1: depthwise 3x3 (32 ch) -> project 32 -> 16 (+BN), one 16-pixel tile per wave step
+  const x8 pa = load8<DT>(Wp + (size_t)r16 * 32 + 8 * kg);
+  const float4 pb = *reinterpret_cast<const float4*>(bp + 4 * kg);
+#pragma unroll
+  for (int qi = 0; qi < QPW; ++qi) {
+    const int o = (wave * QPW + qi) * 16 + r16;
+    const int oy = o / TW, ox = o - (o / TW) * TW;
+    float a8[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a8[e] = Sl[9 * 32 + 8 * kg + e];
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const x8 v = *reinterpret_cast<const x8*>(Xs + ((oy + ky) * SW + (ox + kx)) * XS + 8 * kg);
+        const float* w = Sl + (ky * 3 + kx) * 32 + 8 * kg;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], w[e], a8[e]);
+      }
+    x8 bf;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    acc = DT::mfma(pa, bf, acc);
+    const int gy = oy0 + oy, gx = ox0 + ox;
+    if (gy < SH_img && gx < SW_img) {
+      x4 out;
+      out[0] = (T)(acc[0] + pb.x);
+      out[1] = (T)(acc[1] + pb.y);
+      out[2] = (T)(acc[2] + pb.z);
+      out[3] = (T)(acc[3] + pb.w);
+      *reinterpret_cast<x4*>(Y + (((size_t)b * SH_img + gy) * SW_img + gx) * 16 + 4 * kg) = out;
+    }
+  }
+}
+
+hipError_t launch_front(int dtype, const void* x, const float* ws, const float* bs, const float* wd, const float* bd,
+                        const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
+                        hipStream_t s) {
+  constexpr int TH = 16, TW = 16, NW = 8;
+  const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
+  const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
+  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+  const uint32_t nwg = (uint32_t)nwg64;
+  if (dtype == DT_F16)
+    front_kernel<F16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, ws, bs, wd, bd, (const _Float16*)wp, bp,
+                                                          (_Float16*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
+  else
+    front_kernel<BF16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, ws, bs, wd, bd, (const __bf16*)wp, bp,
+                                                           (__bf16*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
+  return hipGetLastError();
+}
+
+}  // namespace spef

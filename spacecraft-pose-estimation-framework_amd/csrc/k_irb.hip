@@ -9,49 +9,61 @@
 // Rounding points are identical to the unfused kernels (fp16/bf16 after expand, after depthwise, after
 // project), and so is the accumulation order: the fused block is bit-identical to the unfused schedule.
 //
-// MFMA 16x16x32 C^T formulation (see k_conv.hip): A = weights [out ch][k], B = activations [k][pixel],
+// MFMA 16x16x32 C^T formulation (see k_gemm.hip): A = weights [out ch][k], B = activations [k][pixel],
 // lane l holds B[k = 8(l>>4)+e][pixel l&15] = 16 contiguous bytes of an LDS pixel row.
+//
+// Work split (NW waves): the expand distributes the input-tile pixel tiles over all waves; the depthwise +
+// project phase gives wave w the output pixel tiles of group w % WP and the output-channel tiles of group
+// w / WP (WCO groups; WCO > 1 duplicates the cheap depthwise to cut per-wave accumulators on wide blocks).
+// Synchronisation: ONE barrier per hidden chunk. Es is double-buffered; the per-chunk depthwise weight slab
+// (9x32 weights, dw bias, expand bias; fp32) is triple-buffered and filled one chunk ahead.
 #include "spef_common.hpp"
 #include "spef_kernels.hpp"
 
 namespace spef {
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO>
 struct IrbGeom {
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW;
   static constexpr int PIN16 = (PIN + 15) / 16;
   static constexpr int PINP = PIN16 * 16;
   static constexpr int CINP = (CIN + 31) / 32 * 32;
-  static constexpr int XS = CINP + 8;        // Xs row stride (elements): +16 B against bank conflicts
+  static constexpr int XS = CINP + 8;          // Xs row stride (elements): +16 B against bank conflicts
   static constexpr int ES = EXPAND ? 40 : XS;  // hidden-chunk row stride (32 ch + 16 B)
   static constexpr int NCH = (HID + 31) / 32;
-  static constexpr int HIDP = NCH * 32;      // project K (blob pads to 32)
+  static constexpr int HIDP = NCH * 32;        // project K (blob pads to 32)
   static constexpr int POUT = TH * TW;
   static constexpr int POUT16 = POUT / 16;
-  static constexpr int QPW = POUT16 / NW;    // output pixel tiles per wave
+  static constexpr int WP = NW / WCO;          // pixel-tile groups in the depthwise/project phase
+  static constexpr int QPW = POUT16 / WP;      // output pixel tiles per wave
   static constexpr int NCT = (COUT + 15) / 16;
-  static constexpr int LDS_ELEMS = PINP * XS + (EXPAND ? 2 * PINP * ES : 0);
-  static_assert(POUT % 16 == 0 && POUT16 % NW == 0, "output tile must split into 16-pixel MFMA tiles per wave");
+  static constexpr int NCTW = NCT / WCO;       // output-channel tiles per wave
+  static constexpr int KS = CINP / 32;
+  static constexpr int SLAB = 9 * 32 + 32 + 32;  // floats: dw weights [9][32], dw bias, expand bias
+  static constexpr int LDS_BYTES = (PINP * XS + (EXPAND ? 2 * PINP * ES : 0)) * 2 + 3 * SLAB * 4;
+  static_assert(POUT % 16 == 0 && POUT16 % WP == 0 && NW % WCO == 0 && NCT % WCO == 0, "tile split");
   static_assert(CIN % 8 == 0 && HID % 8 == 0 && COUT % 4 == 0, "channel counts must be multiples of 8");
   static_assert(EXPAND || HID == 32, "t == 1 blocks are supported for 32 channels (MobileNet-V2 block 1)");
   static_assert(!RES || (S == 1 && CIN == COUT), "residual needs stride 1 and cin == cout");
+  static_assert(NW * 64 >= SLAB / 4, "slab fill needs one float4 per thread");
 };
 
-template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW>
+template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO>
 __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const typename DT::T* __restrict__ X, const typename DT::T* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
     int tiles_y, uint32_t nwg) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW>;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
   using x4 = typename DT::x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Xs = reinterpret_cast<T*>(smem);
   T* Es0 = Xs + G::PINP * G::XS;
-  T* Es1 = Es0 + G::PINP * G::ES;
+  T* Es1 = Es0 + (EXPAND ? G::PINP * G::ES : 0);
+  float* Sl = reinterpret_cast<float*>(Es1 + (EXPAND ? G::PINP * G::ES : 0));   // [3][SLAB]
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
@@ -62,6 +74,28 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   const int b = (int)(L / (uint32_t)tiles_y);
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+
+  // slab fill for chunk cc: thread t < SLAB/4 moves one float4 (dw weights, dw bias, expand bias)
+  auto slab_load = [&](int cc) -> float4 {
+    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (tid < G::SLAB / 4 && cc < G::NCH) {
+      const int f = tid * 4;
+      if (f < 9 * 32) {
+        const int tap = f >> 5, ch = 32 * cc + (f & 31);
+        if (ch < HID) v = *reinterpret_cast<const float4*>(Wd + tap * HID + ch);
+      } else if (f < 9 * 32 + 32) {
+        const int ch = 32 * cc + (f - 9 * 32);
+        if (ch < HID) v = *reinterpret_cast<const float4*>(bd + ch);
+      } else if (EXPAND) {
+        const int ch = 32 * cc + (f - 9 * 32 - 32);
+        if (ch < HID) v = *reinterpret_cast<const float4*>(be + ch);
+      }
+    }
+    return v;
+  };
+  auto slab_store = [&](int cc, float4 v) {
+    if (tid < G::SLAB / 4) *reinterpret_cast<float4*>(Sl + (cc % 3) * G::SLAB + tid * 4) = v;
+  };
 
   // ---- 1. stage the input tile (+halo) in LDS; outside the image (and K padding) -> 0
   {
@@ -78,36 +112,51 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       }
       *reinterpret_cast<x8*>(Xs + p * G::XS + g * 8) = v;
     }
+    slab_store(0, slab_load(0));
   }
   __syncthreads();
 
-  // per-lane output pixel of each owned 16-pixel tile
-  int opix[G::QPW];
+  const int wp = wave % G::WP, wc = wave / G::WP;
+  int oyq[G::QPW], oxq[G::QPW];
 #pragma unroll
-  for (int qi = 0; qi < G::QPW; ++qi) opix[qi] = (wave * G::QPW + qi) * 16 + r16;
+  for (int qi = 0; qi < G::QPW; ++qi) {
+    const int o = (wp * G::QPW + qi) * 16 + r16;
+    oyq[qi] = o / TW;
+    oxq[qi] = o - oyq[qi] * TW;
+  }
 
-  f32x4 acc[G::QPW][G::NCT];
+  f32x4 acc[G::QPW][G::NCTW];
 #pragma unroll
   for (int qi = 0; qi < G::QPW; ++qi)
 #pragma unroll
-    for (int t = 0; t < G::NCT; ++t) acc[qi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
 
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
+    const float4 slab_next = slab_load(c + 1);     // issued now, stored after this chunk's expand
+    const float* sl = Sl + (c % 3) * G::SLAB;
     const T* Es;
     if constexpr (EXPAND) {
       T* Ew = (c & 1) ? Es1 : Es0;
       const int vh = HID - 32 * c < 32 ? HID - 32 * c : 32;   // valid hidden channels in this chunk
       // ---- 2. expand: E[p][h] = relu(sum_k X[p][k] We[32c+h][k] + be) for all tile pixels
+      x8 a0[G::KS], a1[G::KS];
+      const T* w0 = We + (size_t)(32 * c + r16) * G::CINP + 8 * kg;
+#pragma unroll
+      for (int ks = 0; ks < G::KS; ++ks) {
+        a0[ks] = load8<DT>(w0 + 32 * ks);
+        a1[ks] = vh > 16 ? load8<DT>(w0 + 16 * G::CINP + 32 * ks) : zero8<DT>();
+      }
+      const float4 eb0 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 32 + 4 * kg);
+      const float4 eb1 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 32 + 16 + 4 * kg);
       for (int pt = wave; pt < G::PIN16; pt += NW) {
         f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
         const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
-        const T* w0 = We + (size_t)(32 * c + r16) * G::CINP + 8 * kg;
 #pragma unroll
-        for (int ks = 0; ks < G::CINP / 32; ++ks) {
+        for (int ks = 0; ks < G::KS; ++ks) {
           const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
-          e0 = DT::mfma(load8<DT>(w0 + 32 * ks), bx, e0);
-          if (vh > 16) e1 = DT::mfma(load8<DT>(w0 + 16 * G::CINP + 32 * ks), bx, e1);
+          e0 = DT::mfma(a0[ks], bx, e0);
+          e1 = DT::mfma(a1[ks], bx, e1);
         }
         const int p = pt * 16 + r16;
         bool pv = p < G::PIN;
@@ -117,83 +166,79 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
           pv = iy >= 0 && iy < H && ix >= 0 && ix < W;     // zero padding of the depthwise input
         }
         T* er = Ew + p * G::ES + 4 * kg;
-#pragma unroll
-        for (int t = 0; t < 2; ++t) {
-          const f32x4 e = t ? e1 : e0;
-          x4 o;
-          if (16 * t < vh && pv) {
-            const float4 bb = *reinterpret_cast<const float4*>(be + 32 * c + 16 * t + 4 * kg);
-            o[0] = (T)fmaxf(e[0] + bb.x, 0.f);
-            o[1] = (T)fmaxf(e[1] + bb.y, 0.f);
-            o[2] = (T)fmaxf(e[2] + bb.z, 0.f);
-            o[3] = (T)fmaxf(e[3] + bb.w, 0.f);
-          } else {
-#pragma unroll
-            for (int r = 0; r < 4; ++r) o[r] = (T)0.f;
-          }
-          *reinterpret_cast<x4*>(er + 16 * t) = o;
-        }
+        x4 o0, o1;
+        o0[0] = (T)(pv ? fmaxf(e0[0] + eb0.x, 0.f) : 0.f);
+        o0[1] = (T)(pv ? fmaxf(e0[1] + eb0.y, 0.f) : 0.f);
+        o0[2] = (T)(pv ? fmaxf(e0[2] + eb0.z, 0.f) : 0.f);
+        o0[3] = (T)(pv ? fmaxf(e0[3] + eb0.w, 0.f) : 0.f);
+        const bool v1 = pv && vh > 16;
+        o1[0] = (T)(v1 ? fmaxf(e1[0] + eb1.x, 0.f) : 0.f);
+        o1[1] = (T)(v1 ? fmaxf(e1[1] + eb1.y, 0.f) : 0.f);
+        o1[2] = (T)(v1 ? fmaxf(e1[2] + eb1.z, 0.f) : 0.f);
+        o1[3] = (T)(v1 ? fmaxf(e1[3] + eb1.w, 0.f) : 0.f);
+        *reinterpret_cast<x4*>(er) = o0;
+        *reinterpret_cast<x4*>(er + 16) = o1;
       }
-      __syncthreads();
       Es = Ew;
     } else {
       Es = Xs;
     }
+    slab_store(c + 1, slab_next);
+    __syncthreads();
 
     // ---- 3. depthwise 3x3 on this hidden chunk -> project B fragment in registers; 4. project MFMA
-    const int hch = 32 * c + 8 * kg;           // this lane's 8 hidden channels
-    const bool hv = hch < HID;
-    float wdv[9][8];
-    float bdv[8];
-    if (hv) {
+    // project weights for this chunk first: their latency hides under the depthwise
+    x8 pa[G::NCTW];
+    const T* wpp = Wp + (size_t)(wc * G::NCTW * 16 + r16) * G::HIDP + 32 * c + 8 * kg;
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const float4 a = *reinterpret_cast<const float4*>(Wd + tap * HID + hch);
-        const float4 bq = *reinterpret_cast<const float4*>(Wd + tap * HID + hch + 4);
-        wdv[tap][0] = a.x; wdv[tap][1] = a.y; wdv[tap][2] = a.z; wdv[tap][3] = a.w;
-        wdv[tap][4] = bq.x; wdv[tap][5] = bq.y; wdv[tap][6] = bq.z; wdv[tap][7] = bq.w;
-      }
-      const float4 a = *reinterpret_cast<const float4*>(bd + hch);
-      const float4 bq = *reinterpret_cast<const float4*>(bd + hch + 4);
-      bdv[0] = a.x; bdv[1] = a.y; bdv[2] = a.z; bdv[3] = a.w;
-      bdv[4] = bq.x; bdv[5] = bq.y; bdv[6] = bq.z; bdv[7] = bq.w;
-    }
+    for (int t = 0; t < G::NCTW; ++t) pa[t] = load8<DT>(wpp + (size_t)t * 16 * G::HIDP);
+    const bool hv = 32 * c + 8 * kg < HID;    // this lane's 8 hidden channels exist
 #pragma unroll
     for (int qi = 0; qi < G::QPW; ++qi) {
       x8 bf = zero8<DT>();
       if (hv) {
-        const int oy = opix[qi] / TW, ox = opix[qi] - (opix[qi] / TW) * TW;
         float a8[8];
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a8[e] = bdv[e];
+        {
+          const float4 u0 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 8 * kg);
+          const float4 u1 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 8 * kg + 4);
+          a8[0] = u0.x; a8[1] = u0.y; a8[2] = u0.z; a8[3] = u0.w;
+          a8[4] = u1.x; a8[5] = u1.y; a8[6] = u1.z; a8[7] = u1.w;
+        }
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
           for (int kx = 0; kx < 3; ++kx) {
-            const int p = (oy * S + ky) * G::IW + (ox * S + kx);
-            const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + (EXPAND ? 8 * kg : hch));
-#pragma unroll
-            for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wdv[ky * 3 + kx][e], a8[e]);
+            const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
+            const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + 8 * kg);
+            const float4 w0 = *reinterpret_cast<const float4*>(sl + (ky * 3 + kx) * 32 + 8 * kg);
+            const float4 w1 = *reinterpret_cast<const float4*>(sl + (ky * 3 + kx) * 32 + 8 * kg + 4);
+            a8[0] = fmaf((float)v[0], w0.x, a8[0]);
+            a8[1] = fmaf((float)v[1], w0.y, a8[1]);
+            a8[2] = fmaf((float)v[2], w0.z, a8[2]);
+            a8[3] = fmaf((float)v[3], w0.w, a8[3]);
+            a8[4] = fmaf((float)v[4], w1.x, a8[4]);
+            a8[5] = fmaf((float)v[5], w1.y, a8[5]);
+            a8[6] = fmaf((float)v[6], w1.z, a8[6]);
+            a8[7] = fmaf((float)v[7], w1.w, a8[7]);
           }
 #pragma unroll
         for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
       }
-      const T* wp = Wp + (size_t)r16 * G::HIDP + 32 * c + 8 * kg;
 #pragma unroll
-      for (int t = 0; t < G::NCT; ++t) acc[qi][t] = DT::mfma(load8<DT>(wp + (size_t)t * 16 * G::HIDP), bf, acc[qi][t]);
+      for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
     }
   }
 
   // ---- 5. epilogue: + bias (+ residual from the staged input tile) -> y (NHWC)
 #pragma unroll
   for (int qi = 0; qi < G::QPW; ++qi) {
-    const int oy = opix[qi] / TW, ox = opix[qi] - (opix[qi] / TW) * TW;
+    const int oy = oyq[qi], ox = oxq[qi];
     const int gy = oy0 + oy, gx = ox0 + ox;
     if (gy >= OH || gx >= OW) continue;
     T* yr = Y + (((size_t)b * OH + gy) * OW + gx) * COUT;
 #pragma unroll
-    for (int t = 0; t < G::NCT; ++t) {
-      const int co = 16 * t + 4 * kg;
+    for (int t = 0; t < G::NCTW; ++t) {
+      const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
       if (co >= COUT) continue;
       const float4 bb = *reinterpret_cast<const float4*>(bp + co);
       f32x4 v = acc[qi][t];
@@ -212,35 +257,35 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 }
 
 // ------------------------------------------------------------------------------------------ dispatch
-// One instantiation per MobileNet-V2 block geometry, tile sized so the LDS working set leaves room for
-// 2-3 workgroups per CU. Unknown geometries return hipErrorNotSupported -> the executor falls back to the
-// unfused kernels.
-#define SPEF_IRB_TABLE(X)                                      \
-  X(32, 32, 16, 1, 16, 16, false, false, 4)   /* block 1      */ \
-  X(16, 96, 24, 2, 8, 8, true, false, 4)      /* block 2      */ \
-  X(24, 144, 24, 1, 8, 16, true, true, 4)     /* block 3      */ \
-  X(24, 144, 32, 2, 8, 8, true, false, 4)     /* block 4      */ \
-  X(32, 192, 32, 1, 8, 16, true, true, 4)     /* blocks 5-6   */ \
-  X(32, 192, 64, 2, 8, 8, true, false, 4)     /* block 7      */ \
-  X(64, 384, 64, 1, 8, 16, true, true, 4)     /* blocks 8-10  */ \
-  X(64, 384, 96, 1, 8, 16, true, false, 4)    /* block 11     */ \
-  X(96, 576, 96, 1, 8, 16, true, true, 4)     /* blocks 12-13 */ \
-  X(96, 576, 160, 2, 4, 8, true, false, 2)    /* block 14     */ \
-  X(160, 960, 160, 1, 8, 8, true, true, 4)    /* blocks 15-16 */ \
-  X(160, 960, 320, 1, 8, 8, true, false, 4)   /* block 17     */
+// One instantiation per MobileNet-V2 block geometry: (cin, hidden, cout, stride, tile TH x TW, expand,
+// residual, waves, cout groups). Unknown geometries return hipErrorNotSupported -> the executor falls back
+// to the unfused kernels.
+#define SPEF_IRB_TABLE(X)                                         \
+  X(32, 32, 16, 1, 16, 16, false, false, 8, 1)   /* block 1      */ \
+  X(16, 96, 24, 2, 8, 8, true, false, 4, 1)      /* block 2      */ \
+  X(24, 144, 24, 1, 8, 16, true, true, 8, 1)     /* block 3      */ \
+  X(24, 144, 32, 2, 8, 8, true, false, 4, 1)     /* block 4      */ \
+  X(32, 192, 32, 1, 8, 16, true, true, 8, 1)     /* blocks 5-6   */ \
+  X(32, 192, 64, 2, 8, 8, true, false, 8, 2)     /* block 7      */ \
+  X(64, 384, 64, 1, 8, 16, true, true, 8, 1)     /* blocks 8-10  */ \
+  X(64, 384, 96, 1, 8, 16, true, false, 8, 1)    /* block 11     */ \
+  X(96, 576, 96, 1, 8, 16, true, true, 8, 1)     /* blocks 12-13 */ \
+  X(96, 576, 160, 2, 4, 8, true, false, 4, 2)    /* block 14     */ \
+  X(160, 960, 160, 1, 8, 8, true, true, 8, 2)    /* blocks 15-16 */ \
+  X(160, 960, 320, 1, 8, 8, true, false, 8, 2)   /* block 17     */
 
-template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW>
+template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO>
 static hipError_t irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                          hipStream_t s) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW>;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
   using T = typename DT::T;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  const size_t lds = (size_t)G::LDS_ELEMS * sizeof(T);
-  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW>;
+  const size_t lds = (size_t)G::LDS_BYTES;
+  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
   static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
   if (!attr_set && lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -256,16 +301,16 @@ template <typename DT>
 static hipError_t irb_dispatch(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
                                const void* we, const float* be, const float* wd, const float* bd, const void* wp,
                                const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
-#define SPEF_IRB_CASE(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_)                                                  \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                      \
-    return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s);
+#define SPEF_IRB_CASE(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_)                                               \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                        \
+    return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s);
   SPEF_IRB_TABLE(SPEF_IRB_CASE)
 #undef SPEF_IRB_CASE
   return hipErrorNotSupported;
 }
 
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
-#define SPEF_IRB_HAS(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_) \
+#define SPEF_IRB_HAS(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_) \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS) return true;
   SPEF_IRB_TABLE(SPEF_IRB_HAS)
 #undef SPEF_IRB_HAS

@@ -44,7 +44,9 @@ struct spef_ctx {
   int n_ori_bins = 0;
   double* d_pos_grid = nullptr;
   int n_pos_bins = 0;
-  bool fuse = true;  // SPEF_OPT_FUSE_BLOCKS
+  int fuse = 1;              // SPEF_OPT_FUSE_BLOCKS: 0 never, 1 when input H*W >= fuse_min_hw
+  int64_t fuse_min_hw = 0;   // SPEF_OPT_FUSE_MIN_HW
+  int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
   // per-launch HIP-event profiling (bench.py roofline leg)
   bool profiling = false;
   struct Rec {
@@ -93,6 +95,17 @@ hipError_t prof_launch(spef_ctx* c, hipStream_t s, const char* key, double bytes
   hipEventRecord(b, s);
   c->recs.push_back({key, a, b, bytes, flops});
   return e;
+}
+
+hipError_t pw_any(spef_ctx* c, int dt, int epi, const void* x, const void* wt, const float* bias, const void* r,
+                  void* y, int64_t M, int K, int N, hipStream_t s) {
+  return c->gemm ? launch_gemm_pw(dt, epi, x, wt, bias, r, y, M, K, N, s)
+                 : launch_pw(dt, epi, x, wt, bias, r, y, M, K, N, s);
+}
+
+const char* pw_key(int dt, int epi, int N);
+const char* pw_any_key(spef_ctx* c, int dt, int epi, int N) {
+  return c->gemm ? gemm_key(dt, epi, N) : pw_key(dt, epi, N);
 }
 
 const char* pw_key(int dt, int epi, int N) {
@@ -168,6 +181,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
   void* cur = nullptr;
   int h = H, w = W, ch = 3;
   int op_index = 0;
+  bool skip_next = false;
   auto pick = [&](std::initializer_list<void*> busy) -> void* {
     for (void* b : c->buf) {
       bool used = false;
@@ -177,8 +191,34 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
     return nullptr;
   };
   for (const OpDesc& op : c->ops) {
+    if (skip_next) {  // block 1 already produced by the fused front kernel
+      skip_next = false;
+      if (mode == 1 && op_index == stop) break;
+      ++op_index;
+      continue;
+    }
     if (op.kind == OP_STEM) {
       const int OH = conv_out(h, 2), OW = conv_out(w, 2);
+      const OpDesc* nx = (&op + 1 < c->ops.data() + c->ops.size()) ? &op + 1 : nullptr;
+      const bool front = c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx && nx->kind == OP_IRB &&
+                         nx->cin == 32 && nx->hidden == 32 && nx->cout == 16 && nx->expand == 1 && nx->stride == 1 &&
+                         op.cout == 32;
+      if (front) {
+        void* y = c->buf[0];
+        const double px = (double)B * OH * OW;
+        HIP_TRY(prof_launch(c, s, "front_kernel<stem+block1>", (double)B * h * w * 3 + px * 16 * 2,
+                            px * (2 * 27 * 32 + 18 * 32 + 2 * 32 * 16), [&] {
+          return launch_front(dt, input, ptr<float>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
+                              ptr<float>(c, nx->b1), ptr<void>(c, nx->w2), ptr<float>(c, nx->b2), y, B, h, w, OH, OW, s);
+        }));
+        cur = y;
+        h = OH;
+        w = OW;
+        ch = (int)nx->cout;
+        skip_next = true;
+        ++op_index;
+        continue;
+      }
       void* y = c->buf[0];
       const double px = (double)B * OH * OW;
       const double in_b = (double)B * h * w * 3 * (layout == IN_U8_NHWC ? 1 : 4);
@@ -196,7 +236,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const bool res = op.flags & 1u;
       const bool expand = op.expand != 1;
       void* x = cur;
-      if (c->fuse && irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res)) {
+      if (c->fuse && (int64_t)h * w >= c->fuse_min_hw && irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res)) {
         void* y = pick({x});
         const int64_t M2 = (int64_t)B * OH * OW;
         const double flops = 2.0 * M * op.cin * op.hidden * (expand ? 1 : 0) + 18.0 * M2 * op.hidden +
@@ -219,9 +259,9 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         void* h1 = x;
         if (expand) {
           h1 = pick({x});
-          HIP_TRY(prof_launch(c, s, pw_key(dt, EPI_RELU, op.hidden), pw_bytes(M, op.cin, op.hidden, false),
+          HIP_TRY(prof_launch(c, s, pw_any_key(c, dt, EPI_RELU, op.hidden), pw_bytes(M, op.cin, op.hidden, false),
                               2.0 * M * op.cin * op.hidden, [&] {
-            return launch_pw(dt, EPI_RELU, x, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, h1, M,
+            return pw_any(c, dt, EPI_RELU, x, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, h1, M,
                              (int)op.cin, (int)op.hidden, s);
           }));
         }
@@ -234,9 +274,9 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         }));
         void* y = res ? pick({x, h2}) : pick({h2});
         const int64_t M2 = (int64_t)B * OH * OW;
-        HIP_TRY(prof_launch(c, s, pw_key(dt, res ? EPI_RES : EPI_NONE, op.cout), pw_bytes(M2, op.hidden, op.cout, res),
-                            2.0 * M2 * op.hidden * op.cout, [&] {
-          return launch_pw(dt, res ? EPI_RES : EPI_NONE, h2, ptr<void>(c, op.w2), ptr<float>(c, op.b2),
+        HIP_TRY(prof_launch(c, s, pw_any_key(c, dt, res ? EPI_RES : EPI_NONE, op.cout),
+                            pw_bytes(M2, op.hidden, op.cout, res), 2.0 * M2 * op.hidden * op.cout, [&] {
+          return pw_any(c, dt, res ? EPI_RES : EPI_NONE, h2, ptr<void>(c, op.w2), ptr<float>(c, op.b2),
                            res ? x : nullptr, y, M2, (int)op.hidden, (int)op.cout, s);
         }));
         cur = y;
@@ -255,7 +295,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         }));
       } else if (mode == 2) {
         void* y = pick({cur});
-        HIP_TRY(launch_pw(dt, EPI_RELU, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, y,
+        HIP_TRY(pw_any(c, dt, EPI_RELU, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, y,
                           (int64_t)B * h * w, (int)op.cin, (int)op.cout, s));
         cur = y;
         ch = (int)op.cout;
@@ -521,6 +561,14 @@ int spef_set_option(spef_ctx* c, int option, int value) {
   if (!c) return fail(SPEF_ERR_ARG, "null context");
   if (option == SPEF_OPT_FUSE_BLOCKS) {
     c->fuse = value != 0;
+    return SPEF_OK;
+  }
+  if (option == SPEF_OPT_FUSE_MIN_HW) {
+    c->fuse_min_hw = value;
+    return SPEF_OK;
+  }
+  if (option == SPEF_OPT_PW_GEMM) {
+    c->gemm = value != 0;
     return SPEF_OK;
   }
   return fail(SPEF_ERR_ARG, "unknown option");

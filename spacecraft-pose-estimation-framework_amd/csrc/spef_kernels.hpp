@@ -19,6 +19,11 @@ hipError_t launch_stem(int dtype, int in_layout, const void* in, const float* w,
 hipError_t launch_pw(int dtype, int epi, const void* x, const void* wt, const float* bias, const void* r,
                      void* y, int64_t M, int K, int N, hipStream_t s);
 
+// Same contract, LDS-tiled double-buffered MFMA GEMM (k_gemm.hip); gemm_key names the instantiation used.
+hipError_t launch_gemm_pw(int dtype, int epi, const void* x, const void* wt, const float* bias, const void* r,
+                          void* y, int64_t M, int K, int N, hipStream_t s);
+const char* gemm_key(int dtype, int epi, int N);
+
 // Depthwise 3x3 conv, pad 1, stride 1|2, BN folded, ReLU. W9: fp32 [9][C], bias fp32 [C].
 hipError_t launch_dw(int dtype, const void* x, const float* w9, const float* bias, void* y, int B, int H, int W,
                      int C, int stride, int OH, int OW, hipStream_t s);
@@ -37,6 +42,10 @@ bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res
 hipError_t launch_irb(int dtype, int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
                       const void* we, const float* be, const float* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
+
+// Stem (u8 NHWC input) fused with inverted-residual block 1 (32 -> dw -> 16), k_front.hip.
+hipError_t launch_front(int dtype, const void* x, const float* ws, const float* bs, const float* wd, const float* bd,
+                        const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 
 // Activation dtype -> fp32 NHWC copy (debug probes / backbone feature export).
 hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStream_t s);

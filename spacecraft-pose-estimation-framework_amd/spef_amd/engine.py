@@ -130,6 +130,9 @@ class Engine:
         """Fused inverted-residual blocks (default) or one kernel per conv (reference schedule)."""
         L.check(self.lib.spef_set_option(self.ctx, L.OPT_FUSE_BLOCKS, 1 if on else 0))
 
+    def set_option(self, option: int, value: int) -> None:
+        L.check(self.lib.spef_set_option(self.ctx, option, int(value)))
+
     # ------------------------------------------------------------------ profiling
     def profile_begin(self) -> None:
         L.check(self.lib.spef_profile_begin(self.ctx))

@@ -176,8 +176,9 @@ def test_predict_end_to_end():
 @pytest.mark.parametrize('b,h,w', [(2, 512, 512), (3, 240, 384), (2, 100, 136), (1, 64, 64)])
 def test_fused_blocks_bit_identical_to_unfused(engine, b, h, w):
     """The fused inverted-residual kernel rounds and accumulates exactly like the one-kernel-per-conv
-    schedule, so every block output (and the logits) must be bit-identical -- including partial edge tiles."""
-    fr = torch.from_numpy(_frames(b, h, w, 100 + h)).cuda()
+    schedule, so every block output (and the logits) must be bit-identical -- including partial edge tiles.
+    (float32 NCHW input: the uint8 path replaces stem + block 1 by the front kernel, checked separately.)"""
+    fr = M.u8_nhwc_to_nchw_f32(_frames(b, h, w, 100 + h)).contiguous().cuda()
     try:
         for op in range(1, 18):
             engine.set_fused(False)
@@ -192,3 +193,18 @@ def test_fused_blocks_bit_identical_to_unfused(engine, b, h, w):
         assert np.array_equal(uo, fo) and np.array_equal(up, fp)
     finally:
         engine.set_fused(True)
+
+
+@pytest.mark.parametrize('b,h,w', [(2, 512, 512), (3, 240, 384), (2, 100, 136)])
+def test_front_kernel_vs_stem_block1(engine, sd, b, h, w):
+    """uint8 path: fused stem+block-1 front kernel (MFMA stem, split-fp16 weights) vs the fp32 VALU stem +
+    separate block-1 kernel, and vs the oracle's block-1 output."""
+    fr = _frames(b, h, w, 7 + w)
+    x8 = torch.from_numpy(fr).cuda()
+    xf = M.u8_nhwc_to_nchw_f32(fr).contiguous().cuda()
+    got = engine.probe(x8, 1).cpu().numpy()
+    sep = engine.probe(xf, 1).cpu().numpy()
+    ref = M.backbone(M.u8_nhwc_to_nchw_f32(fr), sd, upto=1).permute(0, 2, 3, 1).numpy()
+    scale = np.abs(ref).max()
+    assert np.abs(got - sep).max() / scale < 4e-3
+    assert np.abs(got - ref).max() / scale < 4e-3
