@@ -94,11 +94,13 @@ __global__ __launch_bounds__(256) void pw_kernel(const typename DT::T* __restric
   const int n0 = chunk * 16 * NT;
   const int64_t m0 = ptile * (64 * MT) + (int64_t)wave * 16 * MT;
 
-  f32x4 acc[NT][MT];
+  f32x4 acc[NT][MT];   // accumulators start at the folded-BN bias
 #pragma unroll
-  for (int a = 0; a < NT; ++a)
+  for (int a = 0; a < NT; ++a) {
+    const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + 16 * a + 4 * kg);
 #pragma unroll
-    for (int b = 0; b < MT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < MT; ++b) acc[a][b] = f32x4{bb.x, bb.y, bb.z, bb.w};
+  }
 
   const T* wp = Wt + (size_t)(n0 + r16) * Kp + 8 * kg;
   const T* xp[MT];
@@ -128,13 +130,11 @@ __global__ __launch_bounds__(256) void pw_kernel(const typename DT::T* __restric
   for (int a = 0; a < NT; ++a) {
     const int i = n0 + 16 * a + 4 * kg;
     if (i >= N) continue;
-    const float4 bb = *reinterpret_cast<const float4*>(bias + i);
 #pragma unroll
     for (int b = 0; b < MT; ++b) {
       const int64_t m = m0 + 16 * b + r16;
       if (m >= M) continue;
       f32x4 v = acc[a][b];
-      v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       if (EPI == EPI_RELU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.0f);

@@ -26,7 +26,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   constexpr int IH = 2 * SH + 1, IW = 2 * SW + 1;  // input tile
   constexpr int IRS = (IW * 3 + 15) / 16 * 16;     // input LDS row stride (bytes)
   constexpr int PS = SH * SW, PS16 = (PS + 15) / 16, PSP = PS16 * 16;
-  constexpr int XS = 40;                           // stem-map row stride (32 ch + 16 B)
+  constexpr int XS = 48;                           // stem-map row stride: 96 B, conflict-free b128 reads
   constexpr int POUT16 = TH * TW / 16, QPW = POUT16 / NW;
   static_assert(POUT16 % NW == 0, "tile split");
   __shared__ __attribute__((aligned(16))) uint8_t In[IH * IRS];
@@ -130,15 +130,15 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
     x8 bf;
 #pragma unroll
     for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    f32x4 acc = {pb.x, pb.y, pb.z, pb.w};      // bias as MFMA C (same order as the block kernels)
     acc = DT::mfma(pa, bf, acc);
     const int gy = oy0 + oy, gx = ox0 + ox;
     if (gy < SH_img && gx < SW_img) {
       x4 out;
-      out[0] = (T)(acc[0] + pb.x);
-      out[1] = (T)(acc[1] + pb.y);
-      out[2] = (T)(acc[2] + pb.z);
-      out[3] = (T)(acc[3] + pb.w);
+      out[0] = (T)acc[0];
+      out[1] = (T)acc[1];
+      out[2] = (T)acc[2];
+      out[3] = (T)acc[3];
       *reinterpret_cast<x4*>(Y + (((size_t)b * SH_img + gy) * SW_img + gx) * 16 + 4 * kg) = out;
     }
   }

@@ -22,7 +22,7 @@ __global__ __launch_bounds__(256) void gemm_pw_kernel(const typename DT::T* __re
   using x4 = typename DT::x4;
   constexpr int WM = 4 / WN;
   constexpr int BN = 16 * WN * NT, BM = 16 * WM * MT;
-  constexpr int RS = 40;                                   // LDS row stride (elements): 32 + 16 B pad
+  constexpr int RS = 48;                                   // LDS row stride: 96 B = 6 granules, conflict-free
   constexpr int XP = (BM * 4 + 255) / 256, WP = (BN * 4 + 255) / 256;   // 16-B pieces per thread
   __shared__ __attribute__((aligned(16))) T As[2][BN * RS];
   __shared__ __attribute__((aligned(16))) T Bs[2][BM * RS];
@@ -66,11 +66,15 @@ __global__ __launch_bounds__(256) void gemm_pw_kernel(const typename DT::T* __re
     }
   };
 
-  f32x4 acc[NT][MT];
+  f32x4 acc[NT][MT];   // accumulators start at the folded-BN bias (same order as the fused block kernel)
 #pragma unroll
-  for (int a = 0; a < NT; ++a)
+  for (int a = 0; a < NT; ++a) {
+    const int i = n0 + (wn * NT + a) * 16 + 4 * kg;
+    float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (i < Np) bb = *reinterpret_cast<const float4*>(bias + i);
 #pragma unroll
-    for (int b = 0; b < MT; ++b) acc[a][b] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int b = 0; b < MT; ++b) acc[a][b] = f32x4{bb.x, bb.y, bb.z, bb.w};
+  }
 
   const int KS = Kp >> 5;
   gload(0);
@@ -100,13 +104,11 @@ __global__ __launch_bounds__(256) void gemm_pw_kernel(const typename DT::T* __re
   for (int a = 0; a < NT; ++a) {
     const int i = n0 + (wn * NT + a) * 16 + 4 * kg;
     if (i >= N) continue;
-    const float4 bb = *reinterpret_cast<const float4*>(bias + i);
 #pragma unroll
     for (int b = 0; b < MT; ++b) {
       const int64_t m = mt0 + (wm * MT + b) * 16 + r16;
       if (m >= M) continue;
       f32x4 v = acc[a][b];
-      v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       if (EPI == EPI_RELU) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.0f);

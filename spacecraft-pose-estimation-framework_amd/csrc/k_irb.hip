@@ -22,15 +22,24 @@
 
 namespace spef {
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF>
 struct IrbGeom {
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW;
   static constexpr int PIN16 = (PIN + 15) / 16;
   static constexpr int PINP = PIN16 * 16;
-  static constexpr int CINP = (CIN + 31) / 32 * 32;
-  static constexpr int XS = CINP + 8;          // Xs row stride (elements): +16 B against bank conflicts
-  static constexpr int ES = EXPAND ? 40 : XS;  // hidden-chunk row stride (32 ch + 16 B)
+  static constexpr bool K16 = CIN == 16;          // 16-channel input: K = 16 MFMA, no K padding in LDS
+  static constexpr int CINP = K16 ? 16 : (CIN + 31) / 32 * 32;
+  // Row strides: a multiple of 16 B that is 2 mod 4 granules makes ds_read_b128 of 16 consecutive rows
+  // conflict-free over all four lane groups (MI355X_MICROARCH.md §LDS); +16 B rows leave a 2-way conflict
+  // but less LDS. The wide padding is used only when it costs no workgroups per CU.
+  static constexpr int NBUF = EXPAND ? (DBUF ? 2 : 1) : 0;
+  static constexpr int SLAB = 9 * 32 + 32 + 32;  // floats: dw weights [9][32], dw bias, expand bias
+  static constexpr int bytes_for(int xs, int es) { return (PINP * xs + NBUF * PINP * es) * 2 + 3 * SLAB * 4; }
+  static constexpr bool WIDE = (163840 / bytes_for(CINP + 16, 48)) >= (163840 / bytes_for(CINP + 8, 40));
+  static constexpr int XS = WIDE ? CINP + 16 : CINP + 8;   // Xs row stride (elements)
+  static constexpr int ES = EXPAND ? (WIDE ? 48 : 40) : XS; // hidden-chunk row stride
+  static constexpr int EPT = (PIN16 + NW - 1) / NW;   // expand pixel tiles per wave
   static constexpr int NCH = (HID + 31) / 32;
   static constexpr int HIDP = NCH * 32;        // project K (blob pads to 32)
   static constexpr int POUT = TH * TW;
@@ -39,31 +48,32 @@ struct IrbGeom {
   static constexpr int QPW = POUT16 / WP;      // output pixel tiles per wave
   static constexpr int NCT = (COUT + 15) / 16;
   static constexpr int NCTW = NCT / WCO;       // output-channel tiles per wave
-  static constexpr int KS = CINP / 32;
-  static constexpr int SLAB = 9 * 32 + 32 + 32;  // floats: dw weights [9][32], dw bias, expand bias
-  static constexpr int LDS_BYTES = (PINP * XS + (EXPAND ? 2 * PINP * ES : 0)) * 2 + 3 * SLAB * 4;
+  static constexpr int KS = K16 ? 1 : CINP / 32;
+  static constexpr int LDS_BYTES = bytes_for(XS, ES);
   static_assert(POUT % 16 == 0 && POUT16 % WP == 0 && NW % WCO == 0 && NCT % WCO == 0, "tile split");
   static_assert(CIN % 8 == 0 && HID % 8 == 0 && COUT % 4 == 0, "channel counts must be multiples of 8");
   static_assert(EXPAND || HID == 32, "t == 1 blocks are supported for 32 channels (MobileNet-V2 block 1)");
   static_assert(!RES || (S == 1 && CIN == COUT), "residual needs stride 1 and cin == cout");
   static_assert(NW * 64 >= SLAB / 4, "slab fill needs one float4 per thread");
+  static_assert(EPT <= 32, "validity mask is 32 bits");
 };
 
-template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO>
+template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
+          bool DBUF>
 __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const typename DT::T* __restrict__ X, const typename DT::T* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
     int tiles_y, uint32_t nwg) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
   using x4 = typename DT::x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Xs = reinterpret_cast<T*>(smem);
   T* Es0 = Xs + G::PINP * G::XS;
-  T* Es1 = Es0 + (EXPAND ? G::PINP * G::ES : 0);
-  float* Sl = reinterpret_cast<float*>(Es1 + (EXPAND ? G::PINP * G::ES : 0));   // [3][SLAB]
+  T* Es1 = Es0 + (G::NBUF == 2 ? G::PINP * G::ES : 0);
+  float* Sl = reinterpret_cast<float*>(Es0 + G::NBUF * G::PINP * G::ES);   // [3][SLAB]
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
@@ -99,7 +109,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 
   // ---- 1. stage the input tile (+halo) in LDS; outside the image (and K padding) -> 0
   {
-    constexpr int GPR = G::CINP / 8;        // 16-B groups per LDS row
+    constexpr int GPR = G::CINP / 8;        // 16-B groups per LDS row (CIN 16: 2)
     constexpr int CG = CIN / 8;             // valid groups
     const T* Xb = X + (size_t)b * H * W * CIN;
     for (int u = tid; u < G::PINP * GPR; u += NW * 64) {
@@ -116,6 +126,19 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   }
   __syncthreads();
 
+  // per-lane validity of its expand pixels (inside the tile and the image): the depthwise zero padding
+  uint32_t pvmask = 0;
+  if constexpr (EXPAND) {
+#pragma unroll
+    for (int j = 0; j < G::EPT; ++j) {
+      const int p = (wave + NW * j) * 16 + r16;
+      if (p < G::PIN) {
+        const int py = p / G::IW, px = p - py * G::IW;
+        const int iy = iy0 + py, ix = ix0 + px;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) pvmask |= 1u << j;
+      }
+    }
+  }
   const int wp = wave % G::WP, wc = wave / G::WP;
   int oyq[G::QPW], oxq[G::QPW];
 #pragma unroll
@@ -125,11 +148,13 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     oxq[qi] = o - oyq[qi] * TW;
   }
 
-  f32x4 acc[G::QPW][G::NCTW];
+  f32x4 acc[G::QPW][G::NCTW];   // project accumulators start at the folded-BN bias
 #pragma unroll
-  for (int qi = 0; qi < G::QPW; ++qi)
+  for (int t = 0; t < G::NCTW; ++t) {
+    const float4 bb = *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg);
 #pragma unroll
-    for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int qi = 0; qi < G::QPW; ++qi) acc[qi][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
+  }
 
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
@@ -137,47 +162,61 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const float* sl = Sl + (c % 3) * G::SLAB;
     const T* Es;
     if constexpr (EXPAND) {
+      if constexpr (G::NBUF == 1) {
+        if (c > 0) __syncthreads();   // single hidden slab: all depthwise reads of chunk c-1 done
+      }
       T* Ew = (c & 1) ? Es1 : Es0;
       const int vh = HID - 32 * c < 32 ? HID - 32 * c : 32;   // valid hidden channels in this chunk
       // ---- 2. expand: E[p][h] = relu(sum_k X[p][k] We[32c+h][k] + be) for all tile pixels
+      // expand weights are stored [Np][Kp] with Kp = CIN rounded up to 32 (blob layout)
+      constexpr int WKP = (CIN + 31) / 32 * 32;
       x8 a0[G::KS], a1[G::KS];
-      const T* w0 = We + (size_t)(32 * c + r16) * G::CINP + 8 * kg;
+      x4 q0 = {}, q1 = {};
+      if constexpr (G::K16) {
+        const T* w0 = We + (size_t)(32 * c + r16) * WKP + 4 * kg;
+        q0 = *reinterpret_cast<const x4*>(w0);
+        if (vh > 16) q1 = *reinterpret_cast<const x4*>(w0 + 16 * WKP);
+      } else {
+        const T* w0 = We + (size_t)(32 * c + r16) * WKP + 8 * kg;
 #pragma unroll
-      for (int ks = 0; ks < G::KS; ++ks) {
-        a0[ks] = load8<DT>(w0 + 32 * ks);
-        a1[ks] = vh > 16 ? load8<DT>(w0 + 16 * G::CINP + 32 * ks) : zero8<DT>();
+        for (int ks = 0; ks < G::KS; ++ks) {
+          a0[ks] = load8<DT>(w0 + 32 * ks);
+          a1[ks] = vh > 16 ? load8<DT>(w0 + 16 * WKP + 32 * ks) : zero8<DT>();
+        }
       }
       const float4 eb0 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 32 + 4 * kg);
       const float4 eb1 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 32 + 16 + 4 * kg);
-      for (int pt = wave; pt < G::PIN16; pt += NW) {
-        f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
-        const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
 #pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-          const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
-          e0 = DT::mfma(a0[ks], bx, e0);
-          e1 = DT::mfma(a1[ks], bx, e1);
+      for (int j = 0; j < G::EPT; ++j) {
+        const int pt = wave + NW * j;
+        if (pt >= G::PIN16) break;
+        f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
+        if constexpr (G::K16) {
+          const x4 bx = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
+          e0 = DT::mfma16(q0, bx, e0);
+          e1 = DT::mfma16(q1, bx, e1);
+        } else {
+          const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
+#pragma unroll
+          for (int ks = 0; ks < G::KS; ++ks) {
+            const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
+            e0 = DT::mfma(a0[ks], bx, e0);
+            e1 = DT::mfma(a1[ks], bx, e1);
+          }
         }
-        const int p = pt * 16 + r16;
-        bool pv = p < G::PIN;
-        if (pv) {
-          const int py = p / G::IW, px = p - py * G::IW;
-          const int iy = iy0 + py, ix = ix0 + px;
-          pv = iy >= 0 && iy < H && ix >= 0 && ix < W;     // zero padding of the depthwise input
-        }
-        T* er = Ew + p * G::ES + 4 * kg;
+        const uint32_t m0 = ((pvmask >> j) & 1u) ? 0xffffffffu : 0u;
+        const uint32_t m1 = vh > 16 ? m0 : 0u;
         x4 o0, o1;
-        o0[0] = (T)(pv ? fmaxf(e0[0] + eb0.x, 0.f) : 0.f);
-        o0[1] = (T)(pv ? fmaxf(e0[1] + eb0.y, 0.f) : 0.f);
-        o0[2] = (T)(pv ? fmaxf(e0[2] + eb0.z, 0.f) : 0.f);
-        o0[3] = (T)(pv ? fmaxf(e0[3] + eb0.w, 0.f) : 0.f);
-        const bool v1 = pv && vh > 16;
-        o1[0] = (T)(v1 ? fmaxf(e1[0] + eb1.x, 0.f) : 0.f);
-        o1[1] = (T)(v1 ? fmaxf(e1[1] + eb1.y, 0.f) : 0.f);
-        o1[2] = (T)(v1 ? fmaxf(e1[2] + eb1.z, 0.f) : 0.f);
-        o1[3] = (T)(v1 ? fmaxf(e1[3] + eb1.w, 0.f) : 0.f);
-        *reinterpret_cast<x4*>(er) = o0;
-        *reinterpret_cast<x4*>(er + 16) = o1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o0[r] = (T)fmaxf(e0[r], 0.f);
+          o1[r] = (T)fmaxf(e1[r], 0.f);
+        }
+        uint2 u0 = *reinterpret_cast<uint2*>(&o0), u1 = *reinterpret_cast<uint2*>(&o1);
+        u0.x &= m0; u0.y &= m0; u1.x &= m1; u1.y &= m1;
+        T* er = Ew + (pt * 16 + r16) * G::ES + 4 * kg;
+        *reinterpret_cast<uint2*>(er) = u0;
+        *reinterpret_cast<uint2*>(er + 16) = u1;
       }
       Es = Ew;
     } else {
@@ -240,9 +279,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     for (int t = 0; t < G::NCTW; ++t) {
       const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
       if (co >= COUT) continue;
-      const float4 bb = *reinterpret_cast<const float4*>(bp + co);
       f32x4 v = acc[qi][t];
-      v[0] += bb.x; v[1] += bb.y; v[2] += bb.z; v[3] += bb.w;
       if constexpr (RES) {
         const x4 r = *reinterpret_cast<const x4*>(Xs + ((oy + 1) * G::IW + (ox + 1)) * G::XS + co);
 #pragma unroll
@@ -260,32 +297,33 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 // One instantiation per MobileNet-V2 block geometry: (cin, hidden, cout, stride, tile TH x TW, expand,
 // residual, waves, cout groups). Unknown geometries return hipErrorNotSupported -> the executor falls back
 // to the unfused kernels.
-#define SPEF_IRB_TABLE(X)                                         \
-  X(32, 32, 16, 1, 16, 16, false, false, 8, 1)   /* block 1      */ \
-  X(16, 96, 24, 2, 8, 8, true, false, 4, 1)      /* block 2      */ \
-  X(24, 144, 24, 1, 8, 16, true, true, 8, 1)     /* block 3      */ \
-  X(24, 144, 32, 2, 8, 8, true, false, 4, 1)     /* block 4      */ \
-  X(32, 192, 32, 1, 8, 16, true, true, 8, 1)     /* blocks 5-6   */ \
-  X(32, 192, 64, 2, 8, 8, true, false, 8, 2)     /* block 7      */ \
-  X(64, 384, 64, 1, 8, 16, true, true, 8, 1)     /* blocks 8-10  */ \
-  X(64, 384, 96, 1, 8, 16, true, false, 8, 1)    /* block 11     */ \
-  X(96, 576, 96, 1, 8, 16, true, true, 8, 1)     /* blocks 12-13 */ \
-  X(96, 576, 160, 2, 4, 8, true, false, 4, 2)    /* block 14     */ \
-  X(160, 960, 160, 1, 8, 8, true, true, 8, 2)    /* blocks 15-16 */ \
-  X(160, 960, 320, 1, 8, 8, true, false, 8, 2)   /* block 17     */
+#define SPEF_IRB_TABLE(X)                                                \
+  X(32, 32, 16, 1, 16, 16, false, false, 8, 1, true)    /* block 1      */ \
+  X(16, 96, 24, 2, 8, 8, true, false, 4, 1, false)      /* block 2      */ \
+  X(24, 144, 24, 1, 8, 16, true, true, 8, 1, true)      /* block 3      */ \
+  X(24, 144, 32, 2, 8, 8, true, false, 4, 1, false)     /* block 4      */ \
+  X(32, 192, 32, 1, 8, 16, true, true, 8, 1, true)      /* blocks 5-6   */ \
+  X(32, 192, 64, 2, 8, 8, true, false, 8, 2, false)     /* block 7      */ \
+  X(64, 384, 64, 1, 8, 16, true, true, 8, 1, true)      /* blocks 8-10  */ \
+  X(64, 384, 96, 1, 8, 16, true, false, 8, 1, true)     /* block 11     */ \
+  X(96, 576, 96, 1, 8, 16, true, true, 8, 1, true)      /* blocks 12-13 */ \
+  X(96, 576, 160, 2, 4, 8, true, false, 4, 2, true)     /* block 14     */ \
+  X(160, 960, 160, 1, 8, 8, true, true, 8, 2, true)     /* blocks 15-16 */ \
+  X(160, 960, 320, 1, 8, 8, true, false, 8, 2, true)    /* block 17     */
 
-template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO>
+template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
+          bool DBUF>
 static hipError_t irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                          hipStream_t s) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF>;
   using T = typename DT::T;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   const size_t lds = (size_t)G::LDS_BYTES;
-  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
+  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF>;
   static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
   if (!attr_set && lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -301,16 +339,17 @@ template <typename DT>
 static hipError_t irb_dispatch(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
                                const void* we, const float* be, const float* wd, const float* bd, const void* wp,
                                const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
-#define SPEF_IRB_CASE(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_)                                               \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                        \
-    return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s);
+#define SPEF_IRB_CASE(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_)                            \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)            \
+    return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
+                                                                      OW, s);
   SPEF_IRB_TABLE(SPEF_IRB_CASE)
 #undef SPEF_IRB_CASE
   return hipErrorNotSupported;
 }
 
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
-#define SPEF_IRB_HAS(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_) \
+#define SPEF_IRB_HAS(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_) \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS) return true;
   SPEF_IRB_TABLE(SPEF_IRB_HAS)
 #undef SPEF_IRB_HAS

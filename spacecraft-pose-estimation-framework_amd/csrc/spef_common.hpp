@@ -17,12 +17,16 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // Element-type traits: the MFMA used for a 16x16 output tile with K = 32 per instruction.
 // gfx950 lane map (cdna_hip_programming.md §3): A[i = l&15][k = 8(l>>4)+e], B[k = 8(l>>4)+e][j = l&15],
 // D[i = 4(l>>4)+r][j = l&15].
+// mfma16: K = 16 form, lane holds A[i = l&15][k = 4(l>>4)+e], B[k = 4(l>>4)+e][j = l&15] (4 elements).
 struct F16 {
   using T = _Float16;
   using x8 = f16x8;
   using x4 = f16x4;
   static __device__ __forceinline__ f32x4 mfma(x8 a, x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x4 mfma16(x4 a, x4 b, f32x4 c) {
+    return __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c, 0, 0, 0);
   }
 };
 struct BF16 {
@@ -31,6 +35,10 @@ struct BF16 {
   using x4 = bf16x4;
   static __device__ __forceinline__ f32x4 mfma(x8 a, x8 b, f32x4 c) {
     return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+  }
+  static __device__ __forceinline__ f32x4 mfma16(x4 a, x4 b, f32x4 c) {
+    typedef short s4 __attribute__((ext_vector_type(4)));
+    return __builtin_amdgcn_mfma_f32_16x16x16bf16_1k(__builtin_bit_cast(s4, a), __builtin_bit_cast(s4, b), c, 0, 0, 0);
   }
 };
 
