@@ -100,7 +100,8 @@ int spef_decode(spef_ctx* ctx, int ori_mode, int pos_mode, const float* ori_raw,
 /* SPEF_OPT_FUSE_MIN_HW: fuse only blocks whose input has at least this many pixels per image (late,
  * low-resolution blocks then run as GEMM + depthwise + GEMM with the hidden tensor L2/MALL-resident).
  * SPEF_OPT_PW_GEMM (default 1): LDS-tiled MFMA GEMM for unfused 1x1 convs; 0 = register-direct kernel. */
-enum spef_option { SPEF_OPT_FUSE_BLOCKS = 1, SPEF_OPT_FUSE_MIN_HW = 2, SPEF_OPT_PW_GEMM = 3 };
+/* SPEF_OPT_IRB_VARIANT: fused-block tile variant (0 = tuned default; others for tuning sweeps). */
+enum spef_option { SPEF_OPT_FUSE_BLOCKS = 1, SPEF_OPT_FUSE_MIN_HW = 2, SPEF_OPT_PW_GEMM = 3, SPEF_OPT_IRB_VARIANT = 4 };
 int spef_set_option(spef_ctx* ctx, int option, int value);
 
 /* Per-launch HIP-event profiling of every kernel the context enqueues between begin and end (bench.py's

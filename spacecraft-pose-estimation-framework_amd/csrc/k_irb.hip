@@ -22,7 +22,8 @@
 
 namespace spef {
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
+          bool STW>
 struct IrbGeom {
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW;
@@ -34,8 +35,24 @@ struct IrbGeom {
   // conflict-free over all four lane groups (MI355X_MICROARCH.md §LDS); +16 B rows leave a 2-way conflict
   // but less LDS. The wide padding is used only when it costs no workgroups per CU.
   static constexpr int NBUF = EXPAND ? (DBUF ? 2 : 1) : 0;
-  static constexpr int SLAB = 9 * 32 + 32 + 32;  // floats: dw weights [9][32], dw bias, expand bias
-  static constexpr int bytes_for(int xs, int es) { return (PINP * xs + NBUF * PINP * es) * 2 + 3 * SLAB * 4; }
+  static constexpr int NCH_ = (HID + 31) / 32;
+  static constexpr int SLAB = 9 * 32;             // floats: depthwise weights [9][32] of one hidden chunk
+  static constexpr int BIAS = 2 * NCH_ * 32;      // floats: dw bias + expand bias of every hidden channel
+  // STW: per-chunk expand / project weights staged once per workgroup in LDS (3 + 2 buffers) instead of every
+  // wave fetching its own fragments from L2 (8x less L2 traffic for an 8-wave workgroup)
+  static constexpr int WKP = (CIN + 31) / 32 * 32;      // blob row length of the expand weights
+  static constexpr int WEK = K16 ? 16 : WKP;            // elements of a row the MFMA needs
+  static constexpr int WES = K16 ? 24 : WKP + 16;       // LDS row strides (conflict-free for b128 reads)
+  static constexpr int WPS = 48;
+  static constexpr int NCTP = (COUT + 15) / 16 * 16;
+  static constexpr int WE_ELEMS = STW && EXPAND ? 3 * 32 * WES : 0;
+  static constexpr int WP_ELEMS = STW ? 2 * NCTP * WPS : 0;
+  static constexpr int WE_PIECES = STW && EXPAND ? 32 * WEK / 8 : 0;
+  static constexpr int WP_PIECES = STW ? NCTP * 4 : 0;
+  static constexpr int W_PPT = (WE_PIECES + WP_PIECES + NW * 64 - 1) / (NW * 64);   // 16-B pieces per thread
+  static constexpr int bytes_for(int xs, int es) {
+    return (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 + (2 * SLAB + BIAS) * 4;
+  }
   static constexpr bool WIDE = (163840 / bytes_for(CINP + 16, 48)) >= (163840 / bytes_for(CINP + 8, 40));
   static constexpr int XS = WIDE ? CINP + 16 : CINP + 8;   // Xs row stride (elements)
   static constexpr int ES = EXPAND ? (WIDE ? 48 : 40) : XS; // hidden-chunk row stride
@@ -55,17 +72,19 @@ struct IrbGeom {
   static_assert(EXPAND || HID == 32, "t == 1 blocks are supported for 32 channels (MobileNet-V2 block 1)");
   static_assert(!RES || (S == 1 && CIN == COUT), "residual needs stride 1 and cin == cout");
   static_assert(NW * 64 >= SLAB / 4, "slab fill needs one float4 per thread");
+  static_assert(SLAB % 4 == 0 && (NCH_ * 32) % 4 == 0, "float4 slabs");
   static_assert(EPT <= 32, "validity mask is 32 bits");
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
 template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
-          bool DBUF>
+          bool DBUF, bool STW>
 __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const typename DT::T* __restrict__ X, const typename DT::T* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
     int tiles_y, uint32_t nwg) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF>;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
   using x4 = typename DT::x4;
@@ -73,7 +92,11 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   T* Xs = reinterpret_cast<T*>(smem);
   T* Es0 = Xs + G::PINP * G::XS;
   T* Es1 = Es0 + (G::NBUF == 2 ? G::PINP * G::ES : 0);
-  float* Sl = reinterpret_cast<float*>(Es0 + G::NBUF * G::PINP * G::ES);   // [3][SLAB]
+  T* WEs = Es0 + G::NBUF * G::PINP * G::ES;                                // [3][32][WES] expand weights
+  T* WPs = WEs + G::WE_ELEMS;                                               // [2][NCTP][WPS] project weights
+  float* Sl = reinterpret_cast<float*>(WPs + G::WP_ELEMS);                  // [2][SLAB] dw weights
+  float* Bd = Sl + 2 * G::SLAB;                                             // [HIDP] dw bias
+  float* Be = Bd + G::NCH * 32;                                             // [HIDP] expand bias
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
@@ -85,26 +108,53 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
 
-  // slab fill for chunk cc: thread t < SLAB/4 moves one float4 (dw weights, dw bias, expand bias)
+  // depthwise-weight slab of chunk cc: thread t < SLAB/4 moves one float4 of [9][32]
   auto slab_load = [&](int cc) -> float4 {
     float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
     if (tid < G::SLAB / 4 && cc < G::NCH) {
-      const int f = tid * 4;
-      if (f < 9 * 32) {
-        const int tap = f >> 5, ch = 32 * cc + (f & 31);
-        if (ch < HID) v = *reinterpret_cast<const float4*>(Wd + tap * HID + ch);
-      } else if (f < 9 * 32 + 32) {
-        const int ch = 32 * cc + (f - 9 * 32);
-        if (ch < HID) v = *reinterpret_cast<const float4*>(bd + ch);
-      } else if (EXPAND) {
-        const int ch = 32 * cc + (f - 9 * 32 - 32);
-        if (ch < HID) v = *reinterpret_cast<const float4*>(be + ch);
-      }
+      const int f = tid * 4, tap = f >> 5, ch = 32 * cc + (f & 31);
+      if (ch < HID) v = *reinterpret_cast<const float4*>(Wd + tap * HID + ch);
     }
     return v;
   };
   auto slab_store = [&](int cc, float4 v) {
-    if (tid < G::SLAB / 4) *reinterpret_cast<float4*>(Sl + (cc % 3) * G::SLAB + tid * 4) = v;
+    if (tid < G::SLAB / 4) *reinterpret_cast<float4*>(Sl + (cc & 1) * G::SLAB + tid * 4) = v;
+  };
+
+  // weight staging: pieces [0, WE_PIECES) = expand rows of chunk ce, then project rows of chunk cp
+  x8 wst[G::W_PPT > 0 ? G::W_PPT : 1];
+  auto wst_load = [&](int ce, int cp) {
+    if constexpr (STW) {
+#pragma unroll
+      for (int i = 0; i < G::W_PPT; ++i) {
+        const int p = tid + NW * 64 * i;
+        x8 v = zero8<DT>();
+        if (p < G::WE_PIECES) {
+          const int row = p / (G::WEK / 8), g = p - row * (G::WEK / 8);
+          const int h = 32 * ce + row;
+          if (ce < G::NCH && h < (HID + 15) / 16 * 16) v = load8<DT>(We + (size_t)h * G::WKP + 8 * g);
+        } else if (p < G::WE_PIECES + G::WP_PIECES) {
+          const int q = p - G::WE_PIECES, row = q >> 2, g = q & 3;
+          if (cp < G::NCH) v = load8<DT>(Wp + (size_t)row * G::HIDP + 32 * cp + 8 * g);
+        }
+        wst[i] = v;
+      }
+    }
+  };
+  auto wst_store = [&](int ce, int cp) {
+    if constexpr (STW) {
+#pragma unroll
+      for (int i = 0; i < G::W_PPT; ++i) {
+        const int p = tid + NW * 64 * i;
+        if (p < G::WE_PIECES) {
+          const int row = p / (G::WEK / 8), g = p - row * (G::WEK / 8);
+          *reinterpret_cast<x8*>(WEs + (ce % 3) * 32 * G::WES + row * G::WES + 8 * g) = wst[i];
+        } else if (p < G::WE_PIECES + G::WP_PIECES) {
+          const int q = p - G::WE_PIECES, row = q >> 2, g = q & 3;
+          *reinterpret_cast<x8*>(WPs + (cp & 1) * G::NCTP * G::WPS + row * G::WPS + 8 * g) = wst[i];
+        }
+      }
+    }
   };
 
   // ---- 1. stage the input tile (+halo) in LDS; outside the image (and K padding) -> 0
@@ -123,7 +173,16 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       *reinterpret_cast<x8*>(Xs + p * G::XS + g * 8) = v;
     }
     slab_store(0, slab_load(0));
+    if constexpr (STW && EXPAND) {   // expand weights of chunk 0 (the project weights of chunk 0 follow the schedule)
+      wst_load(0, G::NCH);
+      wst_store(0, 0);
+    }
+    for (int u = tid; u < G::NCH * 32; u += NW * 64) {   // all biases, once
+      Bd[u] = u < HID ? bd[u] : 0.f;
+      if constexpr (EXPAND) Be[u] = u < HID ? be[u] : 0.f;
+    }
   }
+  wst_load(1, 0);      // in flight across the first expand
   __syncthreads();
 
   // per-lane validity of its expand pixels (inside the tile and the image): the depthwise zero padding
@@ -158,8 +217,15 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
-    const float4 slab_next = slab_load(c + 1);     // issued now, stored after this chunk's expand
-    const float* sl = Sl + (c % 3) * G::SLAB;
+    const float4 slab_next = slab_load(c + 1);     // issued now, stored after this chunk's depthwise
+    const float* sl = Sl + (c & 1) * G::SLAB;
+    // project weight fragments of this chunk (no STW): issued before the expand so their latency hides under it
+    x8 pa[G::NCTW];
+    if constexpr (!STW) {
+      const T* wpp = Wp + (size_t)(wc * G::NCTW * 16 + r16) * G::HIDP + 32 * c + 8 * kg;
+#pragma unroll
+      for (int t = 0; t < G::NCTW; ++t) pa[t] = load8<DT>(wpp + (size_t)t * 16 * G::HIDP);
+    }
     const T* Es;
     if constexpr (EXPAND) {
       if constexpr (G::NBUF == 1) {
@@ -172,7 +238,19 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       constexpr int WKP = (CIN + 31) / 32 * 32;
       x8 a0[G::KS], a1[G::KS];
       x4 q0 = {}, q1 = {};
-      if constexpr (G::K16) {
+      if constexpr (STW) {
+        const T* w0 = WEs + (c % 3) * 32 * G::WES + r16 * G::WES;
+        if constexpr (G::K16) {
+          q0 = *reinterpret_cast<const x4*>(w0 + 4 * kg);
+          q1 = *reinterpret_cast<const x4*>(w0 + 16 * G::WES + 4 * kg);
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < G::KS; ++ks) {
+            a0[ks] = *reinterpret_cast<const x8*>(w0 + 32 * ks + 8 * kg);
+            a1[ks] = *reinterpret_cast<const x8*>(w0 + 16 * G::WES + 32 * ks + 8 * kg);
+          }
+        }
+      } else if constexpr (G::K16) {
         const T* w0 = We + (size_t)(32 * c + r16) * WKP + 4 * kg;
         q0 = *reinterpret_cast<const x4*>(w0);
         if (vh > 16) q1 = *reinterpret_cast<const x4*>(w0 + 16 * WKP);
@@ -184,8 +262,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
           a1[ks] = vh > 16 ? load8<DT>(w0 + 16 * WKP + 32 * ks) : zero8<DT>();
         }
       }
-      const float4 eb0 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 32 + 4 * kg);
-      const float4 eb1 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 32 + 16 + 4 * kg);
+      const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
+      const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
         const int pt = wave + NW * j;
@@ -222,15 +300,16 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     } else {
       Es = Xs;
     }
-    slab_store(c + 1, slab_next);
+    wst_store(c + 1, c);      // expand weights of chunk c+1, project weights of chunk c
     __syncthreads();
+    wst_load(c + 2, c + 1);   // next stage in flight across this depthwise/project and the next expand
+    if constexpr (STW) {
+      const T* wpp = WPs + (c & 1) * G::NCTP * G::WPS + (wc * G::NCTW * 16 + r16) * G::WPS + 8 * kg;
+#pragma unroll
+      for (int t = 0; t < G::NCTW; ++t) pa[t] = *reinterpret_cast<const x8*>(wpp + t * 16 * G::WPS);
+    }
 
     // ---- 3. depthwise 3x3 on this hidden chunk -> project B fragment in registers; 4. project MFMA
-    // project weights for this chunk first: their latency hides under the depthwise
-    x8 pa[G::NCTW];
-    const T* wpp = Wp + (size_t)(wc * G::NCTW * 16 + r16) * G::HIDP + 32 * c + 8 * kg;
-#pragma unroll
-    for (int t = 0; t < G::NCTW; ++t) pa[t] = load8<DT>(wpp + (size_t)t * 16 * G::HIDP);
     const bool hv = 32 * c + 8 * kg < HID;    // this lane's 8 hidden channels exist
 #pragma unroll
     for (int qi = 0; qi < G::QPW; ++qi) {
@@ -238,8 +317,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       if (hv) {
         float a8[8];
         {
-          const float4 u0 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 8 * kg);
-          const float4 u1 = *reinterpret_cast<const float4*>(sl + 9 * 32 + 8 * kg + 4);
+          const float4 u0 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg);
+          const float4 u1 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg + 4);
           a8[0] = u0.x; a8[1] = u0.y; a8[2] = u0.z; a8[3] = u0.w;
           a8[4] = u1.x; a8[5] = u1.y; a8[6] = u1.z; a8[7] = u1.w;
         }
@@ -266,6 +345,9 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
     }
+    // next chunk's depthwise weights: buffer (c+1)&1 was last read by dw(c-1), which every wave finished
+    // before the barrier of this chunk; the barrier of chunk c+1 publishes it before dw(c+1) reads it.
+    slab_store(c + 1, slab_next);
   }
 
   // ---- 5. epilogue: + bias (+ residual from the staged input tile) -> y (NHWC)
@@ -297,33 +379,55 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 // One instantiation per MobileNet-V2 block geometry: (cin, hidden, cout, stride, tile TH x TW, expand,
 // residual, waves, cout groups). Unknown geometries return hipErrorNotSupported -> the executor falls back
 // to the unfused kernels.
-#define SPEF_IRB_TABLE(X)                                                \
-  X(32, 32, 16, 1, 16, 16, false, false, 8, 1, true)    /* block 1      */ \
-  X(16, 96, 24, 2, 8, 8, true, false, 4, 1, false)      /* block 2      */ \
-  X(24, 144, 24, 1, 8, 16, true, true, 8, 1, true)      /* block 3      */ \
-  X(24, 144, 32, 2, 8, 8, true, false, 4, 1, false)     /* block 4      */ \
-  X(32, 192, 32, 1, 8, 16, true, true, 8, 1, true)      /* blocks 5-6   */ \
-  X(32, 192, 64, 2, 8, 8, true, false, 8, 2, false)     /* block 7      */ \
-  X(64, 384, 64, 1, 8, 16, true, true, 8, 1, true)      /* blocks 8-10  */ \
-  X(64, 384, 96, 1, 8, 16, true, false, 8, 1, true)     /* block 11     */ \
-  X(96, 576, 96, 1, 8, 16, true, true, 8, 1, true)      /* blocks 12-13 */ \
-  X(96, 576, 160, 2, 4, 8, true, false, 4, 2, true)     /* block 14     */ \
-  X(160, 960, 160, 1, 8, 8, true, true, 8, 2, true)     /* blocks 15-16 */ \
-  X(160, 960, 320, 1, 8, 8, true, false, 8, 2, true)    /* block 17     */
+// Variant 0 is the default; variants >= 1 are alternatives for tuning sweeps (spef_set_option
+// SPEF_OPT_IRB_VARIANT); a geometry without the requested variant uses variant 0.
+#define SPEF_IRB_TABLE(X)                                                   \
+  X(0, 32, 32, 16, 1, 16, 16, false, false, 8, 1, true, false)    /* block 1      */ \
+  X(1, 32, 32, 16, 1, 8, 16, false, false, 8, 1, true, false)                        \
+  X(0, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false)     /* block 2      */ \
+  X(1, 16, 96, 24, 2, 8, 8, true, false, 4, 1, false, false)                         \
+  X(0, 24, 144, 24, 1, 8, 16, true, true, 8, 1, false, false)     /* block 3      */ \
+  X(1, 24, 144, 24, 1, 8, 16, true, true, 8, 1, true, false)                         \
+  X(0, 24, 144, 32, 2, 8, 8, true, false, 4, 1, false, false)     /* block 4      */ \
+  X(1, 24, 144, 32, 2, 8, 16, true, false, 8, 1, false, false)                       \
+  X(0, 32, 192, 32, 1, 8, 16, true, true, 8, 1, false, false)     /* blocks 5-6   */ \
+  X(1, 32, 192, 32, 1, 8, 16, true, true, 8, 1, true, false)                         \
+  X(0, 32, 192, 64, 2, 8, 8, true, false, 8, 2, false, false)     /* block 7      */ \
+  X(1, 32, 192, 64, 2, 8, 8, true, false, 4, 1, false, false)                        \
+  X(0, 64, 384, 64, 1, 8, 16, true, true, 8, 1, false, true)     /* blocks 8-10  */ \
+  X(1, 64, 384, 64, 1, 8, 16, true, true, 8, 1, true, true)                          \
+  X(0, 64, 384, 96, 1, 8, 16, true, false, 8, 1, true, true)     /* block 11     */ \
+  X(1, 64, 384, 96, 1, 8, 16, true, false, 8, 1, false, true)                       \
+  X(0, 96, 576, 96, 1, 8, 16, true, true, 8, 1, true, true)      /* blocks 12-13 */ \
+  X(1, 96, 576, 96, 1, 8, 16, true, true, 8, 1, false, true)                        \
+  X(0, 96, 576, 160, 2, 4, 8, true, false, 4, 2, true, false)    /* block 14     */ \
+  X(1, 96, 576, 160, 2, 4, 8, true, false, 4, 2, true, true)                        \
+  X(0, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true)     /* blocks 15-16 */ \
+  X(1, 160, 960, 160, 1, 8, 8, true, true, 8, 2, false, true)                       \
+  X(0, 160, 960, 320, 1, 8, 8, true, false, 8, 2, false, true)   /* block 17     */ \
+  X(1, 160, 960, 320, 1, 8, 8, true, false, 8, 2, false, false)                      \
+  X(2, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, true)                         \
+  X(2, 24, 144, 24, 1, 8, 16, true, true, 8, 1, false, true)                         \
+  X(2, 24, 144, 32, 2, 8, 8, true, false, 4, 1, false, true)                         \
+  X(2, 32, 192, 32, 1, 8, 16, true, true, 8, 1, false, true)                         \
+  X(2, 32, 192, 64, 2, 8, 8, true, false, 8, 2, false, true)                         \
+  X(2, 64, 384, 64, 1, 8, 16, true, true, 8, 1, true, false)                         \
+  X(2, 96, 576, 96, 1, 8, 16, true, true, 8, 1, true, false)                         \
+  X(2, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, false)
 
 template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
-          bool DBUF>
+          bool DBUF, bool STW>
 static hipError_t irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                          hipStream_t s) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF>;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW>;
   using T = typename DT::T;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   const size_t lds = (size_t)G::LDS_BYTES;
-  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF>;
+  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW>;
   static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
   if (!attr_set && lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -335,34 +439,40 @@ static hipError_t irb_go(const void* x, const void* we, const float* be, const f
   return hipGetLastError();
 }
 
+static bool irb_has(int variant, int cin, int hid, int cout, int stride, bool expand, bool res) {
+#define SPEF_IRB_HAS(V, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_) \
+  if (variant == V && cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS) return true;
+  SPEF_IRB_TABLE(SPEF_IRB_HAS)
+#undef SPEF_IRB_HAS
+  return false;
+}
+
 template <typename DT>
-static hipError_t irb_dispatch(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
-                               const void* we, const float* be, const float* wd, const float* bd, const void* wp,
-                               const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
-#define SPEF_IRB_CASE(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_)                            \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)            \
-    return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
-                                                                      OW, s);
+static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stride, bool expand, bool res,
+                               const void* x, const void* we, const float* be, const float* wd, const float* bd,
+                               const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
+                               hipStream_t s) {
+  if (!irb_has(variant, cin, hid, cout, stride, expand, res)) variant = 0;
+#define SPEF_IRB_CASE(V, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_)                            \
+  if (variant == V && cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)   \
+    return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_>(x, we, be, wd, bd, wp, bp, y, B, H, W, \
+                                                                           OH, OW, s);
   SPEF_IRB_TABLE(SPEF_IRB_CASE)
 #undef SPEF_IRB_CASE
   return hipErrorNotSupported;
 }
 
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
-#define SPEF_IRB_HAS(CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_) \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS) return true;
-  SPEF_IRB_TABLE(SPEF_IRB_HAS)
-#undef SPEF_IRB_HAS
-  return false;
+  return irb_has(0, cin, hid, cout, stride, expand, res);
 }
 
-hipError_t launch_irb(int dtype, int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
-                      const void* we, const float* be, const float* wd, const float* bd, const void* wp,
+hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int stride, bool expand, bool res,
+                      const void* x, const void* we, const float* be, const float* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
-  return dtype == DT_F16
-             ? irb_dispatch<F16>(cin, hid, cout, stride, expand, res, x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s)
-             : irb_dispatch<BF16>(cin, hid, cout, stride, expand, res, x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW,
-                                  s);
+  return dtype == DT_F16 ? irb_dispatch<F16>(variant, cin, hid, cout, stride, expand, res, x, we, be, wd, bd, wp, bp,
+                                             y, B, H, W, OH, OW, s)
+                         : irb_dispatch<BF16>(0, cin, hid, cout, stride, expand, res, x, we, be, wd, bd, wp, bp, y, B,
+                                              H, W, OH, OW, s);
 }
 
 }  // namespace spef

@@ -47,6 +47,7 @@ struct spef_ctx {
   int fuse = 1;              // SPEF_OPT_FUSE_BLOCKS: 0 never, 1 when input H*W >= fuse_min_hw
   int64_t fuse_min_hw = 0;   // SPEF_OPT_FUSE_MIN_HW
   int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
+  int irb_variant = 0;       // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps)
   // per-launch HIP-event profiling (bench.py roofline leg)
   bool profiling = false;
   struct Rec {
@@ -247,7 +248,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         char key[96];
         snprintf(key, sizeof(key), "irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
-          return launch_irb(dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
+          return launch_irb(c->irb_variant, dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
                             ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
                             ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
         }));
@@ -565,6 +566,10 @@ int spef_set_option(spef_ctx* c, int option, int value) {
   }
   if (option == SPEF_OPT_FUSE_MIN_HW) {
     c->fuse_min_hw = value;
+    return SPEF_OK;
+  }
+  if (option == SPEF_OPT_IRB_VARIANT) {
+    c->irb_variant = value;
     return SPEF_OK;
   }
   if (option == SPEF_OPT_PW_GEMM) {

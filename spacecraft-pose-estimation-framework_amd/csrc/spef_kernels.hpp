@@ -39,7 +39,7 @@ hipError_t launch_fc(const float* x, const float* w, const float* bias, float* o
 
 // Fused InvertedResidual block (expand -> depthwise -> project [+x]) for the geometries in k_irb.hip's table.
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
-hipError_t launch_irb(int dtype, int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
+hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
                       const void* we, const float* be, const float* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 

@@ -47,6 +47,10 @@ def main():
     fr = torch.from_numpy(rng.integers(0, 256, (B, S, S, 3), dtype=np.uint8)).cuda()
     ori = torch.empty((B, 1728), device='cuda')
     pos = torch.empty((B, 3), device='cuda')
+    if os.environ.get('SWEEP'):
+        for v in (0, 1, 2):
+            run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 1, L.OPT_IRB_VARIANT: v}, label=f'fused variant {v}')
+        return
     ref = run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 0, L.OPT_PW_GEMM: 0}, label='unfused, direct pw')
     g = run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 0, L.OPT_PW_GEMM: 1}, label='unfused, LDS GEMM')
     print('gemm == direct:', torch.equal(ref[0], g[0]))
