@@ -18,14 +18,16 @@
 namespace spef {
 
 // ------------------------------------------------------------------------------------------ fc
-// out[b][i] = sum_k X[b][k] W[i][k] + bias[i]. Lane l loads float4 W[i0+(l&15)][t+4(l>>4)..] and
-// X[j0+(l&15)][t+4(l>>4)..]; MFMA step e takes element e from both, so A and B see the same k.
+// out[b][i] = sum_k X[b][k] W[i][k] + bias[i]. One workgroup per 16x16 output tile; its 4 waves take
+// interleaved quarters of K (split-K inside the workgroup, reduced through LDS in a fixed order, so the
+// result is deterministic). Lane l loads float4 W[i0+(l&15)][t+4(l>>4)..] and X[j0+(l&15)][t+4(l>>4)..];
+// MFMA step e takes element e from both, so A and B see the same k.
 __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, const float* __restrict__ W,
                                                  const float* __restrict__ bias, float* __restrict__ out0, int n0,
                                                  float* __restrict__ out1, int n1, int B, int K, int Np) {
+  __shared__ f32x4 part[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i0 = (blockIdx.x * 4 + wave) * 16;
-  if (i0 >= Np) return;
+  const int i0 = blockIdx.x * 16;
   const int j0 = blockIdx.y * 16;
   const int r16 = lane & 15, kg = lane >> 4;
   const float* wp = W + (size_t)(i0 + r16) * K + 4 * kg;
@@ -33,7 +35,7 @@ __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, co
   const bool jv = j < B;
   const float* xp = X + (size_t)(jv ? j : 0) * K + 4 * kg;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (int t = 0; t < K; t += 16) {
+  for (int t = 16 * wave; t < K; t += 64) {
     const float4 a = *reinterpret_cast<const float4*>(wp + t);
     float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
     if (jv) b = *reinterpret_cast<const float4*>(xp + t);
@@ -42,11 +44,14 @@ __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, co
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
   }
-  if (!jv) return;
+  part[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0 || !jv) return;
+  const f32x4 s = (part[0][lane] + part[1][lane]) + (part[2][lane] + part[3][lane]);
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int i = i0 + 4 * kg + r;
-    const float v = acc[r] + bias[i];
+    const float v = s[r] + bias[i];
     if (i < n0)
       out0[(size_t)j * n0 + i] = v;
     else if (i < n0 + n1)
@@ -219,7 +224,7 @@ hipError_t launch_fc(const float* x, const float* w, const float* bias, float* o
                      int K, hipStream_t s) {
   if (K % 16) return hipErrorInvalidValue;
   const int Np = (n0 + n1 + 15) & ~15;
-  dim3 g((Np / 16 + 3) / 4, (B + 15) / 16);
+  dim3 g(Np / 16, (B + 15) / 16);
   fc_kernel<<<g, 256, 0, s>>>(x, w, bias, out0, n0, out1, n1, B, K, Np);
   return hipGetLastError();
 }

@@ -1,0 +1,139 @@
+// Last ConvBnAct 320->1280 1x1 + ReLU (mobilenet_v2.py:264) fused with URSONetHead's x.mean([2,3])
+// (src/modeling/head/ursonet.py:30) as one LDS-tiled MFMA GEMM whose epilogue reduces over pixels.
+//
+// Workgroup = 8 waves (2 channel x 4 pixel) on one image x 128 output channels; pixel chunks of 256 are
+// looped inside the workgroup (any H*W), K = 320 advances 32 per double-buffered LDS step. ReLU(conv + b) is
+// summed in fp32 registers over the wave's pixel tiles, then over the 16 pixel lanes by shuffles and over the
+// 4 pixel waves through LDS: the 1280-channel map never exists in memory and the mean is deterministic.
+#include "spef_common.hpp"
+#include "spef_kernels.hpp"
+
+namespace spef {
+
+template <typename DT>
+__global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __restrict__ X,
+                                                        const typename DT::T* __restrict__ Wt,
+                                                        const float* __restrict__ bias, float* __restrict__ pooled,
+                                                        int HW, int K, int Kp, int N) {
+  using T = typename DT::T;
+  using x8 = typename DT::x8;
+  constexpr int NT = 4, MT = 4;                 // wave tile: 64 channels x 64 pixels
+  constexpr int BN = 2 * 16 * NT, BM = 4 * 16 * MT;   // 128 x 256
+  constexpr int RS = 48;                        // LDS row stride (96 B: conflict-free b128)
+  constexpr int XP = BM * 4 / 512, WP = BN * 4 / 512; // 16-B pieces per thread per K step
+  __shared__ __attribute__((aligned(16))) T As[2][BN * RS];
+  __shared__ __attribute__((aligned(16))) T Bs[2][BM * RS];
+  __shared__ float red[4][BN];
+
+  const int b = blockIdx.y, n0 = blockIdx.x * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  const int wn = wave & 1, wm = wave >> 1;
+  const T* Xb = X + (size_t)b * HW * K;
+  const int KS = Kp >> 5;
+
+  f32x4 bias4[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    const float4 t = *reinterpret_cast<const float4*>(bias + n0 + (wn * NT + a) * 16 + 4 * kg);
+    bias4[a] = f32x4{t.x, t.y, t.z, t.w};
+  }
+  f32x4 sum[NT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) sum[a] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  x8 xr[XP], wr[WP];
+  for (int m0 = 0; m0 < HW; m0 += BM) {
+    auto gload = [&](int ks) {
+#pragma unroll
+      for (int i = 0; i < XP; ++i) {
+        const int p = tid + 512 * i, row = p >> 2, g = p & 3, k = ks * 32 + 8 * g;
+        xr[i] = (m0 + row < HW && k < K) ? load8<DT>(Xb + (size_t)(m0 + row) * K + k) : zero8<DT>();
+      }
+#pragma unroll
+      for (int i = 0; i < WP; ++i) {
+        const int p = tid + 512 * i, row = p >> 2, g = p & 3;
+        wr[i] = load8<DT>(Wt + (size_t)(n0 + row) * Kp + ks * 32 + 8 * g);
+      }
+    };
+    auto lstore = [&](int buf) {
+#pragma unroll
+      for (int i = 0; i < XP; ++i) {
+        const int p = tid + 512 * i;
+        *reinterpret_cast<x8*>(&Bs[buf][(p >> 2) * RS + 8 * (p & 3)]) = xr[i];
+      }
+#pragma unroll
+      for (int i = 0; i < WP; ++i) {
+        const int p = tid + 512 * i;
+        *reinterpret_cast<x8*>(&As[buf][(p >> 2) * RS + 8 * (p & 3)]) = wr[i];
+      }
+    };
+    f32x4 acc[NT][MT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int q = 0; q < MT; ++q) acc[a][q] = bias4[a];
+    __syncthreads();   // previous chunk's LDS reads done
+    gload(0);
+    lstore(0);
+    __syncthreads();
+    for (int ks = 0; ks < KS; ++ks) {
+      const int buf = ks & 1;
+      if (ks + 1 < KS) gload(ks + 1);
+      x8 af[NT], bf[MT];
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+        af[a] = *reinterpret_cast<const x8*>(&As[buf][((wn * NT + a) * 16 + r16) * RS + 8 * kg]);
+#pragma unroll
+      for (int q = 0; q < MT; ++q)
+        bf[q] = *reinterpret_cast<const x8*>(&Bs[buf][((wm * MT + q) * 16 + r16) * RS + 8 * kg]);
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int q = 0; q < MT; ++q) acc[a][q] = DT::mfma(af[a], bf[q], acc[a][q]);
+      if (ks + 1 < KS) {
+        lstore(buf ^ 1);
+        __syncthreads();
+      }
+    }
+#pragma unroll
+    for (int q = 0; q < MT; ++q) {
+      const bool pv = m0 + (wm * MT + q) * 16 + r16 < HW;
+#pragma unroll
+      for (int a = 0; a < NT; ++a)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sum[a][e] += pv ? fmaxf(acc[a][q][e], 0.f) : 0.f;
+    }
+  }
+  // reduce over the 16 pixel lanes, then over the 4 pixel waves
+#pragma unroll
+  for (int a = 0; a < NT; ++a)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = sum[a][e];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      if (r16 == 0) red[wm][(wn * NT + a) * 16 + 4 * kg + e] = v;
+    }
+  __syncthreads();
+  if (tid < BN && n0 + tid < N) {
+    const float v = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    pooled[(size_t)b * N + n0 + tid] = v / (float)HW;
+  }
+}
+
+hipError_t launch_pool_gemm(int dtype, const void* x, const void* wt, const float* bias, float* pooled, int B, int HW,
+                            int K, int N, hipStream_t s) {
+  const int Kp = (K + 31) & ~31, Np = (N + 15) & ~15;
+  if ((K & 7) || (Np % 128)) return hipErrorInvalidValue;
+  dim3 g(Np / 128, B);
+  if (dtype == DT_F16)
+    pool_gemm_kernel<F16><<<g, 512, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
+  else
+    pool_gemm_kernel<BF16><<<g, 512, 0, s>>>((const __bf16*)x, (const __bf16*)wt, bias, pooled, HW, K, Kp, N);
+  return hipGetLastError();
+}
+
+}  // namespace spef

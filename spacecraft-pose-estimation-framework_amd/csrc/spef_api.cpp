@@ -288,11 +288,14 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
     } else if (op.kind == OP_LAST) {
       if (mode == 0) {
         const double M3 = (double)B * h * w;
-        HIP_TRY(prof_launch(c, s, "pw_pool_kernel<4>",
+        const bool tiled = c->gemm && ((op.cout + 15) & ~15u) % 128 == 0;
+        HIP_TRY(prof_launch(c, s, tiled ? "pool_gemm_kernel" : "pw_pool_kernel<4>",
                             M3 * op.cin * 2 + (double)op.cout * (op.cin * 2 + 4) + (double)B * op.cout * 4,
                             2.0 * M3 * op.cin * op.cout, [&] {
-          return launch_pw_pool(dt, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), c->pooled, B, h * w,
-                                (int)op.cin, (int)op.cout, s);
+          return tiled ? launch_pool_gemm(dt, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), c->pooled, B, h * w,
+                                          (int)op.cin, (int)op.cout, s)
+                       : launch_pw_pool(dt, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), c->pooled, B, h * w,
+                                        (int)op.cin, (int)op.cout, s);
         }));
       } else if (mode == 2) {
         void* y = pick({cur});

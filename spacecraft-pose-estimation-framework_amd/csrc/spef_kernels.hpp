@@ -32,6 +32,10 @@ hipError_t launch_dw(int dtype, const void* x, const float* w9, const float* bia
 hipError_t launch_pw_pool(int dtype, const void* x, const void* wt, const float* bias, float* pooled, int B,
                           int HW, int K, int N, hipStream_t s);
 
+// Same contract, LDS-tiled GEMM with a pixel-reducing epilogue (k_pool.hip); needs round_up(N,16) % 128 == 0.
+hipError_t launch_pool_gemm(int dtype, const void* x, const void* wt, const float* bias, float* pooled, int B, int HW,
+                            int K, int N, hipStream_t s);
+
 // fp32 head GEMM (f32-input MFMA): out[b][i] = sum_k X[b][k] W[i][k] + bias[i], columns [0,n0) -> out0,
 // [n0, n0+n1) -> out1. W fp32 [Np][K], K % 16 == 0.
 hipError_t launch_fc(const float* x, const float* w, const float* bias, float* out0, int n0, float* out1, int n1,
