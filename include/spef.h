@@ -95,6 +95,17 @@ int spef_set_decode_tables(spef_ctx* ctx, const double* ori_bins, int n_ori_bins
 int spef_decode(spef_ctx* ctx, int ori_mode, int pos_mode, const float* ori_raw, const float* pos_raw, int B,
                 float* ori_soft, float* quat, float* pos_soft, float* pos, int* status, void* stream);
 
+/* Keypoint mode (ORI == POS == 'keypoints', config.py:53-58): the 3-D model points (host float32 n x 3,
+ * e.g. tangoPoints.mat's 11 Tango keypoints, keypoints_utils.py:31-45), the camera matrix (host float64
+ * 3x3 row-major) and the image size the keypoints are normalised by (Camera nu, nv; speed.py:18-32). */
+int spef_set_keypoints(spef_ctx* ctx, const float* kp3d, int n, const double* K, float nu, float nv);
+
+/* SPEUtils.last_activ (sigmoid, spe_utils.py:68) + KeyPoints.decode_batch (keypoints_utils.py:152-174):
+ * raw [B x 2(n+1)] (origin + n keypoints) -> optional kp_out (sigmoid values, same shape), quat [B x 4],
+ * pos [B x 3] by batched EPnP (cv2.SOLVEPNP_EPNP semantics) + dcm2quat. status bit 8 = EPnP failure. */
+int spef_decode_keypoints(spef_ctx* ctx, const float* raw, int B, int apply_sigmoid, float* kp_out, float* quat,
+                          float* pos, int* status, void* stream);
+
 /* Options. SPEF_OPT_FUSE_BLOCKS (default 1): run each inverted-residual block as one fused kernel
  * (expand + depthwise + project on-chip) where its geometry is in the fused table; 0 = one kernel per conv. */
 /* SPEF_OPT_FUSE_MIN_HW: fuse only blocks whose input has at least this many pixels per image (late,

@@ -109,9 +109,13 @@ __global__ __launch_bounds__(256) void gemm_pw_kernel(const typename DT::T* __re
       const int64_t m = mt0 + (wm * MT + b) * 16 + r16;
       if (m >= M) continue;
       f32x4 v = acc[a][b];
-      if (EPI == EPI_RELU) {
+      if (EPI == EPI_RELU || EPI == EPI_RELU_F32) {
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.0f);
+      }
+      if constexpr (EPI == EPI_RELU_F32) {   // fp32 feature map (keypoint head / backbone export)
+        *reinterpret_cast<float4*>(reinterpret_cast<float*>(Y) + (size_t)m * N + i) = make_float4(v[0], v[1], v[2], v[3]);
+        continue;
       }
       if (EPI == EPI_RES) {
         const x4 rr = *reinterpret_cast<const x4*>(R + (size_t)m * N + i);
@@ -142,6 +146,9 @@ static hipError_t gemm_go(int epi, const void* x, const void* wt, const float* b
   if (epi == EPI_RELU)
     gemm_pw_kernel<DT, WN, NT, MT, EPI_RELU><<<nwg, 256, 0, s>>>(X, W, bias, nullptr, (T*)y, M, K, N, Kp, Np,
                                                                   n_chunks, nwg);
+  else if (epi == EPI_RELU_F32)
+    gemm_pw_kernel<DT, WN, NT, MT, EPI_RELU_F32><<<nwg, 256, 0, s>>>(X, W, bias, nullptr, (T*)y, M, K, N, Kp, Np,
+                                                                      n_chunks, nwg);
   else if (epi == EPI_RES)
     gemm_pw_kernel<DT, WN, NT, MT, EPI_RES><<<nwg, 256, 0, s>>>(X, W, bias, (const T*)r, (T*)y, M, K, N, Kp, Np,
                                                                  n_chunks, nwg);

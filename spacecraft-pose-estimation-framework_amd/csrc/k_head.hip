@@ -59,6 +59,47 @@ __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, co
   }
 }
 
+// Split-K form for very long K (KeypointRegressionHead: K = 1280*8*12 = 122880, keypoints.py:20): grid.z
+// slices of K write fp32 partial tiles, fc_reduce_kernel sums them in slice order (deterministic).
+__global__ __launch_bounds__(256) void fc_partial_kernel(const float* __restrict__ X, const float* __restrict__ W,
+                                                         float* __restrict__ part, int B, int K, int Np, int kslice) {
+  __shared__ f32x4 red[4][64];
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16, z = blockIdx.z;
+  const int r16 = lane & 15, kg = lane >> 4;
+  const int j = j0 + r16;
+  const bool jv = j < B;
+  const float* wp = W + (size_t)(i0 + r16) * K + 4 * kg;
+  const float* xp = X + (size_t)(jv ? j : 0) * K + 4 * kg;
+  const int k0 = z * kslice, k1 = min(K, k0 + kslice);
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (int t = k0 + 16 * wave; t < k1; t += 64) {
+    const float4 a = *reinterpret_cast<const float4*>(wp + t);
+    float4 b = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (jv) b = *reinterpret_cast<const float4*>(xp + t);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.x, b.x, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.y, b.y, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.z, b.z, acc, 0, 0, 0);
+    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a.w, b.w, acc, 0, 0, 0);
+  }
+  red[wave][lane] = acc;
+  __syncthreads();
+  if (wave != 0 || !jv) return;
+  const f32x4 s = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+  float* o = part + ((size_t)z * B + j) * Np + i0 + 4 * kg;
+  *reinterpret_cast<float4*>(o) = make_float4(s[0], s[1], s[2], s[3]);
+}
+
+__global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __restrict__ bias,
+                                 float* __restrict__ out, int n, int B, int Np, int splits) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= B * n) return;
+  const int j = idx / n, i = idx - j * n;
+  float v = bias[i];
+  for (int z = 0; z < splits; ++z) v += part[((size_t)z * B + j) * Np + i];
+  out[(size_t)j * n + i] = v;
+}
+
 // ------------------------------------------------------------------------------------------ reductions
 __device__ __forceinline__ float block_max256(float v, float* sh) {
   v = warp_max(v);
@@ -226,6 +267,19 @@ hipError_t launch_fc(const float* x, const float* w, const float* bias, float* o
   const int Np = (n0 + n1 + 15) & ~15;
   dim3 g(Np / 16, (B + 15) / 16);
   fc_kernel<<<g, 256, 0, s>>>(x, w, bias, out0, n0, out1, n1, B, K, Np);
+  return hipGetLastError();
+}
+
+hipError_t launch_fc_splitk(const float* x, const float* w, const float* bias, float* out, int n, int B, int K,
+                            int splits, float* part, hipStream_t s) {
+  if (K % 16) return hipErrorInvalidValue;
+  const int Np = (n + 15) & ~15;
+  int kslice = (K + splits - 1) / splits;
+  kslice = (kslice + 63) / 64 * 64;
+  splits = (K + kslice - 1) / kslice;
+  dim3 g(Np / 16, (B + 15) / 16, splits);
+  fc_partial_kernel<<<g, 256, 0, s>>>(x, w, part, B, K, Np, kslice);
+  fc_reduce_kernel<<<(B * n + 255) / 256, 256, 0, s>>>(part, bias, out, n, B, Np, splits);
   return hipGetLastError();
 }
 

@@ -5,7 +5,10 @@
 #include "../../include/spef.h"
 
 #include <hip/hip_runtime.h>
+#include <math.h>
 #include <string.h>
+
+#include <algorithm>
 
 #include <string>
 #include <vector>
@@ -16,6 +19,7 @@
 using namespace spef;
 
 static thread_local std::string g_err;
+static const int kKpSplits = 60;   // split-K slices of the keypoint head (K = 122880 -> 2048 per slice)
 
 static int fail(int code, const std::string& msg) {
   g_err = msg;
@@ -39,6 +43,14 @@ struct spef_ctx {
   size_t buf_bytes = 0;
   void* buf[4] = {nullptr, nullptr, nullptr, nullptr};
   float* pooled = nullptr;  // [B][1280] fp32
+  float* kpfeat = nullptr;  // keypoint head: fp32 NHWC feature map [B][fh*fw*1280]
+  float* kppart = nullptr;  // keypoint head: split-K partials
+  // keypoint decode configuration (KeyPoints, keypoints_utils.py:19-45; Camera, speed.py:18-32)
+  float* kp3d = nullptr;
+  double* kp_model = nullptr;  // control points [4][3] + alphas [n][4] (fp64, computed once on the host)
+  int kp_n = 0;
+  double camK[9] = {0};
+  float cam_nu = 0.f, cam_nv = 0.f;
   // decode tables
   double* d_ori_bins = nullptr;
   int n_ori_bins = 0;
@@ -177,7 +189,7 @@ int check_ready(spef_ctx* c, int B, int H, int W) {
 // Runs the backbone. mode: 0 = full (pool into c->pooled), 1 = stop after op `stop` and leave the
 // activation in *out_buf, 2 = unfused last conv (feature map in *out_buf).
 int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W, hipStream_t s, int mode,
-                 int stop, void** out_buf, int* oc, int* oh, int* ow) {
+                 int stop, void** out_buf, int* oc, int* oh, int* ow, float* feat_f32 = nullptr) {
   const int dt = (int)c->hdr.dtype;
   void* cur = nullptr;
   int h = H, w = W, ch = 3;
@@ -297,6 +309,14 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
                        : launch_pw_pool(dt, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), c->pooled, B, h * w,
                                         (int)op.cin, (int)op.cout, s);
         }));
+      } else if (mode == 2 && feat_f32) {   // fp32 feature map straight from the GEMM epilogue
+        HIP_TRY(prof_launch(c, s, gemm_key(dt, EPI_RELU_F32, op.cout), pw_bytes(B * h * w, op.cin, op.cout, false) +
+                            (double)B * h * w * op.cout * 2, 2.0 * B * h * w * op.cin * op.cout, [&] {
+          return launch_gemm_pw(dt, EPI_RELU_F32, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, feat_f32,
+                                (int64_t)B * h * w, (int)op.cin, (int)op.cout, s);
+        }));
+        cur = feat_f32;
+        ch = (int)op.cout;
       } else if (mode == 2) {
         void* y = pick({cur});
         HIP_TRY(pw_any(c, dt, EPI_RELU, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, y,
@@ -323,6 +343,10 @@ void free_workspace(spef_ctx* c) {
   }
   if (c->pooled) hipFree(c->pooled);
   c->pooled = nullptr;
+  if (c->kpfeat) hipFree(c->kpfeat);
+  c->kpfeat = nullptr;
+  if (c->kppart) hipFree(c->kppart);
+  c->kppart = nullptr;
   c->ws_B = c->ws_H = c->ws_W = 0;
   c->buf_bytes = 0;
 }
@@ -357,6 +381,8 @@ int spef_destroy(spef_ctx* c) {
   if (c->d_data) hipFree(c->d_data);
   if (c->d_ori_bins) hipFree(c->d_ori_bins);
   if (c->d_pos_grid) hipFree(c->d_pos_grid);
+  if (c->kp3d) hipFree(c->kp3d);
+  if (c->kp_model) hipFree(c->kp_model);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
   delete c;
   return SPEF_OK;
@@ -444,6 +470,10 @@ int spef_reserve(spef_ctx* c, int B, int H, int W) {
   const size_t bytes = (size_t)per_img * B * elem_size(c) + 256;
   for (void*& b : c->buf) HIP_TRY(hipMalloc(&b, bytes));
   HIP_TRY(hipMalloc(&c->pooled, (size_t)B * c->hdr.feat_c * sizeof(float)));
+  if (c->hdr.head == HEAD_KEYPOINTS) {
+    HIP_TRY(hipMalloc(&c->kpfeat, (size_t)B * fh * fw * c->hdr.feat_c * sizeof(float)));
+    HIP_TRY(hipMalloc(&c->kppart, (size_t)kKpSplits * B * ((c->hdr.n_out0 + 15) & ~15u) * sizeof(float)));
+  }
   c->buf_bytes = bytes;
   c->ws_B = B;
   c->ws_H = H;
@@ -472,13 +502,22 @@ int spef_forward(spef_ctx* c, const void* input, int layout, int B, int H, int W
         }));
     return SPEF_OK;
   }
-  // keypoint head: flatten of the (unpooled) 1280 x fh x fw map, then one Linear
+  // keypoint head (keypoints.py:24-27): flatten of the unpooled 1280 x fh x fw map -> Linear(122880, 24).
+  // The blob stores the weight columns in NHWC flatten order, so the NHWC map is used as is.
   void* feat = nullptr;
   int fc_ = 0, fh = 0, fw = 0;
-  rc = run_backbone(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw);
+  rc = run_backbone(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw, c->kpfeat);
   if (rc) return rc;
-  (void)feat;
-  return fail(SPEF_ERR_STATE, "keypoint head not implemented in this build");
+  const int64_t F = (int64_t)fh * fw * fc_;
+  for (const OpDesc& op : c->ops)
+    if (op.kind == OP_FCKP) {
+      if ((int64_t)op.cin != F) return fail(SPEF_ERR_ARG, "keypoint head size does not match the feature map");
+      HIP_TRY(prof_launch(c, s, "fc_splitk_kernel", ((double)B + op.cout) * F * 4, 2.0 * B * F * op.cout, [&] {
+        return launch_fc_splitk(c->kpfeat, ptr<float>(c, op.w0), ptr<float>(c, op.b0), out0, (int)op.cout, B, (int)F,
+                                kKpSplits, c->kppart, s);
+      }));
+    }
+  return SPEF_OK;
 }
 
 int spef_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W, float* features, void* stream) {
@@ -489,9 +528,8 @@ int spef_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int 
   hipStream_t s = (hipStream_t)stream;
   void* feat = nullptr;
   int fc_ = 0, fh = 0, fw = 0;
-  rc = run_backbone(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw);
+  rc = run_backbone(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw, features);
   if (rc) return rc;
-  HIP_TRY(launch_to_f32((int)c->hdr.dtype, feat, features, (int64_t)B * fh * fw * fc_, s));
   return SPEF_OK;
 }
 
@@ -544,7 +582,10 @@ int spef_decode(spef_ctx* c, int ori_mode, int pos_mode, const float* ori_raw, c
   HIP_TRY(hipMemsetAsync(status, 0, sizeof(int) * B, s));
   if (ori_mode == SPEF_CLASSIFICATION) {
     if (!c->d_ori_bins) return fail(SPEF_ERR_STATE, "orientation bins not set (spef_set_decode_tables)");
-    HIP_TRY(launch_decode_ori(ori_raw, B, c->n_ori_bins, c->d_ori_bins, ori_soft, quat, status, s));
+    HIP_TRY(prof_launch(c, s, "decode_ori_kernel", (double)B * c->n_ori_bins * (ori_soft ? 8 : 4) + 32.0 * c->n_ori_bins,
+                        (double)B * c->n_ori_bins * 30, [&] {
+      return launch_decode_ori(ori_raw, B, c->n_ori_bins, c->d_ori_bins, ori_soft, quat, status, s);
+    }));
   } else if (ori_mode == SPEF_REGRESSION) {
     HIP_TRY(launch_normalize_ori(ori_raw, B, quat, s));
   } else {
@@ -558,6 +599,122 @@ int spef_decode(spef_ctx* c, int ori_mode, int pos_mode, const float* ori_raw, c
   } else {
     return fail(SPEF_ERR_ARG, "pos_mode must be regression or classification");
   }
+  return SPEF_OK;
+}
+
+int spef_set_keypoints(spef_ctx* c, const float* kp3d, int n, const double* K, float nu, float nv) {
+  if (!c || !kp3d || !K || n < 4 || n > 16) return fail(SPEF_ERR_ARG, "bad keypoint configuration");
+  Dev d(c->device);
+  if (c->kp3d) hipFree(c->kp3d);
+  if (c->kp_model) hipFree(c->kp_model);
+  c->kp3d = nullptr;
+  c->kp_model = nullptr;
+  HIP_TRY(hipMalloc(&c->kp3d, sizeof(float) * 3 * n));
+  HIP_TRY(hipMemcpy(c->kp3d, kp3d, sizeof(float) * 3 * n, hipMemcpyHostToDevice));
+  // epnp.cpp choose_control_points + compute_barycentric_coordinates depend only on the 3-D model: do them
+  // once here (fp64). PCA axis signs are canonical (largest-|component| positive; oracle/epnp_ref.py too).
+  std::vector<double> model(12 + 4 * (size_t)n);
+  {
+    double pw[16][3], c0[3] = {0, 0, 0};
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < 3; ++j) {
+        pw[i][j] = (double)kp3d[3 * i + j];
+        c0[j] += pw[i][j] / n;
+      }
+    double a[3][3] = {}, v[3][3] = {{1, 0, 0}, {0, 1, 0}, {0, 0, 1}};
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < 3; ++j)
+        for (int k = 0; k < 3; ++k) a[j][k] += (pw[i][j] - c0[j]) * (pw[i][k] - c0[k]);
+    for (int sweep = 0; sweep < 50; ++sweep) {
+      double off = a[0][1] * a[0][1] + a[0][2] * a[0][2] + a[1][2] * a[1][2];
+      if (off < 1e-40) break;
+      for (int p = 0; p < 2; ++p)
+        for (int q = p + 1; q < 3; ++q) {
+          if (fabs(a[p][q]) < 1e-300) continue;
+          const double th = (a[q][q] - a[p][p]) / (2 * a[p][q]);
+          const double t = (th >= 0 ? 1.0 : -1.0) / (fabs(th) + sqrt(th * th + 1));
+          const double cs = 1 / sqrt(t * t + 1), sn = t * cs;
+          for (int k = 0; k < 3; ++k) {
+            const double x = a[k][p], y = a[k][q];
+            a[k][p] = cs * x - sn * y;
+            a[k][q] = sn * x + cs * y;
+          }
+          for (int k = 0; k < 3; ++k) {
+            const double x = a[p][k], y = a[q][k];
+            a[p][k] = cs * x - sn * y;
+            a[q][k] = sn * x + cs * y;
+          }
+          for (int k = 0; k < 3; ++k) {
+            const double x = v[k][p], y = v[k][q];
+            v[k][p] = cs * x - sn * y;
+            v[k][q] = sn * x + cs * y;
+          }
+        }
+    }
+    int ord[3] = {0, 1, 2};
+    for (int i = 0; i < 3; ++i)
+      for (int j = i + 1; j < 3; ++j)
+        if (a[ord[j]][ord[j]] > a[ord[i]][ord[i]]) std::swap(ord[i], ord[j]);
+    double cws[4][3];
+    for (int j = 0; j < 3; ++j) cws[0][j] = c0[j];
+    for (int i = 1; i < 4; ++i) {
+      const int e = ord[i - 1];
+      int big = 0;
+      for (int j = 1; j < 3; ++j)
+        if (fabs(v[j][e]) > fabs(v[big][e])) big = j;
+      const double sgn = v[big][e] >= 0 ? 1.0 : -1.0;
+      const double k = sqrt(std::max(a[e][e], 0.0) / n);
+      for (int j = 0; j < 3; ++j) cws[i][j] = c0[j] + k * sgn * v[j][e];
+    }
+    double cc[3][3];
+    for (int i = 0; i < 3; ++i)
+      for (int j = 1; j < 4; ++j) cc[i][j - 1] = cws[j][i] - cws[0][i];
+    const double det = cc[0][0] * (cc[1][1] * cc[2][2] - cc[1][2] * cc[2][1]) -
+                       cc[0][1] * (cc[1][0] * cc[2][2] - cc[1][2] * cc[2][0]) +
+                       cc[0][2] * (cc[1][0] * cc[2][1] - cc[1][1] * cc[2][0]);
+    if (fabs(det) < 1e-300) return fail(SPEF_ERR_ARG, "degenerate 3-D keypoint model");
+    double ci[3][3];
+    ci[0][0] = (cc[1][1] * cc[2][2] - cc[1][2] * cc[2][1]) / det;
+    ci[0][1] = (cc[0][2] * cc[2][1] - cc[0][1] * cc[2][2]) / det;
+    ci[0][2] = (cc[0][1] * cc[1][2] - cc[0][2] * cc[1][1]) / det;
+    ci[1][0] = (cc[1][2] * cc[2][0] - cc[1][0] * cc[2][2]) / det;
+    ci[1][1] = (cc[0][0] * cc[2][2] - cc[0][2] * cc[2][0]) / det;
+    ci[1][2] = (cc[0][2] * cc[1][0] - cc[0][0] * cc[1][2]) / det;
+    ci[2][0] = (cc[1][0] * cc[2][1] - cc[1][1] * cc[2][0]) / det;
+    ci[2][1] = (cc[0][1] * cc[2][0] - cc[0][0] * cc[2][1]) / det;
+    ci[2][2] = (cc[0][0] * cc[1][1] - cc[0][1] * cc[1][0]) / det;
+    for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 3; ++j) model[3 * i + j] = cws[i][j];
+    for (int i = 0; i < n; ++i) {
+      double al[3];
+      for (int j = 0; j < 3; ++j)
+        al[j] = ci[j][0] * (pw[i][0] - cws[0][0]) + ci[j][1] * (pw[i][1] - cws[0][1]) + ci[j][2] * (pw[i][2] - cws[0][2]);
+      model[12 + 4 * i + 0] = 1.0 - al[0] - al[1] - al[2];
+      model[12 + 4 * i + 1] = al[0];
+      model[12 + 4 * i + 2] = al[1];
+      model[12 + 4 * i + 3] = al[2];
+    }
+  }
+  HIP_TRY(hipMalloc(&c->kp_model, sizeof(double) * model.size()));
+  HIP_TRY(hipMemcpy(c->kp_model, model.data(), sizeof(double) * model.size(), hipMemcpyHostToDevice));
+  c->kp_n = n;
+  memcpy(c->camK, K, sizeof(c->camK));
+  c->cam_nu = nu;
+  c->cam_nv = nv;
+  return SPEF_OK;
+}
+
+int spef_decode_keypoints(spef_ctx* c, const float* raw, int B, int apply_sigmoid, float* kp_out, float* quat,
+                          float* pos, int* status, void* stream) {
+  if (!c || !raw || !quat || !pos || !status || B <= 0) return fail(SPEF_ERR_ARG, "null argument");
+  if (!c->kp3d) return fail(SPEF_ERR_STATE, "keypoints not configured (spef_set_keypoints)");
+  Dev d(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  HIP_TRY(hipMemsetAsync(status, 0, sizeof(int) * B, s));
+  HIP_TRY(prof_launch(c, s, "epnp_kernel", (double)B * (2 * (c->kp_n + 1) * 8 + 28), (double)B * 1.0e5, [&] {
+    return launch_epnp(raw, B, c->kp_n, c->kp3d, c->kp_model, c->camK, c->cam_nu, c->cam_nv, apply_sigmoid, kp_out,
+                       quat, pos, status, s);
+  }));
   return SPEF_OK;
 }
 

@@ -7,7 +7,7 @@
 namespace spef {
 
 enum Dtype : int { DT_F16 = 1, DT_BF16 = 2 };
-enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2 };
+enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RELU_F32 = 3 /* ReLU, fp32 output */ };
 enum InLayout : int { IN_U8_NHWC = 0, IN_F32_NCHW = 1 };
 
 // Stem ConvBnAct 3->32, 3x3, stride 2, pad 1, BN folded, ReLU. W: fp32 [27][32] (k = ky*9+kx*3+ci).
@@ -50,6 +50,17 @@ hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int st
 // Stem (u8 NHWC input) fused with inverted-residual block 1 (32 -> dw -> 16), k_front.hip.
 hipError_t launch_front(int dtype, const void* x, const float* ws, const float* bs, const float* wd, const float* bd,
                         const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
+
+// Split-K fp32 head GEMM for very long K: part = workspace [splits][B][round_up(n,16)] floats.
+hipError_t launch_fc_splitk(const float* x, const float* w, const float* bias, float* out, int n, int B, int K,
+                            int splits, float* part, hipStream_t s);
+
+// Keypoint decode: sigmoid (optional) + EPnP + dcm2quat per problem (k_epnp.hip). raw: B x 2(n+1) (origin +
+// n keypoints, normalised x,y); kp3d: n x 3 fp32 (device); K: host 3x3 row-major. status |= 8 on failure.
+// model = control points [4][3] + alphas [n][4] (fp64, device), computed once by spef_set_keypoints.
+hipError_t launch_epnp(const float* raw, int B, int n, const float* kp3d, const double* model, const double* K,
+                       float nu, float nv, int apply_sigmoid, float* kp_out, float* quat, float* pos, int* status,
+                       hipStream_t s);
 
 // Activation dtype -> fp32 NHWC copy (debug probes / backbone feature export).
 hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStream_t s);

@@ -133,6 +133,24 @@ class Engine:
     def set_option(self, option: int, value: int) -> None:
         L.check(self.lib.spef_set_option(self.ctx, option, int(value)))
 
+    def set_keypoints(self, kp3d: np.ndarray, K: np.ndarray, nu: float, nv: float) -> None:
+        kp = np.ascontiguousarray(kp3d, np.float32)
+        kk = np.ascontiguousarray(K, np.float64).reshape(9)
+        L.check(self.lib.spef_set_keypoints(self.ctx, kp.ctypes.data_as(C.c_void_p), kp.shape[0],
+                                            kk.ctypes.data_as(C.c_void_p), float(nu), float(nv)))
+        self._kp = (kp, kk)
+
+    def decode_keypoints(self, raw: torch.Tensor, apply_sigmoid: bool = True):
+        B = raw.shape[0]
+        dev = self.device
+        kp = torch.empty_like(raw)
+        quat = torch.empty((B, 4), dtype=torch.float32, device=dev)
+        pos = torch.empty((B, 3), dtype=torch.float32, device=dev)
+        status = torch.empty((B,), dtype=torch.int32, device=dev)
+        L.check(self.lib.spef_decode_keypoints(self.ctx, _ptr(raw), B, 1 if apply_sigmoid else 0, _ptr(kp), _ptr(quat),
+                                               _ptr(pos), _ptr(status), _stream(dev)))
+        return {'keypoints': kp, 'ori': quat, 'pos': pos, 'status': status}
+
     # ------------------------------------------------------------------ profiling
     def profile_begin(self) -> None:
         L.check(self.lib.spef_profile_begin(self.ctx))

@@ -71,7 +71,12 @@ class SPEUtils:
         self.ori_mode, self.pos_mode, self.camera = ori_mode, pos_mode, camera
         self.orientation = OrientationHistogram(n_ori_bins_per_dim, ori_smooth_factor, ori_delete_unused_bins)
         self.position = PositionHistogram(n_pos_bins_per_dim, pos_smooth_factor)
-        self.keypoints = keypoints_path
+        # KeyPoints(camera, path) like the reference (spe_utils.py:54); a ready KeyPoints object is accepted too
+        if keypoints_path is None or hasattr(keypoints_path, 'keypoints3d'):
+            self.keypoints = keypoints_path
+        else:
+            from .keypoints import KeyPoints
+            self.keypoints = KeyPoints(camera, keypoints_path)
 
     @staticmethod
     def get_score(true_pose: dict, pred_pose: dict) -> dict:

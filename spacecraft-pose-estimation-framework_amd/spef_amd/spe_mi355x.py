@@ -56,8 +56,19 @@ class SPEMi355x:
             self.engine = Engine(model, self.device)
         su = self.spe_utils
         self.ori_mode, self.pos_mode = _MODES[su.ori_mode], _MODES[su.pos_mode]
-        if self.ori_mode == L.KEYPOINTS:
-            raise NotImplementedError('keypoint (EPnP) mode is not available in this build')
+        self.keypoint_mode = self.ori_mode == L.KEYPOINTS and self.pos_mode == L.KEYPOINTS
+        if (self.ori_mode == L.KEYPOINTS) != (self.pos_mode == L.KEYPOINTS):
+            raise ValueError('keypoints mode must be used for both orientation and position')  # spe_utils.py:66
+        if self.keypoint_mode:
+            kp = su.keypoints
+            if kp is None:
+                raise ValueError('keypoints mode needs SPEUtils.keypoints (a KeyPoints with keypoints3d)')
+            cam = kp.camera
+            self.engine.set_keypoints(np.asarray(kp.keypoints3d, np.float32), np.asarray(cam.K, np.float64),
+                                      float(cam.nu), float(cam.nv))
+            assert self.engine.n_out0 == 2 * (kp.keypoints3d.shape[0] + 1), \
+                f'keypoint head width {self.engine.n_out0} != 2 * (n_keypoints + 1)'   # model.py:236
+            return
         ori_bins = su.orientation.histogram if self.ori_mode == L.CLASSIFICATION else None
         pos_grid = su.position.histogram if self.pos_mode == L.CLASSIFICATION else None
         self.engine.set_decode_tables(ori_bins, pos_grid)
@@ -79,6 +90,8 @@ class SPEMi355x:
     # ------------------------------------------------------------------ inference
     def _run(self, x: torch.Tensor):
         raw0, raw1 = self.engine.forward(x)
+        if self.keypoint_mode:   # sigmoid + batched EPnP on the GPU (spe_utils.py:66-68, keypoints_utils.py:152)
+            return raw0, None, self.engine.decode_keypoints(raw0, apply_sigmoid=True)
         return raw0, raw1, self.engine.decode(self.ori_mode, self.pos_mode, raw0, raw1)
 
     def predict(self, images: torch.Tensor, num_predict: int = 1) -> Tuple[Dict, float]:
@@ -101,6 +114,12 @@ class SPEMi355x:
             raise ValueError('Encoded position vector sum is zero, cannot decode.')     # :254
         if np.any(status & 4):
             raise ValueError('Error during position decoding, NaN found in decoded position.')  # :263
+        if np.any(status & 8):
+            raise ValueError('EPnP failed on a batch row (degenerate keypoints)')   # cv2.solvePnP error analogue
+
+        if self.keypoint_mode:
+            return {'keypoints': dec['keypoints'].cpu().numpy(), 'ori': dec['ori'].cpu().numpy(),
+                    'pos': dec['pos'].cpu().numpy()}, latency_ms
 
         pose = {'ori': dec['ori'].cpu().numpy(), 'pos': dec['pos'].cpu().numpy()}
         if self.ori_mode == L.CLASSIFICATION:

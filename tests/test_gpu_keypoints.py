@@ -1,0 +1,100 @@
+"""GPU keypoint mode: batched EPnP kernel and the keypoint-regression head vs the CPU oracle."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import decode_ref as D
+from oracle import epnp_ref as E
+from oracle import model_ref as M
+from spef_amd import blob as Bl
+from spef_amd.arch import mobilenet_v2
+from spef_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def kp_engine():
+    from spef_amd.engine import Engine
+    sd = synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=0.002)
+    e = Engine(Bl.pack(sd, mobilenet_v2('keypoints'), dtype='fp16'), 'cuda:0')
+    yield e, sd
+    e.close()
+
+
+def _cfg(engine, golden):
+    g = golden('keypoints.npz')
+    engine.set_keypoints(g['kp3d'], g['K'], float(g['nu']), float(g['nv']))
+    return g
+
+
+def test_epnp_noise_free_kat(kp_engine, golden):
+    eng, _ = kp_engine
+    g = _cfg(eng, golden)
+    kp = torch.from_numpy(g['kp2d']).cuda()
+    out = eng.decode_keypoints(kp, apply_sigmoid=False)
+    q, t = out['ori'].cpu().numpy(), out['pos'].cpu().numpy()
+    assert not out['status'].cpu().numpy().any()
+    assert D.angle_deg_stable(q, g['q']).max() < 5e-4            # 1,800 reference poses
+    assert np.linalg.norm(t - g['t'], axis=1).max() < 2e-4
+
+
+def test_epnp_matches_oracle_on_noisy_keypoints(kp_engine, golden):
+    eng, _ = kp_engine
+    g = _cfg(eng, golden)
+    rng = np.random.default_rng(3)
+    kp = (g['kp2d'][:256] + rng.normal(0, 3 / 1920, (256, 24))).astype(np.float32)
+    out = eng.decode_keypoints(torch.from_numpy(kp).cuda(), apply_sigmoid=False)
+    rq, rt = E.decode_batch(kp, g['kp3d'], g['K'])
+    ang = D.angle_deg_stable(out['ori'].cpu().numpy(), rq)
+    dt = np.linalg.norm(out['pos'].cpu().numpy() - rt, axis=1)
+    assert np.median(ang) < 1e-4 and ang.max() < 0.1              # north_star: < 0.1 deg
+    assert np.median(dt) < 1e-5 and dt.max() < 1e-3               # < 1 mm
+
+
+def test_sigmoid_then_epnp(kp_engine, golden):
+    eng, _ = kp_engine
+    g = _cfg(eng, golden)
+    inside = np.all((g['kp2d'] > 1e-3) & (g['kp2d'] < 1 - 1e-3), axis=1)   # keypoints in the frame
+    kp = g['kp2d'][inside][:64].astype(np.float64)
+    logit = np.log(kp / (1 - kp)).astype(np.float32)
+    out = eng.decode_keypoints(torch.from_numpy(logit).cuda(), apply_sigmoid=True)
+    sig = D.sigmoid_f32(logit)
+    np.testing.assert_allclose(out['keypoints'].cpu().numpy(), sig, rtol=2e-6, atol=1e-7)
+    rq, rt = E.decode_batch(sig, g['kp3d'], g['K'])
+    assert D.angle_deg_stable(out['ori'].cpu().numpy(), rq).max() < 1e-3
+    assert D.angle_deg_stable(out['ori'].cpu().numpy(), g['q'][inside][:64]).max() < 0.05
+
+
+def test_keypoint_head_forward(kp_engine):
+    """KeypointRegressionHead (flatten NCHW -> Linear 122880 -> 24) at 240x384 vs the oracle."""
+    eng, sd = kp_engine
+    rng = np.random.Generator(np.random.PCG64(5))
+    fr = rng.integers(0, 256, (3, 240, 384, 3), dtype=np.uint8)
+    raw, _ = eng.forward(torch.from_numpy(fr).cuda())
+    ref = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd, head='keypoints')
+    assert np.abs(raw.cpu().numpy() - ref.numpy()).max() < 1e-3
+
+
+def test_predict_keypoint_mode(kp_engine, golden):
+    """SPEMi355x.predict in keypoint mode: pose dict keys of SPETorch (spe_torch.py:63-76), sigmoid keypoints
+    matching the oracle forward, ori/pos equal to the EPnP kernel on those keypoints."""
+    from spef_amd.spe.keypoints import KeyPoints
+    from spef_amd.spe.spe_utils import SPEUtils
+    from spef_amd.spe_mi355x import SPEMi355x
+    eng, sd = kp_engine
+    g = golden('keypoints.npz')
+
+    class Cam:
+        K, nu, nv = g['K'], float(g['nu']), float(g['nv'])
+    su = SPEUtils(Cam, 'keypoints', pos_mode='keypoints', keypoints_path=KeyPoints(Cam, g['kp3d']))
+    spe = SPEMi355x(eng, 'cuda:0', su)
+    rng = np.random.Generator(np.random.PCG64(9))
+    x = torch.from_numpy(rng.random((2, 3, 240, 384), dtype=np.float32))
+    pose, lat = spe.predict(x)
+    assert set(pose) == {'keypoints', 'ori', 'pos'} and lat > 0
+    ref = D.sigmoid_f32(M.forward(x, sd, head='keypoints').numpy())
+    assert np.abs(pose['keypoints'] - ref).max() < 3e-4
+    chk = eng.decode_keypoints(torch.from_numpy(pose['keypoints']).cuda(), apply_sigmoid=False)
+    np.testing.assert_array_equal(chk['ori'].cpu().numpy(), pose['ori'])
+    np.testing.assert_array_equal(chk['pos'].cpu().numpy(), pose['pos'])

@@ -88,3 +88,29 @@ def test_score(golden):
     s = D.get_score(g['q_true'], g['t_true'], g['q_pred'], g['t_pred'])
     for k, v in s.items():
         np.testing.assert_allclose(v, g[k], rtol=1e-6)
+
+
+def test_epnp_oracle_recovers_reference_projections(golden):
+    """EPnP restatement (OpenCV 4.5.5 epnp.cpp semantics) on the reference's own noise-free projections
+    (KeyPoints.create_keypoints2d of valid.json poses): recovers the labelled pose. OpenCV itself is absent,
+    so parity with cv2.solvePnP is pinned only through this known-answer test."""
+    from oracle import epnp_ref as E
+    g = golden('keypoints.npz')
+    idx = np.arange(0, g['q'].shape[0], 15)          # 120 poses spread over the split
+    q, t = E.decode_batch(g['kp2d'][idx], g['kp3d'], g['K'])
+    assert D.angle_deg_stable(q, g['q'][idx]).max() < 5e-4
+    assert np.linalg.norm(t - g['t'][idx], axis=1).max() < 2e-4
+
+
+def test_host_keypoints_mirror_matches_golden(golden):
+    """spef_amd.spe.KeyPoints.create_keypoints2d reproduces the reference's projections (keypoints.npz)."""
+    from spef_amd.spe.camera import SpeedCamera
+    from spef_amd.spe.keypoints import KeyPoints
+    from spef_amd.spe.spe_utils import SPEUtils
+    g = golden('keypoints.npz')
+    np.testing.assert_allclose(SpeedCamera.K, g['K'])
+    kp = KeyPoints(SpeedCamera, g['kp3d'])
+    for i in range(0, 1800, 97):
+        np.testing.assert_allclose(kp.create_keypoints2d(g['q'][i], g['t'][i]), g['kp2d'][i], rtol=1e-6, atol=1e-7)
+    su = SPEUtils(SpeedCamera, 'keypoints', pos_mode='keypoints', keypoints_path=kp)
+    assert su.keypoints is kp
