@@ -45,6 +45,22 @@ def synth_frames(b: int, h: int, w: int, first_index: int, seed: int = 1001):
     return out
 
 
+def pmc_traffic(kernel_key: str, path: str):
+    """HBM bytes per launch of ``kernel_key`` from the committed rocprofv3 FETCH_SIZE/WRITE_SIZE passes
+    (tools/rocprof_summary.py: bytes = (2*FETCH_SIZE + WRITE_SIZE) * 1024, the gfx950 correction), or None when
+    the file is absent or the profiled symbol for this key is ambiguous."""
+    try:
+        with open(path) as f:
+            kernels = json.load(f)['kernels']
+    except (OSError, KeyError, ValueError):
+        return None
+    if kernel_key in kernels:
+        return kernels[kernel_key]['hbm_bytes_per_launch']
+    prefix = kernel_key.split('<')[0] + '<'
+    hits = [v for k, v in kernels.items() if k.startswith(prefix)]
+    return hits[0]['hbm_bytes_per_launch'] if len(hits) == 1 else None
+
+
 def cpu_baseline(args, sd):
     """The CPU oracle (FP32 PyTorch restatement of the reference eval path: forward + softmax + Markley decode,
     pinned to the reference by tests/golden) timed on this host's cores, on a bounded sample."""
@@ -56,17 +72,36 @@ def cpu_baseline(args, sd):
     torch.set_num_threads(threads)
     h, _ = D.orientation_histogram(12, False)
     bs, nb = args.cpu_batch, args.cpu_batches
-    x = M.u8_nhwc_to_nchw_f32(synth_frames(bs, args.size, args.size, 10_000))
+    fr = synth_frames(bs, args.size, args.size, 10_000)
+    x = M.u8_nhwc_to_nchw_f32(fr)
     o, p = M.forward(x[:2], sd)                                        # warm-up
     t0 = time.perf_counter()
     for _ in range(nb):
         o, p = M.forward(x, sd)
         D.decode_orientation_batch(D.softmax_f32(o.numpy()), h)
     dt = time.perf_counter() - t0
-    return {'value': round(bs * nb / dt, 3), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+    base = {'value': round(bs * nb / dt, 3), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
             'sample': f'{nb} batches x {bs} synthetic {args.size}x{args.size} frames, FP32 torch CPU forward + '
                       f'NumPy softmax/Markley decode (oracle/, pinned to the reference by tests/golden), '
                       f'{threads} threads, {dt:.1f} s'}
+    q = D.decode_orientation_batch(D.softmax_f32(o.numpy()), h)
+    return base, (fr, o.numpy(), p.numpy(), q)
+
+
+def pose_error(eng, dev, fr, o_ref, p_ref, q_ref):
+    """'pose err vs fp32 ref' half of the metric: the GPU path (uint8 NHWC frames, as timed) on the CPU
+    baseline's own frames, against the FP32 oracle's logits and decoded pose."""
+    import numpy as np
+    import torch
+    from oracle import decode_ref as D
+    xg = torch.from_numpy(fr).to(dev)
+    o, p = eng.forward(xg)
+    dec = eng.decode(1, 0, o, p, want_soft=True)
+    ang = D.angle_deg_stable(dec['ori'].cpu().numpy().astype(np.float64), q_ref)
+    torch.cuda.synchronize(dev)
+    return {'frames': int(fr.shape[0]), 'ori_logit_max_abs': float(np.abs(o.cpu().numpy() - o_ref).max()),
+            'pos_max_abs_m': float(np.abs(p.cpu().numpy() - p_ref).max()), 'ori_max_deg': float(ang.max()),
+            'tolerance': 'logits 1e-3, pose 0.1 deg / 1 mm (BASELINE.json north_star)'}
 
 
 def main():
@@ -81,6 +116,8 @@ def main():
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--cpu-batch', type=int, default=64)
     ap.add_argument('--cpu-batches', type=int, default=3)
+    ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json'),
+                    help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic')
     args = ap.parse_args()
 
     import numpy as np
@@ -167,8 +204,11 @@ def main():
         ach_tfl = fl / n / avg_s / 1e12
         fpi = flops_per_image(S, S)
         step_ms = elapsed / args.steps * 1e3
+        traffic = pmc_traffic(dom_key, args.traffic)
+        if traffic is not None:
+            traffic *= B / 64.0     # the PMC passes ran batch 64 (tools/pmc.sh); bytes scale with the batch
         rec = {
-            'metric': 'images/sec at 512x512 batch 64 per GPU (MobileNetV2+URSONet forward + on-device decode)',
+            'metric': 'images/sec at 512\u00d7512 batch 64, 1/2/4/8 MI355X; pose err vs fp32 ref',
             'value': round(value, 2),
             'unit': 'images/sec',
             'n_gpus': world,
@@ -183,7 +223,10 @@ def main():
             'config': {'workload': f'C3: full net + decode, {S}x{S}, batch {B} per GPU', 'global_batch': B * world,
                        'image_size': S, 'parallelism': f'frame-parallel x{world} (RCCL weight bcast)'},
             'roofline': {'bound': 'hbm', 'kernel': dom_key, 'achieved': round(ach_gbs, 1), 'peak': HBM_PEAK_GBS,
-                         'unit': 'GB/s', 'frac': round(ach_gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'unit': 'GB/s', 'frac': round(ach_gbs / HBM_PEAK_GBS, 4),
+                         'traffic': None if traffic is None else round(traffic),
+                         'traffic_source': os.path.relpath(args.traffic, ROOT) if traffic is not None else None,
+                         'algorithmic_bytes_per_launch': round(byts / n),
                          'avg_launch_us': round(avg_s * 1e6, 2), 'launches_per_step': n / args.steps,
                          'kernel_mfma_tflops': round(ach_tfl, 2)},
             'mfma_utilisation_whole_net': round(fpi * value / world / 1e12 / MFMA_PEAK_TFLOPS, 5),
@@ -192,7 +235,8 @@ def main():
                         for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1])},
         }
         if world == 1 and not args.no_cpu_baseline:
-            rec['cpu_baseline'] = cpu_baseline(args, sd)
+            rec['cpu_baseline'], ref = cpu_baseline(args, sd)
+            rec['pose_err_vs_fp32'] = pose_error(eng, dev, *ref)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

@@ -1,0 +1,24 @@
+#!/bin/bash
+# One GPU-box pass producing the round's measurement artefacts (run from the repo root on the box):
+#   gpurun_out/bench_<tag>.json    bench.py line (N=1, with cpu_baseline and pose error)
+#   gpurun_out/prof_<tag>/         rocprofv3 --kernel-trace --stats of a short bench run
+#   gpurun_out/pmc_fetch_<tag>/, pmc_write_<tag>/   separate FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md)
+# then: python tools/rocprof_summary.py --tag <tag> --stats gpurun_out/prof_<tag> \
+#         --fetch gpurun_out/pmc_fetch_<tag> --write gpurun_out/pmc_write_<tag>
+set -e
+TAG=${1:-r01}
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+O=$R/gpurun_out
+mkdir -p $O
+timeout -k 10 300 python3 $R/bench.py > $O/bench_$TAG.json 2> $O/bench_$TAG.err
+echo "bench ok"
+(cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --output-format csv \
+  -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline) > $O/prof_$TAG.log 2>&1
+echo "stats ok"
+(cd /tmp && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$TAG -o run --output-format csv \
+  -- python3 $R/tools/fwd_only.py 2) > $O/pmc_fetch_$TAG.log 2>&1
+echo "fetch ok"
+(cd /tmp && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$TAG -o run --output-format csv \
+  -- python3 $R/tools/fwd_only.py 2) > $O/pmc_write_$TAG.log 2>&1
+echo "write ok"
