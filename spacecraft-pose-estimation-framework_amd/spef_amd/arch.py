@@ -175,3 +175,15 @@ def state_dict_shapes(arch: Arch) -> dict:
         shapes['head.layer.1.weight'] = (arch.n_kp, 122880)
         shapes['head.layer.1.bias'] = (arch.n_kp,)
     return shapes
+
+
+def arch_from_state_dict(sd, residual: bool = True) -> Arch:
+    """Topology of a reference state_dict (``model.py:261-266`` layout): head type and widths from the head
+    keys (``head/ursonet.py:17-25`` -> ``head.ori.1`` / ``head.pos.0``; ``head/keypoints.py:20`` ->
+    ``head.layer.1``). ``residual`` is ``MODEL.BACKBONE.RESIDUAL`` (not recoverable from the weights)."""
+    if 'head.layer.1.weight' in sd:
+        return mobilenet_v2('keypoints', residual=residual, n_kp=int(sd['head.layer.1.weight'].shape[0]))
+    if 'head.ori.1.weight' in sd and 'head.pos.0.weight' in sd:
+        return mobilenet_v2('ursonet', int(sd['head.ori.1.weight'].shape[0]), int(sd['head.pos.0.weight'].shape[0]),
+                            residual=residual)
+    raise AssertionError('state_dict has neither a URSONet nor a keypoint-regression head')

@@ -18,7 +18,7 @@ from typing import Dict, List, Optional
 
 import numpy as np
 
-from .arch import Arch, BN_EPS, ConvSpec, LAST_CHANNELS, mobilenet_v2
+from .arch import Arch, BN_EPS, ConvSpec, LAST_CHANNELS, arch_from_state_dict, mobilenet_v2
 
 MAGIC = b'SPEFMI35'
 VERSION = 1
@@ -88,9 +88,10 @@ def _dw_tensor(w: np.ndarray, b: np.ndarray, data: _Data):
 
 
 def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=(8, 12)) -> bytes:
-    """Fold BN and pack a reference-layout state_dict into a blob (bytes)."""
+    """Fold BN and pack a reference-layout state_dict into a blob (bytes). ``arch`` defaults to the topology
+    the state_dict's head keys describe (``arch.arch_from_state_dict``)."""
     assert dtype in DTYPES, dtype
-    arch = arch or mobilenet_v2()
+    arch = arch or arch_from_state_dict(sd)
     data = _Data()
     ops = []
 

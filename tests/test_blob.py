@@ -68,3 +68,14 @@ def test_pointwise_tensor_padding_fp16():
     w, _ = Bl.fold_bn(sd, arch.blocks[2].convs[0])
     np.testing.assert_allclose(wp[:, :24], w[:, :, 0, 0].astype(np.float16))
     assert not wp[:, 24:].any()
+
+
+def test_pack_infers_head_from_state_dict():
+    """pack(sd) without an explicit arch reads the head type/widths from the reference keys."""
+    from spef_amd.arch import arch_from_state_dict, mobilenet_v2
+    from spef_amd.weights import synthetic_state_dict
+    for a in (mobilenet_v2('ursonet', 1232, 1000), mobilenet_v2('keypoints')):
+        sd = synthetic_state_dict(a, seed=3)
+        b = arch_from_state_dict(sd)
+        assert (b.head, b.n_ori, b.n_pos, b.n_kp) == (a.head, a.n_ori, a.n_pos, a.n_kp)
+        assert Bl.pack(sd) == Bl.pack(sd, a)
