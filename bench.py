@@ -137,29 +137,21 @@ def main():
     from spef_amd import blob as Bl
     from spef_amd.arch import flops_per_image, mobilenet_v2
     from spef_amd.engine import Engine
+    from spef_amd.shard import broadcast_blob, max_over_ranks, shard_range
     from spef_amd.spe.spe_utils import SPEUtils
     from spef_amd.weights import synthetic_state_dict
 
     sd = None
     if rank == 0:
         sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=1001)
-        blob = np.frombuffer(Bl.pack(sd, dtype=args.dtype), np.uint8)
-        nbytes = torch.tensor([blob.size], dtype=torch.int64, device=dev)
-    else:
-        nbytes = torch.zeros(1, dtype=torch.int64, device=dev)
-    if world > 1:
-        dist.broadcast(nbytes, 0)
-    dblob = torch.empty(int(nbytes.item()), dtype=torch.uint8, device=dev)
-    if rank == 0:
-        dblob.copy_(torch.from_numpy(blob))
-    if world > 1:
-        dist.broadcast(dblob, 0)                     # RCCL weight broadcast over xGMI
+    dblob = broadcast_blob(Bl.pack(sd, dtype=args.dtype) if rank == 0 else None, dev)   # RCCL over xGMI
     eng = Engine(dblob, dev)
     su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
     eng.set_decode_tables(su.orientation.histogram, None)
 
     B, S = args.batch, args.size
-    frames = torch.from_numpy(synth_frames(B, S, S, rank * B)).to(dev)
+    first, stop = shard_range(B * world, rank, world)          # this rank's global frame indices
+    frames = torch.from_numpy(synth_frames(stop - first, S, S, first)).to(dev)
     eng.reserve(B, S, S)
     ori = torch.empty((B, eng.n_out0), dtype=torch.float32, device=dev)
     pos = torch.empty((B, eng.n_out1), dtype=torch.float32, device=dev)
@@ -182,10 +174,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize(dev)
     elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+    elapsed = max_over_ranks(elapsed, dev)
     assert not out['status'].any().item(), 'decode reported NaN'
 
     # roofline leg: per-kernel HIP events on the engine's stream, K more steps
