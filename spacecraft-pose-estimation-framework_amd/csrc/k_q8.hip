@@ -1,0 +1,417 @@
+// INT8 path: the Brevitas-mirroring quantized MobileNet-V2 + URSONet head
+// (src/modeling/backbone/mobilenet_v2.py:119-229, common/brevitas_layers.py:10-136, head/ursonet.py:36-93)
+// with the integer semantics of oracle/int8_ref.py, which these kernels reproduce bit-exactly:
+//
+//   conv + BN + quant   acc = sum q_x q_w (int32, exact);  q = clip((acc * M[c] + B[c]) >> S[c], lo, hi)
+//                       (int64 fixed point; M, B, S per output channel from the blob, B holds the rounding half)
+//   residual join       q_sum = q_proj + q_in;  q_out = clip((q_sum * R + RB) >> RS, -128, 127)
+//   pool                sum over the map >> tb (TruncTo8bit floor), u8
+//   FC                  out = f32(acc + q_b[c]) * sc[c]
+//
+// MFMA: v_mfma_i32_16x16x64_i8 (signed x signed). Unsigned activations (depthwise outputs, pooled features)
+// are stored offset by -128 (u ^ 0x80) so they are valid int8 operands; the exact correction 128 * sum_k q_w
+// is the accumulator's initial value (`init`, per output channel). The K order inside one MFMA is irrelevant
+// because A and B fragments use the same lane->k assignment (lane (r, g) element j <-> k = 16 g + j).
+#include "spef_common.hpp"
+#include "spef_kernels.hpp"
+
+namespace spef {
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+
+struct Rq {   // per-channel requant parameters, struct-of-arrays over Np channels
+  const int64_t* M;
+  const int64_t* B;
+  const int32_t* S;
+};
+
+__device__ __forceinline__ int requant(int acc, int64_t M, int64_t B, int S, int lo, int hi) {
+  const int64_t v = ((int64_t)acc * M + B) >> S;
+  return (int)(v < lo ? lo : (v > hi ? hi : v));
+}
+
+// ------------------------------------------------------------------------------------------------ stem
+// Input QuantIdentity + QConvBnAct 3->32 3x3/s2 (mobilenet_v2.py:177-182). One thread per output pixel,
+// 27 taps packed into 7 dwords (sdot4), 32 channel accumulators; weights [32][28] int8 broadcast from LDS.
+template <bool F32IN>
+__global__ __launch_bounds__(256) void q_stem_kernel(const void* __restrict__ in, const int8_t* __restrict__ lut,
+                                                     float s_img, const int8_t* __restrict__ w28,
+                                                     Rq rq, uint8_t* __restrict__ Y, int B, int H, int W,
+                                                     int OH, int OW) {
+  __shared__ int Wl[32 * 7];
+  __shared__ int8_t Ll[256];
+  __shared__ int64_t Ml[32], Bl[32];
+  __shared__ int Sl[32];
+  const int tid = threadIdx.x;
+  if (tid < 32 * 7) Wl[tid] = reinterpret_cast<const int*>(w28)[tid];
+  if (!F32IN) Ll[tid] = lut[tid];
+  if (tid < 32) {
+    Ml[tid] = rq.M[tid];
+    Bl[tid] = rq.B[tid];
+    Sl[tid] = rq.S[tid];
+  }
+  __syncthreads();
+  const int64_t p = (int64_t)blockIdx.x * 256 + tid;
+  if (p >= (int64_t)B * OH * OW) return;
+  const int ox = (int)(p % OW);
+  const int oy = (int)((p / OW) % OH);
+  const int b = (int)(p / ((int64_t)OW * OH));
+  int8_t t[28];
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int iy = 2 * oy - 1 + ky, ix = 2 * ox - 1 + kx;
+      const bool v = iy >= 0 && iy < H && ix >= 0 && ix < W;
+#pragma unroll
+      for (int ci = 0; ci < 3; ++ci) {
+        int8_t q = 0;
+        if (v) {
+          if (F32IN) {
+            const float x = reinterpret_cast<const float*>(in)[(((size_t)b * 3 + ci) * H + iy) * W + ix];
+            const float r = rintf(x / s_img);
+            q = (int8_t)fminf(fmaxf(r, -128.f), 127.f);
+          } else {
+            q = Ll[reinterpret_cast<const uint8_t*>(in)[(((size_t)b * H + iy) * W + ix) * 3 + ci]];
+          }
+        }
+        t[ky * 9 + kx * 3 + ci] = q;
+      }
+    }
+  t[27] = 0;
+  int xp[7];
+#pragma unroll
+  for (int d = 0; d < 7; ++d)
+    xp[d] = (int)(uint8_t)t[4 * d] | ((int)(uint8_t)t[4 * d + 1] << 8) | ((int)(uint8_t)t[4 * d + 2] << 16) |
+            ((int)(uint8_t)t[4 * d + 3] << 24);
+  uint32_t o[8];
+#pragma unroll
+  for (int c = 0; c < 32; ++c) {
+    int acc = 0;
+#pragma unroll
+    for (int d = 0; d < 7; ++d) acc = __builtin_amdgcn_sdot4(xp[d], Wl[c * 7 + d], acc, false);
+    const uint32_t q = (uint32_t)requant(acc, Ml[c], Bl[c], Sl[c], 0, 255);
+    if ((c & 3) == 0) o[c >> 2] = 0;
+    o[c >> 2] |= q << (8 * (c & 3));
+  }
+  uint4* dst = reinterpret_cast<uint4*>(Y + (size_t)p * 32);
+  dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+  dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+// ------------------------------------------------------------------------------------------------ depthwise
+// dw QConvBnAct (brevitas_layers.py:113-119): u8 in, int8 [9][C] weights, ReLU-quant; output stored offset
+// (u - 128 as int8) for the projection MFMA. One thread = one output pixel x 8 channels.
+__global__ __launch_bounds__(256) void q_dw_kernel(const uint8_t* __restrict__ X, const int8_t* __restrict__ W9,
+                                                   Rq rq, int8_t* __restrict__ Y, int B, int H, int W, int C,
+                                                   int stride, int OH, int OW) {
+  const int cg = C >> 3;
+  const int64_t t = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (t >= (int64_t)B * OH * OW * cg) return;
+  const int g = (int)(t % cg);
+  const int64_t p = t / cg;
+  const int ox = (int)(p % OW);
+  const int oy = (int)((p / OW) % OH);
+  const int b = (int)(p / ((int64_t)OW * OH));
+  const int c0 = 8 * g;
+  int acc[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+  for (int ky = 0; ky < 3; ++ky) {
+    const int iy = oy * stride - 1 + ky;
+    if (iy < 0 || iy >= H) continue;
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ox * stride - 1 + kx;
+      if (ix < 0 || ix >= W) continue;
+      const uint2 xv = *reinterpret_cast<const uint2*>(X + (((size_t)b * H + iy) * W + ix) * C + c0);
+      const uint2 wv = *reinterpret_cast<const uint2*>(W9 + (size_t)(ky * 3 + kx) * C + c0);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int xs = (int)(((e < 4 ? xv.x : xv.y) >> (8 * (e & 3))) & 0xff);
+        const int ws = (int)(int8_t)(((e < 4 ? wv.x : wv.y) >> (8 * (e & 3))) & 0xff);
+        acc[e] += xs * ws;
+      }
+    }
+  }
+  uint32_t lo = 0, hi = 0;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int c = c0 + e;
+    const uint32_t q = (uint32_t)(requant(acc[e], rq.M[c], rq.B[c], rq.S[c], 0, 255) ^ 0x80);
+    if (e < 4) lo |= q << (8 * e);
+    else hi |= q << (8 * (e - 4));
+  }
+  *reinterpret_cast<uint2*>(Y + p * C + c0) = make_uint2(lo, hi);
+}
+
+// ------------------------------------------------------------------------------------------------ GEMM
+// 1x1 conv / FC as C^T = W X^T on v_mfma_i32_16x16x64_i8: W int8 [Np][Kp] (Kp multiple of 64), X int8 [M][K]
+// (NHWC rows). Workgroup 4 waves = WN (channel) x WM (pixel); K advances 64 per double-buffered LDS step.
+// LDS rows are 80 B (64 + 16 pad): the 16 rows of one ds_read_b128 phase hit disjoint banks.
+template <int WN, int NT, int MT, int EPI>
+__global__ __launch_bounds__(256) void q_gemm_kernel(const int8_t* __restrict__ X, const int8_t* __restrict__ Wt,
+                                                     const int32_t* __restrict__ init, Rq rq,
+                                                     const int8_t* __restrict__ R, int64_t RM, int64_t RB, int RS,
+                                                     void* __restrict__ Y, float* __restrict__ Y1,
+                                                     const float* __restrict__ sc, int n_split, int64_t M, int K,
+                                                     int N, int Kp, int Np, int n_chunks, uint32_t nwg) {
+  constexpr int WM = 4 / WN;
+  constexpr int BN = 16 * WN * NT, BM = 16 * WM * MT;
+  constexpr int RSB = 80;
+  constexpr int XP = (BM * 4 + 255) / 256, WP = (BN * 4 + 255) / 256;
+  __shared__ __attribute__((aligned(16))) int8_t As[2][BN * RSB];
+  __shared__ __attribute__((aligned(16))) int8_t Bs[2][BM * RSB];
+
+  const uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int chunk = (int)(L % (uint32_t)n_chunks);
+  const int64_t mt0 = (int64_t)(L / (uint32_t)n_chunks) * BM;
+  const int n0 = chunk * BN;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  const int wn = wave % WN, wm = wave / WN;
+  const bool k16 = (K & 15) == 0;
+
+  i32x4 xr[XP], wr[WP];
+  auto gload = [&](int ks) {
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int p = tid + 256 * i;
+      const int row = p >> 2, g = p & 3;
+      const int64_t m = mt0 + row;
+      const int k = ks * 64 + 16 * g;
+      i32x4 v = {0, 0, 0, 0};
+      if (p < BM * 4 && m < M) {
+        const int8_t* src = X + (size_t)m * K + k;
+        if (k16) {
+          if (k < K) v = *reinterpret_cast<const i32x4*>(src);
+        } else {
+          if (k < K) {
+            const int2 a = *reinterpret_cast<const int2*>(src);
+            v[0] = a.x;
+            v[1] = a.y;
+          }
+          if (k + 8 < K) {
+            const int2 a = *reinterpret_cast<const int2*>(src + 8);
+            v[2] = a.x;
+            v[3] = a.y;
+          }
+        }
+      }
+      xr[i] = v;
+    }
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int p = tid + 256 * i;
+      const int row = p >> 2, g = p & 3;
+      const int n = n0 + row;
+      i32x4 v = {0, 0, 0, 0};
+      if (p < BN * 4 && n < Np) v = *reinterpret_cast<const i32x4*>(Wt + (size_t)n * Kp + ks * 64 + 16 * g);
+      wr[i] = v;
+    }
+  };
+  auto lstore = [&](int buf) {
+#pragma unroll
+    for (int i = 0; i < XP; ++i) {
+      const int p = tid + 256 * i;
+      if (p < BM * 4) *reinterpret_cast<i32x4*>(&Bs[buf][(p >> 2) * RSB + 16 * (p & 3)]) = xr[i];
+    }
+#pragma unroll
+    for (int i = 0; i < WP; ++i) {
+      const int p = tid + 256 * i;
+      if (p < BN * 4) *reinterpret_cast<i32x4*>(&As[buf][(p >> 2) * RSB + 16 * (p & 3)]) = wr[i];
+    }
+  };
+
+  i32x4 acc[NT][MT];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    const int i = n0 + (wn * NT + a) * 16 + 4 * kg;
+    int4 b0 = make_int4(0, 0, 0, 0);
+    if (init && i < Np) b0 = *reinterpret_cast<const int4*>(init + i);
+#pragma unroll
+    for (int b = 0; b < MT; ++b) acc[a][b] = i32x4{b0.x, b0.y, b0.z, b0.w};
+  }
+
+  const int KS = Kp >> 6;
+  gload(0);
+  lstore(0);
+  __syncthreads();
+  for (int ks = 0; ks < KS; ++ks) {
+    const int buf = ks & 1;
+    if (ks + 1 < KS) gload(ks + 1);
+    i32x4 af[NT], bf[MT];
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+      af[a] = *reinterpret_cast<const i32x4*>(&As[buf][((wn * NT + a) * 16 + r16) * RSB + 16 * kg]);
+#pragma unroll
+    for (int b = 0; b < MT; ++b)
+      bf[b] = *reinterpret_cast<const i32x4*>(&Bs[buf][((wm * MT + b) * 16 + r16) * RSB + 16 * kg]);
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int b = 0; b < MT; ++b) acc[a][b] = __builtin_amdgcn_mfma_i32_16x16x64_i8(af[a], bf[b], acc[a][b], 0, 0, 0);
+    if (ks + 1 < KS) {
+      lstore(buf ^ 1);
+      __syncthreads();
+    }
+  }
+
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    const int i = n0 + (wn * NT + a) * 16 + 4 * kg;
+    if (i >= N) continue;
+#pragma unroll
+    for (int b = 0; b < MT; ++b) {
+      const int64_t m = mt0 + (wm * MT + b) * 16 + r16;
+      if (m >= M) continue;
+      const i32x4 v = acc[a][b];
+      if constexpr (EPI == QEPI_FC) {   // float head outputs: columns [0, n_split) -> Y, the rest -> Y1
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = i + e;
+          if (c >= N) break;
+          const float o = (float)v[e] * sc[c];
+          if (c < n_split) reinterpret_cast<float*>(Y)[(size_t)m * n_split + c] = o;
+          else Y1[(size_t)m * (N - n_split) + (c - n_split)] = o;
+        }
+        continue;
+      }
+      uint32_t packed = 0;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int c = i + e;
+        int q;
+        if constexpr (EPI == QEPI_RELU) {
+          q = requant(v[e], rq.M[c], rq.B[c], rq.S[c], 0, 255);
+        } else if constexpr (EPI == QEPI_PROJ) {
+          q = requant(v[e], rq.M[c], rq.B[c], rq.S[c], -128, 127);
+        } else {   // QEPI_PROJ_RES: residual join, then requantise to the next consumer's scale
+          const int p = requant(v[e], rq.M[c], rq.B[c], rq.S[c], -128, 127) + (int)R[(size_t)m * N + c];
+          const int64_t t = ((int64_t)p * RM + RB) >> RS;
+          q = (int)(t < -128 ? -128 : (t > 127 ? 127 : t));
+        }
+        packed |= ((uint32_t)q & 0xffu) << (8 * e);
+      }
+      *reinterpret_cast<uint32_t*>(reinterpret_cast<int8_t*>(Y) + (size_t)m * N + i) = packed;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------ pool
+// QuantAvgPool2d + TruncTo8bit over the whole map (ursonet.py:61-62, 88): pooled = (sum_hw q) >> tb, stored
+// offset (u - 128) as the FC's int8 B operand. One thread per (image, 4 channels).
+__global__ __launch_bounds__(256) void q_pool_kernel(const uint8_t* __restrict__ X, int8_t* __restrict__ P, int B,
+                                                     int HW, int C, int tb) {
+  const int cg = C >> 2;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= B * cg) return;
+  const int b = t / cg, c0 = 4 * (t % cg);
+  int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  for (int p = 0; p < HW; ++p) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(X + ((size_t)b * HW + p) * C + c0);
+    s0 += v & 0xff;
+    s1 += (v >> 8) & 0xff;
+    s2 += (v >> 16) & 0xff;
+    s3 += v >> 24;
+  }
+  const uint32_t o = (((uint32_t)(s0 >> tb) ^ 0x80) & 0xff) | ((((uint32_t)(s1 >> tb) ^ 0x80) & 0xff) << 8) |
+                     ((((uint32_t)(s2 >> tb) ^ 0x80) & 0xff) << 16) | ((((uint32_t)(s3 >> tb) ^ 0x80) & 0xff) << 24);
+  *reinterpret_cast<uint32_t*>(P + (size_t)b * C + c0) = o;
+}
+
+// int8 / u8 codes -> fp32 (probes, dequantized feature export): y = (code) * scale
+__global__ void q_to_f32_kernel(const void* __restrict__ x, float* __restrict__ y, int64_t n, int is_unsigned,
+                                float scale) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const int v = is_unsigned ? (int)reinterpret_cast<const uint8_t*>(x)[i] : (int)reinterpret_cast<const int8_t*>(x)[i];
+  y[i] = (float)v * scale;
+}
+
+// ------------------------------------------------------------------------------------------------ launchers
+
+hipError_t launch_q_to_f32(const void* x, float* y, int64_t n, int is_unsigned, float scale, hipStream_t s) {
+  const int64_t nb = (n + 255) / 256;
+  if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  if (n > 0) q_to_f32_kernel<<<(unsigned)nb, 256, 0, s>>>(x, y, n, is_unsigned, scale);
+  return hipGetLastError();
+}
+
+hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_img, const int8_t* w28,
+                         const int64_t* M, const int64_t* Bq, const int32_t* S, uint8_t* y, int B, int H, int W,
+                         int OH, int OW, hipStream_t s) {
+  const int64_t n = (int64_t)B * OH * OW;
+  const int64_t nb = (n + 255) / 256;
+  if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  Rq rq{M, Bq, S};
+  if (f32in)
+    q_stem_kernel<true><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, B, H, W, OH, OW);
+  else
+    q_stem_kernel<false><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, B, H, W, OH, OW);
+  return hipGetLastError();
+}
+
+hipError_t launch_q_dw(const uint8_t* x, const int8_t* w9, const int64_t* M, const int64_t* Bq, const int32_t* S,
+                       int8_t* y, int B, int H, int W, int C, int stride, int OH, int OW, hipStream_t s) {
+  if (C & 7) return hipErrorInvalidValue;
+  const int64_t n = (int64_t)B * OH * OW * (C >> 3);
+  const int64_t nb = (n + 255) / 256;
+  if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  q_dw_kernel<<<(unsigned)nb, 256, 0, s>>>(x, w9, Rq{M, Bq, S}, y, B, H, W, C, stride, OH, OW);
+  return hipGetLastError();
+}
+
+template <int WN, int NT, int MT>
+static hipError_t q_gemm_go(const QGemmArgs& a, hipStream_t s) {
+  constexpr int WM = 4 / WN;
+  constexpr int BN = 16 * WN * NT, BM = 16 * WM * MT;
+  const int Kp = (a.K + 63) & ~63, Np = (a.N + 15) & ~15;
+  const int n_chunks = (Np + BN - 1) / BN;
+  const int64_t nwg64 = (a.M + BM - 1) / BM * n_chunks;
+  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+  const uint32_t nwg = (uint32_t)nwg64;
+  const Rq rq{a.rqM, a.rqB, a.rqS};
+#define SPEF_QG(E)                                                                                             \
+  q_gemm_kernel<WN, NT, MT, E><<<nwg, 256, 0, s>>>(a.x, a.w, a.init, rq, a.r, a.rm, a.rb, a.rs, a.y, a.y1, a.sc, \
+                                                   a.n_split, a.M, a.K, a.N, Kp, Np, n_chunks, nwg)
+  switch (a.epi) {
+    case QEPI_RELU: SPEF_QG(QEPI_RELU); break;
+    case QEPI_PROJ: SPEF_QG(QEPI_PROJ); break;
+    case QEPI_PROJ_RES: SPEF_QG(QEPI_PROJ_RES); break;
+    case QEPI_FC: SPEF_QG(QEPI_FC); break;
+    default: return hipErrorInvalidValue;
+  }
+#undef SPEF_QG
+  return hipGetLastError();
+}
+
+hipError_t launch_q_gemm(const QGemmArgs& a, hipStream_t s) {
+  if (a.M <= 0) return hipSuccess;
+  if ((a.K & 7) || (a.epi != QEPI_FC && (a.N & 3))) return hipErrorInvalidValue;
+  const int n16 = ((a.N + 15) & ~15) / 16;
+  if (a.M <= 256) return q_gemm_go<4, 1, 1>(a, s);          // FC: few rows (images), many channels
+  switch (n16) {
+    case 1: return q_gemm_go<1, 1, 2>(a, s);
+    case 2: return q_gemm_go<2, 1, 4>(a, s);
+    case 4: return q_gemm_go<2, 2, 4>(a, s);
+    case 6: return q_gemm_go<2, 3, 4>(a, s);
+    case 9: return q_gemm_go<1, 9, 1>(a, s);
+    case 10: return q_gemm_go<2, 5, 2>(a, s);
+    default: break;
+  }
+  if (n16 % 12 == 0) return q_gemm_go<2, 6, 2>(a, s);
+  if (n16 % 10 == 0) return q_gemm_go<2, 5, 2>(a, s);
+  if (n16 % 8 == 0) return q_gemm_go<2, 4, 4>(a, s);
+  if (n16 % 4 == 0) return q_gemm_go<2, 2, 4>(a, s);
+  if (n16 % 2 == 0) return q_gemm_go<2, 1, 4>(a, s);
+  return q_gemm_go<1, 1, 2>(a, s);
+}
+
+hipError_t launch_q_pool(const uint8_t* x, int8_t* p, int B, int HW, int C, int tb, hipStream_t s) {
+  if (C & 3) return hipErrorInvalidValue;
+  const int n = B * (C >> 2);
+  q_pool_kernel<<<(n + 255) / 256, 256, 0, s>>>(x, p, B, HW, C, tb);
+  return hipGetLastError();
+}
+
+}  // namespace spef

@@ -9,6 +9,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <array>
 
 #include <string>
 #include <vector>
@@ -60,6 +61,15 @@ struct spef_ctx {
   int64_t fuse_min_hw = 0;   // SPEF_OPT_FUSE_MIN_HW
   int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
   int irb_variant = 0;       // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps)
+  // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
+  std::vector<double> q8_sw, q8_bias;
+  std::vector<int32_t> q8_wsum;
+  double q8_sl = 0.0;
+  int32_t* q8_fc_init = nullptr;   // [Np] 128 * sum_k q_w + q_b (q_b depends on the pooled map size)
+  float* q8_fc_sc = nullptr;       // [Np] f32(s_pool * s_w)
+  int q8_fc_hw = 0, q8_fc_tb = 0;
+  float q8_s_img = 0.f;                        // input scale (f32 NCHW path)
+  std::vector<std::array<int64_t, 3>> q8_res;  // per op: residual-join rescale (R, RB, RS)
   // per-launch HIP-event profiling (bench.py roofline leg)
   bool profiling = false;
   struct Rec {
@@ -144,7 +154,7 @@ inline const T* ptr(const spef_ctx* c, uint64_t off) {
   return off == kAbsent ? nullptr : reinterpret_cast<const T*>(c->d_data + off);
 }
 
-size_t elem_size(const spef_ctx* c) { return 2; }  // fp16 / bf16 activations
+size_t elem_size(const spef_ctx* c) { return c->hdr.dtype == DT_I8 ? 1 : 2; }  // int8 | fp16 / bf16 activations
 
 // algorithmic HBM bytes of one pointwise launch: read X, write Y (+ read residual), weights + bias once
 double pw_bytes(int64_t M, uint32_t K, uint32_t N, bool res) {
@@ -157,18 +167,18 @@ int64_t max_act_elems(const spef_ctx* c, int H, int W, int* fh, int* fw) {
   int64_t mx = 0;
   int h = H, w = W;
   for (const OpDesc& op : c->ops) {
-    if (op.kind == OP_STEM) {
+    if (op.kind == OP_STEM || op.kind == OP_QSTEM) {
       h = conv_out(h, 2);
       w = conv_out(w, 2);
       mx = std::max<int64_t>(mx, (int64_t)h * w * op.cout);
-    } else if (op.kind == OP_IRB) {
+    } else if (op.kind == OP_IRB || op.kind == OP_QIRB) {
       mx = std::max<int64_t>(mx, (int64_t)h * w * op.hidden);  // expand output
       const int oh = conv_out(h, op.stride), ow = conv_out(w, op.stride);
       mx = std::max<int64_t>(mx, (int64_t)oh * ow * op.hidden);
       mx = std::max<int64_t>(mx, (int64_t)oh * ow * op.cout);
       h = oh;
       w = ow;
-    } else if (op.kind == OP_LAST) {
+    } else if (op.kind == OP_LAST || op.kind == OP_QLAST) {
       mx = std::max<int64_t>(mx, (int64_t)h * w * op.cout);  // unfused last conv (spef_backbone)
     }
   }
@@ -336,6 +346,165 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
   return SPEF_OK;
 }
 
+// ---- INT8 schedule (k_q8.hip): one kernel per conv. Activations: stem / expand outputs u8, depthwise outputs
+// offset int8 (u - 128), block outputs int8 at the next consumer's scale, last conv u8.
+// mode: 0 = full (pooled offset-int8 codes into c->pooled), 1 = stop after op `stop`, 2 = last conv map.
+// *is_unsigned tells the caller how to read the returned codes.
+int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, int W, hipStream_t s, int mode,
+                    int stop, void** out_buf, int* oc, int* oh, int* ow, int* is_unsigned) {
+  void* cur = nullptr;
+  int h = H, w = W, ch = 3, uns = 0;
+  int op_index = 0;
+  auto pick = [&](std::initializer_list<void*> busy) -> void* {
+    for (void* b : c->buf) {
+      bool used = false;
+      for (void* u : busy) used |= (u == b);
+      if (!used) return b;
+    }
+    return nullptr;
+  };
+  auto rqM = [&](uint64_t off) { return ptr<int64_t>(c, off); };
+  auto rqB = [&](uint64_t off, uint32_t n) { return ptr<int64_t>(c, off) + ((n + 15) & ~15u); };
+  auto rqS = [&](uint64_t off, uint32_t n) {
+    return reinterpret_cast<const int32_t*>(ptr<int64_t>(c, off) + 2 * ((n + 15) & ~15u));
+  };
+  for (const OpDesc& op : c->ops) {
+    if (op.kind == OP_QSTEM) {
+      const int OH = conv_out(h, 2), OW = conv_out(w, 2);
+      uint8_t* y = (uint8_t*)c->buf[0];
+      const float s_img = c->q8_s_img;
+      const double px = (double)B * OH * OW;
+      HIP_TRY(prof_launch(c, s, layout == IN_U8_NHWC ? "q_stem_kernel<u8>" : "q_stem_kernel<f32>",
+                          (double)B * h * w * 3 * (layout == IN_U8_NHWC ? 1 : 4) + px * 32, px * 2 * 27 * 32, [&] {
+        return launch_q_stem(input, layout == IN_F32_NCHW, ptr<int8_t>(c, op.w1), s_img, ptr<int8_t>(c, op.w0),
+                             rqM(op.b0), rqB(op.b0, 32), rqS(op.b0, 32), y, B, h, w, OH, OW, s);
+      }));
+      cur = y;
+      h = OH;
+      w = OW;
+      ch = 32;
+      uns = 1;
+    } else if (op.kind == OP_QIRB) {
+      const int64_t M = (int64_t)B * h * w;
+      const int OH = conv_out(h, (int)op.stride), OW = conv_out(w, (int)op.stride);
+      const int64_t M2 = (int64_t)B * OH * OW;
+      const bool res = op.flags & 1u;
+      void* x = cur;
+      void* h1 = x;
+      if (op.expand != 1) {
+        h1 = pick({x});
+        QGemmArgs a{};
+        a.epi = QEPI_RELU;
+        a.x = (const int8_t*)x;
+        a.w = ptr<int8_t>(c, op.w0);
+        a.rqM = rqM(op.b0);
+        a.rqB = rqB(op.b0, op.hidden);
+        a.rqS = rqS(op.b0, op.hidden);
+        a.y = h1;
+        a.M = M;
+        a.K = (int)op.cin;
+        a.N = (int)op.hidden;
+        HIP_TRY(prof_launch(c, s, "q_gemm<relu>", (double)M * (op.cin + op.hidden) + (double)op.hidden * op.cin,
+                            2.0 * M * op.cin * op.hidden, [&] { return launch_q_gemm(a, s); }));
+      }
+      void* h2 = pick({x, h1});
+      HIP_TRY(prof_launch(c, s, "q_dw_kernel", (double)(M + M2) * op.hidden + 9.0 * op.hidden,
+                          18.0 * M2 * op.hidden, [&] {
+        return launch_q_dw((const uint8_t*)h1, ptr<int8_t>(c, op.w1), rqM(op.b1), rqB(op.b1, op.hidden),
+                           rqS(op.b1, op.hidden), (int8_t*)h2, B, h, w, (int)op.hidden, (int)op.stride, OH, OW, s);
+      }));
+      void* y = res ? pick({x, h2}) : pick({h2});
+      QGemmArgs a{};
+      a.epi = res ? QEPI_PROJ_RES : QEPI_PROJ;
+      a.x = (const int8_t*)h2;
+      a.w = ptr<int8_t>(c, op.w2);
+      a.init = ptr<int32_t>(c, op.x0);
+      a.rqM = rqM(op.b2);
+      a.rqB = rqB(op.b2, op.cout);
+      a.rqS = rqS(op.b2, op.cout);
+      if (res) {
+        const std::array<int64_t, 3>& r3 = c->q8_res[&op - c->ops.data()];
+        a.r = (const int8_t*)x;
+        a.rm = r3[0];
+        a.rb = r3[1];
+        a.rs = (int)r3[2];
+      }
+      a.y = y;
+      a.M = M2;
+      a.K = (int)op.hidden;
+      a.N = (int)op.cout;
+      HIP_TRY(prof_launch(c, s, res ? "q_gemm<proj_res>" : "q_gemm<proj>",
+                          (double)M2 * (op.hidden + op.cout * (res ? 2 : 1)) + (double)op.cout * op.hidden,
+                          2.0 * M2 * op.hidden * op.cout, [&] { return launch_q_gemm(a, s); }));
+      cur = y;
+      h = OH;
+      w = OW;
+      ch = (int)op.cout;
+      uns = 0;
+    } else if (op.kind == OP_QLAST) {
+      const int64_t M = (int64_t)B * h * w;
+      void* y = pick({cur});
+      QGemmArgs a{};
+      a.epi = QEPI_RELU;
+      a.x = (const int8_t*)cur;
+      a.w = ptr<int8_t>(c, op.w0);
+      a.rqM = rqM(op.b0);
+      a.rqB = rqB(op.b0, op.cout);
+      a.rqS = rqS(op.b0, op.cout);
+      a.y = y;
+      a.M = M;
+      a.K = (int)op.cin;
+      a.N = (int)op.cout;
+      HIP_TRY(prof_launch(c, s, "q_gemm<last>", (double)M * (op.cin + op.cout) + (double)op.cout * op.cin,
+                          2.0 * M * op.cin * op.cout, [&] { return launch_q_gemm(a, s); }));
+      cur = y;
+      ch = (int)op.cout;
+      uns = 1;
+      if (mode == 0) {
+        int tb = 0;
+        while ((1 << tb) < h * w) ++tb;
+        HIP_TRY(prof_launch(c, s, "q_pool_kernel", (double)M * op.cout + (double)B * op.cout, (double)M * op.cout, [&] {
+          return launch_q_pool((const uint8_t*)cur, (int8_t*)c->pooled, B, h * w, (int)op.cout, tb, s);
+        }));
+      }
+      break;
+    }
+    if (mode == 1 && op_index == stop) break;
+    ++op_index;
+  }
+  if (out_buf) *out_buf = cur;
+  if (oc) *oc = ch;
+  if (oh) *oh = h;
+  if (ow) *ow = w;
+  if (is_unsigned) *is_unsigned = uns;
+  return SPEF_OK;
+}
+
+// FC constants for a pooled map of `hw` pixels (oracle/int8_ref.py head_params, same float64 expression order).
+int q8_prepare_fc(spef_ctx* c, int hw) {
+  if (c->q8_fc_hw == hw && c->q8_fc_init) return SPEF_OK;
+  int tb = 0;
+  while ((1 << tb) < hw) ++tb;
+  const double s_pool = c->q8_sl * ldexp(1.0, tb) / hw;
+  const size_t np_ = c->q8_sw.size();
+  std::vector<int32_t> init(np_, 0);
+  std::vector<float> sc(np_, 0.f);
+  for (size_t i = 0; i < np_; ++i) {
+    if (c->q8_sw[i] == 0.0) continue;   // padding rows
+    double qb = nearbyint(c->q8_bias[i] / (s_pool * c->q8_sw[i]));
+    qb = qb < -128 ? -128 : (qb > 127 ? 127 : qb);
+    init[i] = c->q8_wsum[i] + (int32_t)qb;
+    sc[i] = (float)(s_pool * c->q8_sw[i]);
+  }
+  if (!c->q8_fc_init) HIP_TRY(hipMalloc(&c->q8_fc_init, np_ * sizeof(int32_t)));
+  if (!c->q8_fc_sc) HIP_TRY(hipMalloc(&c->q8_fc_sc, np_ * sizeof(float)));
+  HIP_TRY(hipMemcpy(c->q8_fc_init, init.data(), np_ * sizeof(int32_t), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(c->q8_fc_sc, sc.data(), np_ * sizeof(float), hipMemcpyHostToDevice));
+  c->q8_fc_hw = hw;
+  c->q8_fc_tb = tb;
+  return SPEF_OK;
+}
+
 void free_workspace(spef_ctx* c) {
   for (void*& b : c->buf) {
     if (b) hipFree(b);
@@ -383,6 +552,8 @@ int spef_destroy(spef_ctx* c) {
   if (c->d_pos_grid) hipFree(c->d_pos_grid);
   if (c->kp3d) hipFree(c->kp3d);
   if (c->kp_model) hipFree(c->kp_model);
+  if (c->q8_fc_init) hipFree(c->q8_fc_init);
+  if (c->q8_fc_sc) hipFree(c->q8_fc_sc);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
   delete c;
   return SPEF_OK;
@@ -394,17 +565,26 @@ static int parse_blob(spef_ctx* c, const uint8_t* head_bytes, size_t bytes) {
   memcpy(&h, head_bytes, sizeof(h));
   if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_BLOB, "bad blob magic");
   if (h.version != kBlobVersion) return fail(SPEF_ERR_BLOB, "unsupported blob version");
-  if (h.dtype != DT_F16 && h.dtype != DT_BF16) return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
+  if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8) return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
   if (h.ops_off + (uint64_t)h.n_ops * sizeof(OpDesc) > bytes || h.data_off + h.data_bytes > bytes)
     return fail(SPEF_ERR_BLOB, "blob truncated");
   std::vector<OpDesc> ops(h.n_ops);
   memcpy(ops.data(), head_bytes + h.ops_off, h.n_ops * sizeof(OpDesc));
   for (const OpDesc& op : ops) {
-    for (uint64_t off : {op.w0, op.b0, op.w1, op.b1, op.w2, op.b2})
+    for (uint64_t off : {op.w0, op.b0, op.w1, op.b1, op.w2, op.b2, op.x0, op.x1})
       if (off != kAbsent && (off >= h.data_bytes || (off & 15)))
         return fail(SPEF_ERR_BLOB, "tensor offset out of range / misaligned");
-    if (op.kind == OP_IRB && (op.cin % 8 || op.cout % 8 || op.hidden % 8 || (op.stride != 1 && op.stride != 2)))
+    if ((op.kind == OP_IRB || op.kind == OP_QIRB) &&
+        (op.cin % 8 || op.cout % 8 || op.hidden % 8 || (op.stride != 1 && op.stride != 2)))
       return fail(SPEF_ERR_BLOB, "unsupported inverted-residual geometry");
+    const bool qop = op.kind >= OP_QSTEM && op.kind <= OP_QFC;
+    if (qop != (h.dtype == DT_I8)) return fail(SPEF_ERR_BLOB, "op kind does not match the blob dtype");
+    if (op.kind == OP_QSTEM && (op.cout != 32 || op.x0 == kAbsent || op.w1 == kAbsent))
+      return fail(SPEF_ERR_BLOB, "int8 stem needs 32 outputs, an input LUT and scale");
+    if (op.kind == OP_QIRB && (op.x0 == kAbsent || ((op.flags & 1u) && op.x1 == kAbsent)))
+      return fail(SPEF_ERR_BLOB, "int8 block lacks its projection init / residual rescale");
+    if (op.kind == OP_QFC && (op.x0 == kAbsent || op.x1 == kAbsent))
+      return fail(SPEF_ERR_BLOB, "int8 FC lacks its constants");
   }
   c->hdr = h;
   c->ops = std::move(ops);
@@ -437,6 +617,27 @@ static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_devi
   const uint8_t* src = (const uint8_t*)blob + c->hdr.data_off;
   HIP_TRY(hipMemcpy(c->d_data, src, c->hdr.data_bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
   c->data_bytes = c->hdr.data_bytes;
+  if (c->hdr.dtype == DT_I8) {   // small host-side constants of the int8 schedule, fetched once
+    c->q8_res.assign(c->ops.size(), {0, 0, 0});
+    c->q8_fc_hw = 0;
+    for (size_t i = 0; i < c->ops.size(); ++i) {
+      const OpDesc& op = c->ops[i];
+      if (op.kind == OP_QSTEM)
+        HIP_TRY(hipMemcpy(&c->q8_s_img, c->d_data + op.x0, sizeof(float), hipMemcpyDeviceToHost));
+      if (op.kind == OP_QIRB && (op.flags & 1u))
+        HIP_TRY(hipMemcpy(c->q8_res[i].data(), c->d_data + op.x1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost));
+      if (op.kind == OP_QFC) {
+        const size_t np_ = (op.cout + 15) & ~15u;
+        c->q8_sw.resize(np_);
+        c->q8_bias.resize(np_);
+        c->q8_wsum.resize(np_);
+        HIP_TRY(hipMemcpy(c->q8_sw.data(), c->d_data + op.b0, np_ * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(c->q8_bias.data(), c->d_data + op.w1, np_ * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(c->q8_wsum.data(), c->d_data + op.x0, np_ * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&c->q8_sl, c->d_data + op.x1, sizeof(double), hipMemcpyDeviceToHost));
+      }
+    }
+  }
   c->loaded = true;
   free_workspace(c);
   return SPEF_OK;
@@ -474,6 +675,10 @@ int spef_reserve(spef_ctx* c, int B, int H, int W) {
     HIP_TRY(hipMalloc(&c->kpfeat, (size_t)B * fh * fw * c->hdr.feat_c * sizeof(float)));
     HIP_TRY(hipMalloc(&c->kppart, (size_t)kKpSplits * B * ((c->hdr.n_out0 + 15) & ~15u) * sizeof(float)));
   }
+  if (c->hdr.dtype == DT_I8) {
+    const int rc = q8_prepare_fc(c, fh * fw);
+    if (rc) return rc;
+  }
   c->buf_bytes = bytes;
   c->ws_B = B;
   c->ws_H = H;
@@ -489,6 +694,31 @@ int spef_forward(spef_ctx* c, const void* input, int layout, int B, int H, int W
   if (layout != SPEF_IN_U8_NHWC && layout != SPEF_IN_F32_NCHW) return fail(SPEF_ERR_ARG, "bad layout");
   Dev d(c->device);
   hipStream_t s = (hipStream_t)stream;
+  if (c->hdr.dtype == DT_I8) {   // INT8 path: backbone + TruncTo8bit pool + int8 FC (ursonet.py:36-93)
+    if (!out1 && c->hdr.n_out1) return fail(SPEF_ERR_ARG, "null position output");
+    int fh = 0, fw = 0;
+    rc = run_backbone_q8(c, input, layout, B, H, W, s, 0, -1, nullptr, nullptr, &fh, &fw, nullptr);
+    if (rc) return rc;
+    if (fh * fw != c->q8_fc_hw) return fail(SPEF_ERR_STATE, "int8 head constants not prepared (spef_reserve)");
+    for (const OpDesc& op : c->ops)
+      if (op.kind == OP_QFC) {
+        QGemmArgs a{};
+        a.epi = QEPI_FC;
+        a.x = (const int8_t*)c->pooled;
+        a.w = ptr<int8_t>(c, op.w0);
+        a.init = c->q8_fc_init;
+        a.y = out0;
+        a.y1 = out1;
+        a.sc = c->q8_fc_sc;
+        a.n_split = (int)c->hdr.n_out0;
+        a.M = B;
+        a.K = (int)op.cin;
+        a.N = (int)op.cout;
+        HIP_TRY(prof_launch(c, s, "q_gemm<fc>", (double)B * op.cin + (double)op.cout * op.cin + (double)B * op.cout * 4,
+                            2.0 * B * op.cin * op.cout, [&] { return launch_q_gemm(a, s); }));
+      }
+    return SPEF_OK;
+  }
   if (c->hdr.head == HEAD_URSONET) {
     if (!out1 && c->hdr.n_out1) return fail(SPEF_ERR_ARG, "null position output");
     rc = run_backbone(c, input, layout, B, H, W, s, 0, -1, nullptr, nullptr, nullptr, nullptr);
@@ -528,6 +758,12 @@ int spef_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int 
   hipStream_t s = (hipStream_t)stream;
   void* feat = nullptr;
   int fc_ = 0, fh = 0, fw = 0;
+  if (c->hdr.dtype == DT_I8) {   // dequantized last-conv map: code * s_l
+    rc = run_backbone_q8(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw, nullptr);
+    if (rc) return rc;
+    HIP_TRY(launch_q_to_f32(feat, features, (int64_t)B * fh * fw * fc_, 1, (float)c->q8_sl, s));
+    return SPEF_OK;
+  }
   rc = run_backbone(c, input, layout, B, H, W, s, 2, -1, &feat, &fc_, &fh, &fw, features);
   if (rc) return rc;
   return SPEF_OK;
@@ -542,9 +778,16 @@ int spef_probe(spef_ctx* c, const void* input, int layout, int B, int H, int W, 
   hipStream_t s = (hipStream_t)stream;
   void* act = nullptr;
   int ch = 0, h = 0, w = 0;
-  rc = run_backbone(c, input, layout, B, H, W, s, 1, stop_op, &act, &ch, &h, &w);
-  if (rc) return rc;
-  HIP_TRY(launch_to_f32((int)c->hdr.dtype, act, out, (int64_t)B * h * w * ch, s));
+  if (c->hdr.dtype == DT_I8) {   // raw integer codes (stem: u8, block outputs: int8)
+    int uns = 0;
+    rc = run_backbone_q8(c, input, layout, B, H, W, s, 1, stop_op, &act, &ch, &h, &w, &uns);
+    if (rc) return rc;
+    HIP_TRY(launch_q_to_f32(act, out, (int64_t)B * h * w * ch, uns, 1.0f, s));
+  } else {
+    rc = run_backbone(c, input, layout, B, H, W, s, 1, stop_op, &act, &ch, &h, &w);
+    if (rc) return rc;
+    HIP_TRY(launch_to_f32((int)c->hdr.dtype, act, out, (int64_t)B * h * w * ch, s));
+  }
   if (oc) *oc = ch;
   if (oh) *oh = h;
   if (ow) *ow = w;

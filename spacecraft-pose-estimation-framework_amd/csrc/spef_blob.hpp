@@ -10,6 +10,17 @@
 //   OP_LAST  ConvBnAct 320->1280 1x1 (mobilenet_v2.py:264)    w0 act [Np][Kp], b0 fp32 [Np]
 //   OP_FC    URSONetHead ori|pos Linear (ursonet.py:17-25)    w0 fp32 [Np][1280] rows = ori then pos, b0 fp32 [Np]
 //   OP_FCKP  KeypointRegressionHead (keypoints.py:18-21)      w0 fp32 [Np][F] columns in NHWC flatten order
+//
+// int8 blob (dtype 3; semantics oracle/int8_ref.py, params spef_amd/quant.py). RQ(n) = requant table over
+// Np channels: int64 M[Np], int64 B[Np], int32 S[Np] back to back.
+//   OP_QSTEM w0 int8 [32][28] (k=ky*9+kx*3+ci, k=27 zero), b0 RQ(32), w1 int8 LUT[256] (u8 pixel -> input
+//            quant), x0 fp32 [1] input scale (f32 NCHW path)
+//   OP_QIRB  w0/b0 expand int8 [Np][Kp64] + RQ (absent if t==1); w1/b1 dw int8 [9][hidden] + RQ;
+//            w2/b2 project int8 [Np][Kp64] + RQ; x0 int32 [Np] project accumulator init (128 * sum_k q_w);
+//            x1 int64 [3] residual-join rescale (R, RB, RS) when flags & 1; flags & 2: unsigned block input
+//   OP_QLAST w0 int8 [Np][Kp64], b0 RQ
+//   OP_QFC   w0 int8 [Np][1280] (ori rows then pos), b0 fp64 [Np] weight scales, w1 fp64 [Np] float bias,
+//            x0 int32 [Np] 128 * sum_k q_w, x1 fp64 [1] last-conv activation scale
 // act = the activation storage type (fp16 or bf16); Kp = K rounded up to 32, Np = N rounded up to 16, padding 0.
 // BatchNorm (eps 1e-5) is folded: w' = w*g/sqrt(v+eps), b' = beta - mean*g/sqrt(v+eps).
 #pragma once
@@ -21,7 +32,10 @@ static const char kBlobMagic[8] = {'S', 'P', 'E', 'F', 'M', 'I', '3', '5'};
 static const uint32_t kBlobVersion = 1;
 static const uint64_t kAbsent = ~0ull;
 
-enum OpKind : uint32_t { OP_STEM = 1, OP_IRB = 2, OP_LAST = 3, OP_FC = 4, OP_FCKP = 5 };
+enum OpKind : uint32_t {
+  OP_STEM = 1, OP_IRB = 2, OP_LAST = 3, OP_FC = 4, OP_FCKP = 5,
+  OP_QSTEM = 11, OP_QIRB = 12, OP_QLAST = 13, OP_QFC = 14   // int8 blob (dtype 3)
+};
 enum HeadKind : uint32_t { HEAD_URSONET = 0, HEAD_KEYPOINTS = 1 };
 
 #pragma pack(push, 1)
@@ -35,7 +49,8 @@ struct BlobHeader {
 struct OpDesc {
   uint32_t kind, cin, cout, hidden, stride, expand, flags, pad0;
   uint64_t w0, b0, w1, b1, w2, b2;
-  uint8_t reserved[48];
+  uint64_t x0, x1;   // int8 ops only (kAbsent otherwise)
+  uint8_t reserved[32];
 };
 #pragma pack(pop)
 static_assert(sizeof(BlobHeader) == 128, "BlobHeader must be 128 bytes");

@@ -6,7 +6,7 @@
 
 namespace spef {
 
-enum Dtype : int { DT_F16 = 1, DT_BF16 = 2 };
+enum Dtype : int { DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3 };
 enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RELU_F32 = 3 /* ReLU, fp32 output */ };
 enum InLayout : int { IN_U8_NHWC = 0, IN_F32_NCHW = 1 };
 
@@ -72,5 +72,40 @@ hipError_t launch_decode_ori(const float* logits, int B, int n_bins, const doubl
 hipError_t launch_normalize_ori(const float* raw, int B, float* quat, hipStream_t s);
 hipError_t launch_decode_pos(const float* logits, int B, int n_bins, const double* grid, float* soft,
                              float* pos, int* status, hipStream_t s);
+
+// ---- INT8 path (k_q8.hip; integer semantics of oracle/int8_ref.py) ----
+enum QEpi : int { QEPI_RELU = 0, QEPI_PROJ = 1, QEPI_PROJ_RES = 2, QEPI_FC = 3 };
+
+// Input quant + stem (u8 NHWC via `lut`, or f32 NCHW via round(x / s_img)) -> u8 NHWC [B][OH][OW][32].
+// w28: int8 [32][28] (k = ky*9+kx*3+ci, k 27 zero); M/B/S: requant [32].
+hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_img, const int8_t* w28,
+                         const int64_t* M, const int64_t* Bq, const int32_t* S, uint8_t* y, int B, int H, int W,
+                         int OH, int OW, hipStream_t s);
+// Depthwise 3x3: u8 in, int8 [9][C] weights -> ReLU-quant, stored offset (u - 128) int8.
+hipError_t launch_q_dw(const uint8_t* x, const int8_t* w9, const int64_t* M, const int64_t* Bq, const int32_t* S,
+                       int8_t* y, int B, int H, int W, int C, int stride, int OH, int OW, hipStream_t s);
+struct QGemmArgs {
+  int epi;
+  const int8_t* x;          // [M][K] int8 rows
+  const int8_t* w;          // [Np][Kp64] int8
+  const int32_t* init;      // [Np] accumulator init (offset correction, FC bias) or null
+  const int64_t* rqM;       // requant [Np] (RELU / PROJ / PROJ_RES)
+  const int64_t* rqB;
+  const int32_t* rqS;
+  const int8_t* r;          // PROJ_RES: residual [M][N] int8
+  int64_t rm, rb;           // PROJ_RES: residual-join rescale
+  int rs;
+  void* y;                  // int8/u8 [M][N]; FC: float [M][n_split]
+  float* y1;                // FC: float [M][N - n_split]
+  const float* sc;          // FC: per-column output scale [Np]
+  int n_split;
+  int64_t M;
+  int K, N;
+};
+hipError_t launch_q_gemm(const QGemmArgs& a, hipStream_t s);
+// TruncTo8bit average pool over the whole map: u8 [B][HW][C] -> offset int8 [B][C] = ((sum) >> tb) - 128.
+hipError_t launch_q_pool(const uint8_t* x, int8_t* p, int B, int HW, int C, int tb, hipStream_t s);
+// int8 (is_unsigned 0) or u8 codes -> fp32 code * scale.
+hipError_t launch_q_to_f32(const void* x, float* y, int64_t n, int is_unsigned, float scale, hipStream_t s);
 
 }  // namespace spef

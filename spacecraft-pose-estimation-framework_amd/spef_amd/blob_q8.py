@@ -1,0 +1,162 @@
+"""INT8 weight blob: reference ``state_dict`` + activation scales (``quant.QParams``) -> blob dtype 3.
+
+Quantisation follows the reference's Brevitas layers (quantizers.py:16-20 per-channel int8 weights; the
+conv -> BatchNorm -> QuantReLU / shared-quantizer chain of brevitas_layers.py:10-136) in the integer form the
+MI355X kernels execute (csrc/k_q8.hip); the formulas are written out in oracle/int8_ref.py's header and the
+op layout in csrc/spef_blob.hpp. Everything is computed in float64 on the host, once:
+
+  * weights: s_w[c] = max|W[c]| / 127, q_w = clip(rint(W / s_w), -127, 127)
+  * conv + BN + quant: m = (s_in * s_w * g) / s_out, b = h / s_out  (g = gamma/sqrt(var+eps), h = beta - mean*g),
+    as fixed point (M, B, sh): q = (acc * M + B) >> sh
+  * unsigned MFMA operands are stored offset by -128; the accumulator starts at 128 * sum_k q_w
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+
+from .arch import Arch, LAST_CHANNELS, arch_from_state_dict
+from .blob import ABSENT, DT_I8, HEAD_URSONET, OP_QFC, OP_QIRB, OP_QLAST, OP_QSTEM, _Data, _np, assemble
+from .quant import validate
+
+BN_EPS = 1e-5
+
+
+def weight_q(w):
+    w = _np(w).astype(np.float64)
+    s = np.maximum(np.abs(w.reshape(w.shape[0], -1)).max(axis=1) / 127.0, 2e-16)
+    q = np.clip(np.rint(w / s.reshape((-1,) + (1,) * (w.ndim - 1))), -127, 127).astype(np.int64)
+    return q, s
+
+
+def _bn(sd, prefix):
+    g = _np(sd[f'{prefix}.1.weight']).astype(np.float64) / np.sqrt(
+        _np(sd[f'{prefix}.1.running_var']).astype(np.float64) + BN_EPS)
+    h = _np(sd[f'{prefix}.1.bias']).astype(np.float64) - _np(sd[f'{prefix}.1.running_mean']).astype(np.float64) * g
+    return g, h
+
+
+def fixed(m, b):
+    """x * m + b in fixed point: (M, B incl. rounding half, sh), |m| 2**sh in [2**29, 2**30), |b| 2**sh < 2**61."""
+    m = np.atleast_1d(np.asarray(m, np.float64))
+    b = np.broadcast_to(np.atleast_1d(np.asarray(b, np.float64)), m.shape)
+    M = np.zeros(m.shape, np.int64)
+    B = np.zeros(m.shape, np.int64)
+    S = np.zeros(m.shape, np.int64)
+    for i in range(m.size):
+        em = math.frexp(abs(m[i]))[1] if m[i] != 0 else -30
+        eb = math.frexp(abs(b[i]))[1] if b[i] != 0 else -200
+        sh = int(min(30 - em, 61 - eb, 62))
+        if sh < 1:
+            raise ValueError(f'requant scale out of range (m={m[i]}, b={b[i]})')
+        M[i] = int(np.rint(math.ldexp(m[i], sh)))
+        B[i] = int(np.rint(math.ldexp(b[i], sh))) + (1 << (sh - 1))
+        S[i] = sh
+    return M, B, S
+
+
+def _rq(data: _Data, M, B, S) -> int:
+    n = M.size
+    np_ = (n + 15) // 16 * 16
+    m = np.zeros(np_, np.int64)
+    bb = np.zeros(np_, np.int64)
+    ss = np.ones(np_, np.int32)
+    m[:n], bb[:n], ss[:n] = M, B, S
+    return data.add(m.tobytes() + bb.tobytes() + ss.tobytes())
+
+
+def _conv(sd, prefix, s_in, s_out):
+    q, s_w = weight_q(sd[f'{prefix}.0.weight'])
+    g, h = _bn(sd, prefix)
+    return q, fixed((s_in * s_w * g) / s_out, h / s_out)
+
+
+def _pw(data: _Data, q):
+    """int8 [Np][Kp64] (zero padded) + the offset-correction init 128 * sum_k q_w as int32 [Np]."""
+    cout, cin = q.shape[0], q.shape[1]
+    kp, np_ = (cin + 63) // 64 * 64, (cout + 15) // 16 * 16
+    w = np.zeros((np_, kp), np.int8)
+    w[:cout, :cin] = q.reshape(cout, cin)
+    init = np.zeros(np_, np.int32)
+    init[:cout] = 128 * q.reshape(cout, cin).sum(axis=1)
+    return data.add(w.tobytes()), init
+
+
+def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None) -> bytes:
+    """Pack a reference-layout FP32 state_dict + activation scales into an int8 blob (URSONet head)."""
+    arch = arch or arch_from_state_dict(sd)
+    if arch.head != 'ursonet':
+        raise NotImplementedError('the int8 path mirrors QURSONetHead (ursonet.py:36-93) only')
+    validate(qp)
+    fp = 'features.features'
+    data = _Data()
+    ops = []
+
+    # stem + input quant
+    q, (M, B, S) = _conv(sd, f'{fp}.0', qp['image'], qp['stem'])
+    w28 = np.zeros((32, 28), np.int8)
+    w28[:, :27] = q.transpose(0, 2, 3, 1).reshape(32, 27)        # k = ky*9 + kx*3 + ci
+    x = np.arange(256, dtype=np.float32) / np.float32(255.0)
+    lut = np.clip(np.rint(x / np.float32(qp['image'])), -128, 127).astype(np.int8)
+    ops.append((OP_QSTEM, 3, 32, 0, 2, 1, 0, data.add(w28.tobytes()), _rq(data, M, B, S), data.add(lut.tobytes()),
+                ABSENT, ABSENT, ABSENT, data.add(np.float32(qp['image']).tobytes()), ABSENT))
+
+    s_x = qp['stem']
+    nb = len(arch.blocks)
+    for n, blk in enumerate(arch.blocks):
+        bq = qp['blocks'][n]
+        s_q = bq['quant']
+        s_next = qp['blocks'][n + 1]['quant'] if n + 1 < nb else qp['final']
+        s_in = s_q if s_q is not None else s_x
+        j = 0
+        e_w = e_b = ABSENT
+        if blk.expand != 1:
+            q, (M, B, S) = _conv(sd, f'{fp}.{blk.index}.conv.0', s_in, bq['expand'])
+            e_w, _ = _pw(data, q)
+            e_b = _rq(data, M, B, S)
+            s_y, j = bq['expand'], 1
+        else:
+            s_y = s_in
+        q, (M, B, S) = _conv(sd, f'{fp}.{blk.index}.conv.{j}', s_y, bq['dw'])
+        w9 = np.ascontiguousarray(q[:, 0].reshape(q.shape[0], 9).T.astype(np.int8))     # [9][C], tap = ky*3+kx
+        d_w, d_b = data.add(w9.tobytes()), _rq(data, M, B, S)
+        p_out = s_q if blk.residual else s_next
+        q, (M, B, S) = _conv(sd, f'{fp}.{blk.index}.conv.{j + 1}', bq['dw'], p_out)
+        p_w, init = _pw(data, q)
+        p_b = _rq(data, M, B, S)
+        x1 = ABSENT
+        if blk.residual:
+            R, RB, RS = fixed(s_q / s_next, 0.0)
+            x1 = data.add(np.array([R[0], RB[0], RS[0]], np.int64).tobytes())
+        flags = (1 if blk.residual else 0) | (2 if s_q is None else 0)
+        ops.append((OP_QIRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, flags,
+                    e_w, e_b, d_w, d_b, p_w, p_b, data.add(init.tobytes()), x1))
+
+    q, (M, B, S) = _conv(sd, arch.last.prefix, qp['final'], qp['last'])
+    l_w, _ = _pw(data, q)
+    ops.append((OP_QLAST, arch.last.cin, arch.last.cout, 0, 1, 1, 0, l_w, _rq(data, M, B, S),
+                ABSENT, ABSENT, ABSENT, ABSENT))
+
+    rows, sws, bs = [], [], []
+    for key in ('head.ori.1', 'head.pos.0'):
+        q, s_w = weight_q(sd[f'{key}.weight'])
+        rows.append(q)
+        sws.append(s_w)
+        bs.append(_np(sd[f'{key}.bias']).astype(np.float64))
+    q = np.concatenate(rows)
+    n = q.shape[0]
+    np_ = (n + 15) // 16 * 16
+    w = np.zeros((np_, LAST_CHANNELS), np.int8)
+    w[:n] = q
+    sw = np.zeros(np_, np.float64)
+    sw[:n] = np.concatenate(sws)
+    bias = np.zeros(np_, np.float64)
+    bias[:n] = np.concatenate(bs)
+    wsum = np.zeros(np_, np.int32)
+    wsum[:n] = 128 * q.sum(axis=1)
+    ops.append((OP_QFC, LAST_CHANNELS, n, 0, 1, 1, 0, data.add(w.tobytes()), data.add(sw.tobytes()),
+                data.add(bias.tobytes()), ABSENT, ABSENT, ABSENT, data.add(wsum.tobytes()),
+                data.add(np.float64(qp['last']).tobytes())))
+    return assemble(DT_I8, HEAD_URSONET, rows[0].shape[0], rows[1].shape[0], 0, 0, ops, data)

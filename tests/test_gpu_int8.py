@@ -1,0 +1,75 @@
+"""INT8 path (C5) on the GPU vs oracle/int8_ref.py: BIT-EXACT integer activations and head outputs.
+
+Parity vs Brevitas itself is unpinned (brevitas absent; see oracle/int8_ref.py); the integer semantics are
+pinned here, and their distance to the float fake-quant graph and to FP32 is measured in test_int8_oracle.py.
+"""
+import numpy as np
+import pytest
+import torch
+
+from bench import synth_frames
+from oracle import int8_ref as Q
+from oracle import model_ref as M
+from spef_amd.arch import mobilenet_v2
+from spef_amd.blob_q8 import pack_int8
+from spef_amd.quant import calibrate
+from spef_amd.weights import synthetic_state_dict
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope='module')
+def q8():
+    from spef_amd.engine import Engine
+    sd = synthetic_state_dict(mobilenet_v2(), seed=1001)
+    qp = calibrate(sd, synth_frames(4, 128, 128, 900))
+    e = Engine(pack_int8(sd, qp), 'cuda:0')
+    yield e, sd, qp
+    e.close()
+
+
+def _nhwc(a):
+    return a.transpose(0, 2, 3, 1)
+
+
+@pytest.mark.parametrize('b,h,w', [(2, 64, 64), (1, 128, 96)])
+def test_int8_activations_bit_exact(q8, b, h, w):
+    eng, sd, qp = q8
+    fr = synth_frames(b, h, w, 7)
+    x = torch.from_numpy(fr).cuda()
+    for op in (0, 1, 2, 3, 5, 8, 12, 16, 17):
+        got = eng.probe(x, op).cpu().numpy()
+        ref = _nhwc(Q.int8_forward(fr, sd, qp, upto=op))
+        assert got.shape == ref.shape, op
+        np.testing.assert_array_equal(got, ref.astype(np.float32), err_msg=f'op {op}')
+
+
+@pytest.mark.parametrize('b,h,w', [(2, 64, 64), (3, 96, 128), (1, 512, 512)])
+def test_int8_head_outputs_bit_exact(q8, b, h, w):
+    eng, sd, qp = q8
+    fr = synth_frames(b, h, w, 11)
+    o, p = eng.forward(torch.from_numpy(fr).cuda())
+    ro, rp = Q.int8_forward(fr, sd, qp)
+    np.testing.assert_array_equal(o.cpu().numpy(), ro)
+    np.testing.assert_array_equal(p.cpu().numpy(), rp)
+
+
+def test_int8_f32_input_matches_u8(q8):
+    """NCHW float32 [0,1] input (the reference `images['torch']`) quantises to the same codes as the u8 LUT."""
+    eng, sd, qp = q8
+    fr = synth_frames(2, 64, 96, 3)
+    o8, p8 = eng.forward(torch.from_numpy(fr).cuda())
+    of, pf = eng.forward(M.u8_nhwc_to_nchw_f32(fr).contiguous().cuda())
+    np.testing.assert_array_equal(o8.cpu().numpy(), of.cpu().numpy())
+    np.testing.assert_array_equal(p8.cpu().numpy(), pf.cpu().numpy())
+
+
+def test_int8_batch_64_512(q8):
+    """C5 shape (B=64, 512x512): outputs equal the oracle on a sample of rows (rows are independent)."""
+    eng, sd, qp = q8
+    fr = synth_frames(64, 512, 512, 100)
+    o, p = eng.forward(torch.from_numpy(fr).cuda())
+    idx = [0, 37, 63]
+    ro, rp = Q.int8_forward(fr[idx], sd, qp)
+    np.testing.assert_array_equal(o.cpu().numpy()[idx], ro)
+    np.testing.assert_array_equal(p.cpu().numpy()[idx], rp)

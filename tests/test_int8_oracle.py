@@ -1,0 +1,74 @@
+"""INT8 oracle and packer on the CPU: integer semantics vs the Brevitas float fake-quant graph and FP32,
+blob structure, bit-width config handling."""
+import numpy as np
+import pytest
+
+from bench import synth_frames
+from oracle import int8_ref as Q
+from oracle import model_ref as M
+from spef_amd import blob as Bl
+from spef_amd.arch import mobilenet_v2
+from spef_amd.blob_q8 import pack_int8
+from spef_amd.quant import calibrate, check_bit_width, validate
+from spef_amd.weights import synthetic_state_dict
+
+
+@pytest.fixture(scope='module')
+def model():
+    sd = synthetic_state_dict(mobilenet_v2(), seed=1001)
+    qp = calibrate(sd, synth_frames(4, 128, 128, 900))
+    validate(qp)
+    return sd, qp
+
+
+def test_integer_semantics_close_to_fake_quant(model):
+    """The fixed-point requant differs from Brevitas' float graph only by rare 1-LSB rounding flips; measured
+    on the head outputs (parity vs Brevitas itself is unpinned: brevitas is absent)."""
+    sd, qp = model
+    fr = synth_frames(2, 96, 96, 5)
+    o, p = Q.int8_forward(fr, sd, qp)
+    fo, fp = Q.fake_quant_forward(fr, sd, qp)
+    scale = np.abs(fo.numpy()).max()
+    assert np.abs(o - fo.numpy()).max() < 0.05 * scale
+    stem_i = Q.int8_forward(fr, sd, qp, upto=0)
+    assert stem_i.min() >= 0 and stem_i.max() <= 255
+
+
+def test_int8_vs_fp32_accuracy(model):
+    """INT8 (calibrated PTQ stand-in for QAT) vs the FP32 model: logits within a few percent of their range."""
+    sd, qp = model
+    fr = synth_frames(2, 128, 128, 77)
+    o, p = Q.int8_forward(fr, sd, qp)
+    ro, rp = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd)
+    assert np.abs(o - ro.numpy()).max() < 0.06 * np.abs(ro.numpy()).max()
+    assert np.abs(p - rp.numpy()).max() < 0.1 * np.abs(rp.numpy()).max()
+
+
+def test_pack_int8_structure(model):
+    sd, qp = model
+    info = Bl.describe(pack_int8(sd, qp))
+    assert info['dtype'] == Bl.DT_I8 and info['n_out0'] == 1728 and info['n_out1'] == 3
+    kinds = [o[0] for o in info['ops']]
+    assert kinds == [Bl.OP_QSTEM] + [Bl.OP_QIRB] * 17 + [Bl.OP_QLAST, Bl.OP_QFC]
+    res = [o[6] & 1 for o in info['ops'][1:18]]
+    assert sum(res) == 10                                   # residual blocks of MobileNetV2
+    assert info['ops'][1][6] & 2                            # block 1 takes the unsigned stem output
+    assert all(o[14] != Bl.ABSENT for o in info['ops'][1:18])   # projection init present
+
+
+def test_fixed_point_requant_matches_float():
+    rng = np.random.default_rng(0)
+    m = rng.uniform(1e-6, 1.0, 64) * rng.choice([-1, 1], 64)
+    b = rng.uniform(-300, 300, 64)
+    M_, B_, S_ = Q.fixed(m, b)
+    # accumulators whose requantised value lands in (or near) the 8-bit range, as in the network
+    acc = np.rint(rng.uniform(-400, 400, (1000, 64)) / np.abs(m) - b / m).astype(np.int64)
+    got = Q.requant(acc, M_, B_, S_, -128, 255)
+    want = np.clip(np.floor(acc * m + b + 0.5), -128, 255)
+    assert np.abs(got - want).max() <= 1 and (got != want).mean() < 1e-4
+
+
+def test_bit_width_config():
+    check_bit_width({'image': '8', 'first_conv': '(8, 8)', 'inverted_residual': ['[(8, 8), (8, 8), (8,)]']})
+    with pytest.raises(NotImplementedError):
+        check_bit_width({'image': '8', 'first_conv': '(4, 4)'})
