@@ -111,7 +111,8 @@ def main():
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=64)
     ap.add_argument('--size', type=int, default=512)
-    ap.add_argument('--dtype', default='fp16', choices=['fp16', 'bf16'])
+    ap.add_argument('--dtype', default='fp16', choices=['fp16', 'bf16', 'int8'],
+                    help='int8 = the Brevitas-mirroring C5 path (calibrated activation scales)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--cpu-batch', type=int, default=64)
@@ -142,9 +143,16 @@ def main():
     from spef_amd.weights import synthetic_state_dict
 
     sd = None
+    blob = None
     if rank == 0:
         sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=1001)
-    dblob = broadcast_blob(Bl.pack(sd, dtype=args.dtype) if rank == 0 else None, dev)   # RCCL over xGMI
+        if args.dtype == 'int8':
+            from spef_amd.blob_q8 import pack_int8
+            from spef_amd.quant import calibrate
+            blob = pack_int8(sd, calibrate(sd, synth_frames(4, 128, 128, 900)))
+        else:
+            blob = Bl.pack(sd, dtype=args.dtype)
+    dblob = broadcast_blob(blob, dev)                 # RCCL over xGMI
     eng = Engine(dblob, dev)
     su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
     eng.set_decode_tables(su.orientation.histogram, None)
@@ -209,7 +217,9 @@ def main():
             'vs_baseline': None,
             'dtype': args.dtype,
             'data': 'synthetic SPEED-style uint8 frames resident in HBM; seeded random weights (BN-calibrated)',
-            'config': {'workload': f'C3: full net + decode, {S}x{S}, batch {B} per GPU', 'global_batch': B * world,
+            'config': {'workload': (f'C5: INT8 (Brevitas-mirroring, calibrated scales) full net + decode, {S}x{S}, '
+                                    f'batch {B} per GPU' if args.dtype == 'int8' else
+                                    f'C3: full net + decode, {S}x{S}, batch {B} per GPU'), 'global_batch': B * world,
                        'image_size': S, 'parallelism': f'frame-parallel x{world} (RCCL weight bcast)'},
             'roofline': {'bound': 'hbm', 'kernel': dom_key, 'achieved': round(ach_gbs, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(ach_gbs / HBM_PEAK_GBS, 4),
@@ -218,7 +228,8 @@ def main():
                          'algorithmic_bytes_per_launch': round(byts / n),
                          'avg_launch_us': round(avg_s * 1e6, 2), 'launches_per_step': n / args.steps,
                          'kernel_mfma_tflops': round(ach_tfl, 2)},
-            'mfma_utilisation_whole_net': round(fpi * value / world / 1e12 / MFMA_PEAK_TFLOPS, 5),
+            'mfma_utilisation_whole_net': round(fpi * value / world / 1e12 /
+                                                (2 * MFMA_PEAK_TFLOPS if args.dtype == 'int8' else MFMA_PEAK_TFLOPS), 5),
             'kernels': {k: {'launches_per_step': v[0] / args.steps, 'ms_per_step': round(v[1] / args.steps, 4),
                             'GB/s': round(v[2] / (v[1] / 1e3) / 1e9, 1) if v[1] > 0 else None}
                         for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1])},
