@@ -15,7 +15,7 @@ namespace spef {
 
 template <typename DT, int TH, int TW, int NW>
 __global__ __launch_bounds__(NW * 64) void front_kernel(
-    const uint8_t* __restrict__ X, const float* __restrict__ ws, const float* __restrict__ bs,
+    const uint8_t* __restrict__ X, const typename DT::T* __restrict__ wsp, const float* __restrict__ bs,
     const float* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int SH_img, int SW_img,
     int tiles_x, int tiles_y, uint32_t nwg) {
@@ -24,7 +24,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   using x4 = typename DT::x4;
   constexpr int SH = TH + 2, SW = TW + 2;          // stem tile (block-1 output tile + depthwise halo)
   constexpr int IH = 2 * SH + 1, IW = 2 * SW + 1;  // input tile
-  constexpr int IRS = (IW * 3 + 15) / 16 * 16;     // input LDS row stride (bytes)
+  constexpr int IRS = ((IW * 3 + 3) / 4 * 4 + 4 + 15) / 16 * 16;   // input LDS row stride (bytes)
   constexpr int PS = SH * SW, PS16 = (PS + 15) / 16, PSP = PS16 * 16;
   constexpr int XS = 48;                           // stem-map row stride: 96 B, conflict-free b128 reads
   constexpr int POUT16 = TH * TW / 16, QPW = POUT16 / NW;
@@ -44,30 +44,75 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   const int sy0 = oy0 - 1, sx0 = ox0 - 1;            // stem tile origin
   const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;    // input tile origin
 
-  // ---- 1. input bytes -> LDS (zero outside the image = the stem's padding)
+  // ---- 1. input bytes -> LDS (zero outside the image = the stem's padding). Each input row is a contiguous
+  // IW*3-byte run of the NHWC frame, fetched as aligned dwords with ALL of a thread's loads issued before any
+  // LDS store. Interior tiles (every column inside the image, W % 4 == 0) copy the dwords as they are and the
+  // reader offsets by the common misalignment `mis`; edge tiles scatter bytes and zero the outside columns.
+  int mis = 0;
   {
+    constexpr int RB = IW * 3;                        // bytes per input-tile row
+    constexpr int DPR = (RB + 3) / 4 + 1;             // dwords covering a row at any byte alignment
+    constexpr int ND = IH * DPR, NIT = (ND + NW * 64 - 1) / (NW * 64);
+    static_assert(4 * DPR <= IRS, "LDS row holds the dword-aligned run");
     const uint8_t* Xb = X + (size_t)b * H * W * 3;
-    for (int u = tid; u < IH * IW * 3; u += NW * 64) {
-      const int r = u / (IW * 3), cb = u - r * (IW * 3);
-      const int iy = iy0 + r, ix = ix0 + cb / 3;
-      uint8_t v = 0;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = Xb[((size_t)iy * W + ix0) * 3 + cb];
-      In[r * IRS + cb] = v;
+    const int64_t img_bytes = (int64_t)H * W * 3;
+    const bool fast = (W & 3) == 0 && ix0 >= 0 && ix0 + IW <= W;
+    uint32_t v[NIT];
+    int64_t a[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int d = tid + NW * 64 * i;
+      const int r = d / DPR, k = d - r * DPR;
+      const int iy = iy0 + r;
+      const int64_t rs = ((int64_t)iy * W + ix0) * 3;
+      a[i] = (rs & ~(int64_t)3) + 4 * k;
+      v[i] = 0;
+      if (d < ND && iy >= 0 && iy < H && a[i] >= 0) {
+        if (a[i] + 4 <= img_bytes) {
+          v[i] = *reinterpret_cast<const uint32_t*>(Xb + a[i]);
+        } else {
+          for (int j = 0; j < 4; ++j)
+            if (a[i] + j < img_bytes) v[i] |= (uint32_t)Xb[a[i] + j] << (8 * j);
+        }
+      }
+    }
+    if (fast) {
+      mis = (int)((((int64_t)iy0 * W + ix0) * 3) & 3);   // the same for every row when W % 4 == 0
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        const int d = tid + NW * 64 * i;
+        if (d < ND) {
+          const int r = d / DPR, k = d - r * DPR;
+          *reinterpret_cast<uint32_t*>(In + r * IRS + 4 * k) = v[i];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NIT; ++i) {
+        const int d = tid + NW * 64 * i;
+        if (d >= ND) continue;
+        const int r = d / DPR;
+        const int iy = iy0 + r;
+        const int64_t rs = ((int64_t)iy * W + ix0) * 3;
+        const bool row_ok = iy >= 0 && iy < H;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int o = (int)(a[i] + j - rs);             // byte offset inside the tile row
+          if (o < 0 || o >= RB) continue;
+          const int ix = ix0 + o / 3;
+          In[r * IRS + o] = (row_ok && ix >= 0 && ix < W) ? (uint8_t)(v[i] >> (8 * j)) : (uint8_t)0;
+        }
+      }
     }
     for (int u = tid; u < 9 * 32 + 32; u += NW * 64) Sl[u] = u < 9 * 32 ? Wd[(u >> 5) * 32 + (u & 31)] : bd[u - 9 * 32];
   }
-  // stem weight fragments (fp32 [27][32] -> /255 -> hi + lo), channel tiles t = 0, 1
+  // stem weight fragments: /255-folded weights split hi + lo, [2][32 ch][32 k] from the blob; tiles t = 0, 1
   x8 ahi[2], alo[2];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const int k = 8 * kg + e;
-      const float w = k < 27 ? ws[k * 32 + 16 * t + r16] / 255.0f : 0.0f;
-      const T hi = (T)w;
-      ahi[t][e] = hi;
-      alo[t][e] = (T)(w - (float)hi);
-    }
+  for (int t = 0; t < 2; ++t) {
+    ahi[t] = load8<DT>(wsp + (16 * t + r16) * 32 + 8 * kg);
+    alo[t] = load8<DT>(wsp + 32 * 32 + (16 * t + r16) * 32 + 8 * kg);
+  }
   const float4 sb0 = *reinterpret_cast<const float4*>(bs + 4 * kg);
   const float4 sb1 = *reinterpret_cast<const float4*>(bs + 16 + 4 * kg);
   // per-lane tap offsets inside the input tile for k = 8kg + e: (k / 9) * IRS + k % 9
@@ -83,7 +128,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   for (int pt = wave; pt < PS16; pt += NW) {
     const int p = pt * 16 + r16;
     const int spy = p / SW, spx = p - (p / SW) * SW;
-    const int base = (2 * spy) * IRS + 2 * spx * 3;
+    const int base = (2 * spy) * IRS + 2 * spx * 3 + mis;
     x8 bx;
 #pragma unroll
     for (int e = 0; e < 8; ++e) bx[e] = (koff[e] >= 0 && p < PS) ? (T)(float)In[base + koff[e]] : (T)0.0f;
@@ -144,7 +189,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   }
 }
 
-hipError_t launch_front(int dtype, const void* x, const float* ws, const float* bs, const float* wd, const float* bd,
+hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* bs, const float* wd, const float* bd,
                         const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                         hipStream_t s) {
   constexpr int TH = 16, TW = 16, NW = 8;
@@ -153,10 +198,10 @@ hipError_t launch_front(int dtype, const void* x, const float* ws, const float* 
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   if (dtype == DT_F16)
-    front_kernel<F16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, ws, bs, wd, bd, (const _Float16*)wp, bp,
+    front_kernel<F16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, (const _Float16*)wsp, bs, wd, bd, (const _Float16*)wp, bp,
                                                           (_Float16*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   else
-    front_kernel<BF16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, ws, bs, wd, bd, (const __bf16*)wp, bp,
+    front_kernel<BF16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, (const __bf16*)wsp, bs, wd, bd, (const __bf16*)wp, bp,
                                                            (__bf16*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   return hipGetLastError();
 }

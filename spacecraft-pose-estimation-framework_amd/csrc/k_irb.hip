@@ -162,15 +162,26 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     constexpr int GPR = G::CINP / 8;        // 16-B groups per LDS row (CIN 16: 2)
     constexpr int CG = CIN / 8;             // valid groups
     const T* Xb = X + (size_t)b * H * W * CIN;
-    for (int u = tid; u < G::PINP * GPR; u += NW * 64) {
+    constexpr int NU = G::PINP * GPR, NIT = (NU + NW * 64 - 1) / (NW * 64);
+    x8 xin[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {   // all loads in flight before the first LDS store
+      const int u = tid + NW * 64 * i;
       const int p = u / GPR, g = u - p * GPR;
-      x8 v = zero8<DT>();
-      if (p < G::PIN && g < CG) {
+      xin[i] = zero8<DT>();
+      if (u < NU && p < G::PIN && g < CG) {
         const int py = p / G::IW, px = p - py * G::IW;
         const int iy = iy0 + py, ix = ix0 + px;
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W) v = load8<DT>(Xb + ((size_t)iy * W + ix) * CIN + g * 8);
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) xin[i] = load8<DT>(Xb + ((size_t)iy * W + ix) * CIN + g * 8);
       }
-      *reinterpret_cast<x8*>(Xs + p * G::XS + g * 8) = v;
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int u = tid + NW * 64 * i;
+      if (u < NU) {
+        const int p = u / GPR, g = u - p * GPR;
+        *reinterpret_cast<x8*>(Xs + p * G::XS + g * 8) = xin[i];
+      }
     }
     slab_store(0, slab_load(0));
     if constexpr (STW && EXPAND) {   // expand weights of chunk 0 (the project weights of chunk 0 follow the schedule)

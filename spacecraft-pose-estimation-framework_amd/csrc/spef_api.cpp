@@ -225,13 +225,13 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const OpDesc* nx = (&op + 1 < c->ops.data() + c->ops.size()) ? &op + 1 : nullptr;
       const bool front = c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx && nx->kind == OP_IRB &&
                          nx->cin == 32 && nx->hidden == 32 && nx->cout == 16 && nx->expand == 1 && nx->stride == 1 &&
-                         op.cout == 32;
+                         op.cout == 32 && op.x0 != kAbsent;
       if (front) {
         void* y = c->buf[0];
         const double px = (double)B * OH * OW;
         HIP_TRY(prof_launch(c, s, "front_kernel<stem+block1>", (double)B * h * w * 3 + px * 16 * 2,
                             px * (2 * 27 * 32 + 18 * 32 + 2 * 32 * 16), [&] {
-          return launch_front(dt, input, ptr<float>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
+          return launch_front(dt, input, ptr<void>(c, op.x0), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
                               ptr<float>(c, nx->b1), ptr<void>(c, nx->w2), ptr<float>(c, nx->b2), y, B, h, w, OH, OW, s);
         }));
         cur = y;

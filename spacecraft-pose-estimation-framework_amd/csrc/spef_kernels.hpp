@@ -47,8 +47,9 @@ hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int st
                       const void* we, const float* be, const float* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 
-// Stem (u8 NHWC input) fused with inverted-residual block 1 (32 -> dw -> 16), k_front.hip.
-hipError_t launch_front(int dtype, const void* x, const float* ws, const float* bs, const float* wd, const float* bd,
+// Stem (u8 NHWC input) fused with inverted-residual block 1 (32 -> dw -> 16), k_front.hip. wsp: /255-folded stem
+// weights split hi + lo in the activation dtype, [2][32][32] (blob OP_STEM x0).
+hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* bs, const float* wd, const float* bd,
                         const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 
 // Split-K fp32 head GEMM for very long K: part = workspace [splits][B][round_up(n,16)] floats.

@@ -60,6 +60,14 @@ def _to_act(a: np.ndarray, dtype: str) -> bytes:
     return r.tobytes()
 
 
+def _round_act(a: np.ndarray, dtype: str) -> np.ndarray:
+    """float32 -> nearest value of the activation dtype, returned as float32."""
+    a = np.ascontiguousarray(a, dtype=np.float32)
+    if dtype == 'fp16':
+        return a.astype(np.float16).astype(np.float32)
+    return np.frombuffer(_to_act(a, 'bf16'), np.uint16).astype(np.uint32).__lshift__(16).view(np.float32).reshape(a.shape)
+
+
 class _Data:
     def __init__(self):
         self.chunks: List[bytes] = []
@@ -100,8 +108,16 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
     # stem: [27][32], k = ky*9 + kx*3 + ci
     w, b = fold_bn(sd, arch.stem)
     ws = np.ascontiguousarray(w.transpose(2, 3, 1, 0).reshape(27, arch.stem.cout), dtype=np.float32)
+    # MFMA A operand of the fused front kernel (uint8 input): ToTensor's /255 folded in float32, split
+    # hi + lo in the activation dtype, [2][32 ch][32 k] (k = 27..31 zero)
+    w255 = ws / np.float32(255.0)
+    hi = np.zeros((arch.stem.cout, 32), np.float32)
+    hi[:, :27] = w255.T
+    hi_r = _round_act(hi, dtype)
+    lo_r = _round_act(hi - hi_r, dtype)
     ops.append((OP_STEM, 3, arch.stem.cout, 0, 2, 1, 0,
-                data.add(ws.tobytes()), data.add(np.asarray(b, np.float32).tobytes()), ABSENT, ABSENT, ABSENT, ABSENT))
+                data.add(ws.tobytes()), data.add(np.asarray(b, np.float32).tobytes()), ABSENT, ABSENT, ABSENT, ABSENT,
+                data.add(_to_act(np.concatenate([hi_r, lo_r]), dtype))))
 
     for blk in arch.blocks:
         convs = list(blk.convs)
