@@ -106,6 +106,13 @@ int spef_set_keypoints(spef_ctx* ctx, const float* kp3d, int n, const double* K,
 int spef_decode_keypoints(spef_ctx* ctx, const float* raw, int B, int apply_sigmoid, float* kp_out, float* quat,
                           float* pos, int* status, void* stream);
 
+/* Input preprocessing on the device (SPEDataset.__getitem__ + transforms.Resize(img_size), utils.py:212-249,
+ * speed.py:66-69): decoded frames uint8 [B x Hin x Win x 3] (RGB, HWC) -> uint8 [B x H x W x 3], bit-identical to
+ * Pillow's Image.resize((W, H), BILINEAR). The result feeds spef_forward with SPEF_IN_U8_NHWC (ToTensor's /255
+ * is fused into the stem). Temporary storage is owned by the context. */
+int spef_preprocess(spef_ctx* ctx, const uint8_t* frames, int B, int Hin, int Win, uint8_t* out, int H, int W,
+                    void* stream);
+
 /* Options. SPEF_OPT_FUSE_BLOCKS (default 1): run each inverted-residual block as one fused kernel
  * (expand + depthwise + project on-chip) where its geometry is in the fused table; 0 = one kernel per conv. */
 /* SPEF_OPT_FUSE_MIN_HW: fuse only blocks whose input has at least this many pixels per image (late,

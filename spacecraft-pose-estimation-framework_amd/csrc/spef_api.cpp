@@ -69,6 +69,13 @@ struct spef_ctx {
   float* q8_fc_sc = nullptr;       // [Np] f32(s_pool * s_w)
   int q8_fc_hw = 0, q8_fc_tb = 0;
   float q8_s_img = 0.f;                        // input scale (f32 NCHW path)
+  // preprocessing (Pillow BILINEAR resize): coefficient tables for the last (Hin, Win, H, W), temp image
+  int pre_key[4] = {0, 0, 0, 0};
+  int* pre_bh = nullptr;   // [W][2] (xmin, count), then [W][ksize_h] coefficients
+  int* pre_bv = nullptr;   // [H][2] (ymin - y0, count), then [H][ksize_v]
+  int pre_ksh = 0, pre_ksv = 0, pre_y0 = 0, pre_ht = 0;
+  uint8_t* pre_tmp = nullptr;
+  size_t pre_tmp_bytes = 0;
   std::vector<std::array<int64_t, 3>> q8_res;  // per op: residual-join rescale (R, RB, RS)
   // per-launch HIP-event profiling (bench.py roofline leg)
   bool profiling = false;
@@ -553,6 +560,9 @@ int spef_destroy(spef_ctx* c) {
   if (c->kp3d) hipFree(c->kp3d);
   if (c->kp_model) hipFree(c->kp_model);
   if (c->q8_fc_init) hipFree(c->q8_fc_init);
+  if (c->pre_bh) hipFree(c->pre_bh);
+  if (c->pre_bv) hipFree(c->pre_bv);
+  if (c->pre_tmp) hipFree(c->pre_tmp);
   if (c->q8_fc_sc) hipFree(c->q8_fc_sc);
   for (hipEvent_t e : c->pool) hipEventDestroy(e);
   delete c;
@@ -957,6 +967,87 @@ int spef_decode_keypoints(spef_ctx* c, const float* raw, int B, int apply_sigmoi
   HIP_TRY(prof_launch(c, s, "epnp_kernel", (double)B * (2 * (c->kp_n + 1) * 8 + 28), (double)B * 1.0e5, [&] {
     return launch_epnp(raw, B, c->kp_n, c->kp3d, c->kp_model, c->camK, c->cam_nu, c->cam_nv, apply_sigmoid, kp_out,
                        quat, pos, status, s);
+  }));
+  return SPEF_OK;
+}
+
+// Pillow precompute_coeffs + normalize_coeffs_8bpc (libImaging/Resample.c), BILINEAR filter (support 1):
+// bounds [out][2] = (xmin, count), coefficients [out][ksize] in fixed point with 22 fractional bits.
+static int pil_coeffs(int in_size, int out_size, std::vector<int>& bounds, std::vector<int>& kk) {
+  const double scale = (double)(float)in_size / out_size;
+  const double filterscale = scale < 1.0 ? 1.0 : scale;
+  const double support = 1.0 * filterscale;
+  const int ksize = (int)ceil(support) * 2 + 1;
+  bounds.assign(2 * out_size, 0);
+  kk.assign((size_t)out_size * ksize, 0);
+  std::vector<double> k(ksize);
+  for (int xx = 0; xx < out_size; ++xx) {
+    const double center = (xx + 0.5) * scale;
+    const double ss = 1.0 / filterscale;
+    int xmin = (int)(center - support + 0.5);
+    if (xmin < 0) xmin = 0;
+    int xmax = (int)(center + support + 0.5);
+    if (xmax > in_size) xmax = in_size;
+    xmax -= xmin;
+    double ww = 0.0;
+    for (int x = 0; x < xmax; ++x) {
+      double t = (x + xmin - center + 0.5) * ss;
+      if (t < 0.0) t = -t;
+      const double w = t < 1.0 ? 1.0 - t : 0.0;
+      k[x] = w;
+      ww += w;
+    }
+    for (int x = 0; x < xmax; ++x)
+      if (ww != 0.0) k[x] /= ww;
+    for (int x = 0; x < xmax; ++x)
+      kk[(size_t)xx * ksize + x] = k[x] < 0 ? (int)(-0.5 + k[x] * (1 << 22)) : (int)(0.5 + k[x] * (1 << 22));
+    bounds[2 * xx] = xmin;
+    bounds[2 * xx + 1] = xmax;
+  }
+  return ksize;
+}
+
+int spef_preprocess(spef_ctx* c, const uint8_t* frames, int B, int Hin, int Win, uint8_t* out, int H, int W,
+                    void* stream) {
+  if (!c || !frames || !out) return fail(SPEF_ERR_ARG, "null argument");
+  if (B <= 0 || Hin <= 0 || Win <= 0 || H <= 0 || W <= 0) return fail(SPEF_ERR_ARG, "bad preprocess shape");
+  Dev d(c->device);
+  hipStream_t s = (hipStream_t)stream;
+  const int key[4] = {Hin, Win, H, W};
+  if (memcmp(key, c->pre_key, sizeof(key)) != 0) {
+    std::vector<int> bh, kh, bv, kv;
+    c->pre_ksh = pil_coeffs(Win, W, bh, kh);
+    c->pre_ksv = pil_coeffs(Hin, H, bv, kv);
+    c->pre_y0 = bv[0];
+    c->pre_ht = bv[2 * H - 2] + bv[2 * H - 1] - c->pre_y0;
+    for (int i = 0; i < H; ++i) bv[2 * i] -= c->pre_y0;   // vertical bounds relative to the temp image
+    std::vector<int> th(bh), tv(bv);
+    th.insert(th.end(), kh.begin(), kh.end());
+    tv.insert(tv.end(), kv.begin(), kv.end());
+    if (c->pre_bh) hipFree(c->pre_bh);
+    if (c->pre_bv) hipFree(c->pre_bv);
+    c->pre_bh = c->pre_bv = nullptr;
+    memset(c->pre_key, 0, sizeof(c->pre_key));
+    HIP_TRY(hipMalloc(&c->pre_bh, th.size() * sizeof(int)));
+    HIP_TRY(hipMalloc(&c->pre_bv, tv.size() * sizeof(int)));
+    HIP_TRY(hipMemcpy(c->pre_bh, th.data(), th.size() * sizeof(int), hipMemcpyHostToDevice));
+    HIP_TRY(hipMemcpy(c->pre_bv, tv.data(), tv.size() * sizeof(int), hipMemcpyHostToDevice));
+    memcpy(c->pre_key, key, sizeof(key));
+  }
+  const size_t tmp = (size_t)B * c->pre_ht * W * 3;
+  if (tmp > c->pre_tmp_bytes) {
+    if (c->pre_tmp) hipFree(c->pre_tmp);
+    c->pre_tmp = nullptr;
+    c->pre_tmp_bytes = 0;
+    HIP_TRY(hipMalloc(&c->pre_tmp, tmp));
+    c->pre_tmp_bytes = tmp;
+  }
+  HIP_TRY(prof_launch(c, s, "resize_h_kernel", (double)B * c->pre_ht * Win * 3 + (double)tmp, 0.0, [&] {
+    return launch_resize_h(frames, c->pre_tmp, c->pre_bh, c->pre_bh + 2 * W, c->pre_ksh, B, Hin, Win, c->pre_y0,
+                           c->pre_ht, W, s);
+  }));
+  HIP_TRY(prof_launch(c, s, "resize_v_kernel", (double)tmp + (double)B * H * W * 3, 0.0, [&] {
+    return launch_resize_v(c->pre_tmp, out, c->pre_bv, c->pre_bv + 2 * H, c->pre_ksv, B, c->pre_ht, H, W, s);
   }));
   return SPEF_OK;
 }

@@ -109,4 +109,10 @@ hipError_t launch_q_pool(const uint8_t* x, int8_t* p, int B, int HW, int C, int 
 // int8 (is_unsigned 0) or u8 codes -> fp32 code * scale.
 hipError_t launch_q_to_f32(const void* x, float* y, int64_t n, int is_unsigned, float scale, hipStream_t s);
 
+// ---- input preprocessing (k_pre.hip): Pillow BILINEAR resize with its integer coefficient tables ----
+hipError_t launch_resize_h(const uint8_t* in, uint8_t* tmp, const int* bounds, const int* kk, int ksize, int B,
+                           int Hin, int Win, int y0, int Ht, int Wo, hipStream_t s);
+hipError_t launch_resize_v(const uint8_t* tmp, uint8_t* out, const int* bounds, const int* kk, int ksize, int B,
+                           int Ht, int Ho, int Wo, hipStream_t s);
+
 }  // namespace spef

@@ -26,6 +26,7 @@ SIGNATURES = {
     'spef_load_weights_device': (_i, [_vp, _vp, _sz]),
     'spef_model_info': (_i, [_vp, _ip, _ip, _ip, _ip, _ip]),
     'spef_reserve': (_i, [_vp, _i, _i, _i]),
+    'spef_preprocess': (_i, [_vp, _vp, _i, _i, _i, _vp, _i, _i, _vp]),
     'spef_forward': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp]),
     'spef_backbone': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     'spef_probe': (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _ip, _ip, _ip, _vp]),

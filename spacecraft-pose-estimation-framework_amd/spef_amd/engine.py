@@ -94,6 +94,18 @@ class Engine:
                                       _stream(self.device)))
         return out0, out1
 
+    def preprocess(self, frames: torch.Tensor, size, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Decoded frames uint8 [B, Hin, Win, 3] (device) -> uint8 [B, H, W, 3] = Pillow BILINEAR resize
+        (transforms.Resize(img_size), speed.py:66-69), ready for ``forward``."""
+        assert frames.device == self.device and frames.dtype == torch.uint8 and frames.is_contiguous()
+        assert frames.dim() == 4 and frames.shape[3] == 3, 'frames must be B x H x W x 3 uint8'
+        B, Hin, Win, _ = frames.shape
+        H, W = int(size[0]), int(size[1])
+        if out is None:
+            out = torch.empty((B, H, W, 3), dtype=torch.uint8, device=self.device)
+        L.check(self.lib.spef_preprocess(self.ctx, _ptr(frames), B, Hin, Win, _ptr(out), H, W, _stream(self.device)))
+        return out
+
     def backbone(self, x: torch.Tensor) -> torch.Tensor:
         layout, B, H, W = self._layout(x)
         self.reserve(B, H, W)

@@ -94,6 +94,21 @@ class SPEMi355x:
             return raw0, None, self.engine.decode_keypoints(raw0, apply_sigmoid=True)
         return raw0, raw1, self.engine.decode(self.ori_mode, self.pos_mode, raw0, raw1)
 
+    def predict_frames(self, frames: torch.Tensor, img_size, num_predict: int = 1) -> Tuple[Dict, float]:
+        """Raw decoded camera frames (uint8 [B, Hin, Win, 3], e.g. 1200 x 1920 SPEED images converted to RGB)
+        -> the pose dict: the DataLoader's ``Resize(img_size)`` + ``ToTensor`` (speed.py:66-69, utils.py:212-249)
+        run on the GPU (bit-identical to Pillow's BILINEAR resize), then ``predict``. Latency covers both."""
+        x = frames.to(self.device, non_blocking=True).contiguous()
+        torch.cuda.synchronize(self.device)
+        start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        start.record()
+        for _ in range(max(1, num_predict)):
+            small = self.engine.preprocess(x, img_size)
+            raw0, raw1, dec = self._run(small)
+        end.record()
+        end.synchronize()
+        return self._pose(dec), start.elapsed_time(end) / max(1, num_predict)
+
     def predict(self, images: torch.Tensor, num_predict: int = 1) -> Tuple[Dict, float]:
         """images: NCHW float32 in [0,1] (the reference ``images['torch']``) or NHWC uint8 frames."""
         assert self.engine is not None
@@ -106,7 +121,9 @@ class SPEMi355x:
         end.record()
         end.synchronize()
         latency_ms = start.elapsed_time(end) / max(1, num_predict)
+        return self._pose(dec), latency_ms
 
+    def _pose(self, dec) -> Dict:
         status = dec['status'].cpu().numpy()
         if np.any(status & 1):
             raise ValueError('Error during orientation decoding')                       # classification_utils.py:135
@@ -119,11 +136,11 @@ class SPEMi355x:
 
         if self.keypoint_mode:
             return {'keypoints': dec['keypoints'].cpu().numpy(), 'ori': dec['ori'].cpu().numpy(),
-                    'pos': dec['pos'].cpu().numpy()}, latency_ms
+                    'pos': dec['pos'].cpu().numpy()}
 
         pose = {'ori': dec['ori'].cpu().numpy(), 'pos': dec['pos'].cpu().numpy()}
         if self.ori_mode == L.CLASSIFICATION:
             pose['ori_soft'] = dec['ori_soft'].cpu().numpy()
         if self.pos_mode == L.CLASSIFICATION:
             pose['pos_soft'] = dec['pos_soft'].cpu().numpy()
-        return pose, latency_ms
+        return pose
