@@ -25,24 +25,10 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.join(ROOT, 'spacecraft-pose-estimation-framework_amd'))
 sys.path.insert(0, ROOT)
 
+from spef_amd.data.synthetic import synth_frames  # noqa: E402  (SPEED-style frames)
+
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = 2500.0      # dense fp16/bf16 MFMA, no sparsity
-
-
-def synth_frames(b: int, h: int, w: int, first_index: int, seed: int = 1001):
-    """SPEED-style uint8 NHWC frames (grayscale replicated to RGB, src/data/utils.py:215)."""
-    import numpy as np
-    out = np.empty((b, h, w, 3), np.uint8)
-    yy, xx = np.mgrid[0:h, 0:w].astype(np.float32)
-    for i in range(b):
-        rng = np.random.Generator(np.random.PCG64([seed, first_index + i]))
-        cy, cx = rng.uniform(0.25, 0.75) * h, rng.uniform(0.25, 0.75) * w
-        r = rng.uniform(0.05, 0.25) * min(h, w)
-        g = 200.0 * np.exp(-((yy - cy) ** 2 + (xx - cx) ** 2) / (2 * r * r))
-        g += 30.0 * np.sin(xx / rng.uniform(2, 8)) * (g > 20)
-        g += rng.normal(8.0, 2.0, (h, w)).astype(np.float32)
-        out[i] = np.clip(g, 0, 255).astype(np.uint8)[..., None]
-    return out
 
 
 def pmc_traffic(kernel_key: str, path: str):

@@ -1,0 +1,94 @@
+"""Config surface, evaluation loop and build tool (CPU); deploy tool end to end (GPU)."""
+import json
+import os
+
+import numpy as np
+import pytest
+import torch
+
+EXP_YAML = """
+DATA:
+  BATCH_SIZE: 32
+  IMG_SIZE: [240, 384]
+  PATH: ../datasets/speed
+MODEL:
+  BACKBONE: {NAME: mobilenet_v2_pytorch, RESIDUAL: true}
+  HEAD: {NAME: ursonet_pytorch, ORI: classification, POS: regression, N_ORI_BINS_PER_DIM: 12,
+         ORI_DELETE_UNUSED_BINS: false}
+  PRETRAINED_PATH: null
+TRAIN: {MILESTONES: [35, 45], N_EPOCH: 50}
+"""
+
+
+def test_config_merge_and_validation(tmp_path):
+    from spef_amd.config import load_config, save_config
+    p = tmp_path / 'config.yaml'
+    p.write_text(EXP_YAML)
+    cfg = load_config(str(p))
+    assert cfg.DATA.IMG_SIZE == (240, 384) and cfg.DATA.BATCH_SIZE == 32 and cfg.MODEL.PRETRAINED_PATH is None
+    assert cfg.TRAIN.MILESTONES == (35, 45) and cfg.MI355X.DTYPE == 'fp16'
+    save_config(cfg, str(tmp_path / 'again.yaml'))
+    assert load_config(str(tmp_path / 'again.yaml')) == cfg
+    (tmp_path / 'bad.yaml').write_text('MODEL: {HEAD: {NOPE: 1}}')
+    with pytest.raises(KeyError):
+        load_config(str(tmp_path / 'bad.yaml'))
+    (tmp_path / 'kp.yaml').write_text('MODEL: {HEAD: {ORI: keypoints}}')
+    with pytest.raises(AssertionError):
+        load_config(str(tmp_path / 'kp.yaml'))
+    (tmp_path / 'ty.yaml').write_text('DATA: {BATCH_SIZE: eight}')
+    with pytest.raises(ValueError):
+        load_config(str(tmp_path / 'ty.yaml'))
+
+
+def test_evaluation_loop_matches_get_score():
+    from spef_amd.data.synthetic import speed_like_loader
+    from spef_amd.spe.spe_utils import SPEUtils
+    from spef_amd.tools.evaluation import evaluation
+    su = SPEUtils(None, 'regression', pos_mode='regression')
+
+    class Fake:   # returns the targets perturbed by a fixed rotation / translation
+        def __init__(self):
+            self.batches = list(speed_like_loader(2, 4, (8, 8)))
+            self.i = 0
+
+        def predict(self, images):
+            t = self.batches[self.i][1]
+            self.i += 1
+            q = t['ori'].numpy().copy()
+            q[:, 1] += 0.01
+            q /= np.linalg.norm(q, axis=1, keepdims=True)
+            return {'ori': q, 'pos': t['pos'].numpy() + 0.1}, 1.0
+    fake = Fake()
+    score, error = evaluation(fake, {'valid': fake.batches}, su, ('valid',))
+    allt = {k: np.concatenate([b[1][k].numpy() for b in fake.batches]) for k in ('ori', 'pos')}
+    fake.i = 0
+    preds = [fake.predict(None)[0] for _ in range(2)]
+    allp = {k: np.concatenate([p[k] for p in preds]) for k in ('ori', 'pos')}
+    want = su.get_score(allt, allp)
+    assert np.isclose(score['valid']['esa'][0], want['esa_score'], rtol=1e-6)
+    assert np.isclose(error['valid']['pos'][0], np.sqrt(3) * 0.1, rtol=1e-5)
+    assert set(error['valid']) == {'ori', 'pos', 'ori_std', 'pos_std', 'ori_mad', 'pos_mad'}
+
+
+@pytest.mark.parametrize('dtype', ['fp16', 'int8'])
+def test_build_tool_synthetic(tmp_path, dtype):
+    from spef_amd import blob as Bl
+    from spef_amd.tools.build_mi355x import main
+    out = str(tmp_path / 'b')
+    assert main(['--synthetic', '--dtype', dtype, '--out', out]) == 0
+    info = json.load(open(os.path.join(out, 'build.json')))
+    d = Bl.describe(open(os.path.join(out, 'model.spef'), 'rb').read())
+    assert d['dtype'] == {'fp16': 1, 'int8': 3}[dtype] and info['n_ori'] == 1728
+    assert os.path.exists(os.path.join(out, 'config.yaml'))
+
+
+@pytest.mark.gpu
+def test_deploy_tool_synthetic(tmp_path):
+    from spef_amd.tools.build_mi355x import main as build
+    from spef_amd.tools.deploy_mi355x import main as deploy
+    out = str(tmp_path / 'b')
+    assert build(['--synthetic', '--out', out]) == 0
+    assert deploy(['--build', out, '--synthetic', '1', '--num-predict', '3']) == 0
+    lat = json.load(open(os.path.join(out, 'on_board', 'latency_ms.json')))
+    sc = json.load(open(os.path.join(out, 'on_board', 'score.json')))
+    assert lat['mi355x'][0] > 0 and 'synthetic' in sc['score']
