@@ -154,7 +154,7 @@ __global__ __launch_bounds__(256) void pw_kernel(const typename DT::T* __restric
 
 // ------------------------------------------------------------------------------------------ depthwise
 template <typename DT, int S>
-__global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restrict__ X, const float* __restrict__ W9,
+__global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restrict__ X, const typename DT::DW* __restrict__ W9,
                                                  const float* __restrict__ bias, typename DT::T* __restrict__ Y,
                                                  int B, int H, int W, int C, int OH, int OW) {
   using T = typename DT::T;
@@ -185,17 +185,10 @@ __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restric
       const int ix = ox * S - 1 + kx;
       if (ix < 0 || ix >= W) continue;
       const typename DT::x8 v = load8<DT>(X + (((int64_t)b * H + iy) * W + ix) * C + c);
-      const float* wr = W9 + (ky * 3 + kx) * C + c;
-      const float4 w0 = *reinterpret_cast<const float4*>(wr);
-      const float4 w1 = *reinterpret_cast<const float4*>(wr + 4);
-      acc[0] = fmaf((float)v[0], w0.x, acc[0]);
-      acc[1] = fmaf((float)v[1], w0.y, acc[1]);
-      acc[2] = fmaf((float)v[2], w0.z, acc[2]);
-      acc[3] = fmaf((float)v[3], w0.w, acc[3]);
-      acc[4] = fmaf((float)v[4], w1.x, acc[4]);
-      acc[5] = fmaf((float)v[5], w1.y, acc[5]);
-      acc[6] = fmaf((float)v[6], w1.z, acc[6]);
-      acc[7] = fmaf((float)v[7], w1.w, acc[7]);
+      float wv[8];
+      load_dw8<DT>(W9 + (ky * 3 + kx) * C + c, wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[e] = fmaf((float)v[e], wv[e], acc[e]);
     }
   }
   typename DT::x8 o;
@@ -341,20 +334,20 @@ hipError_t launch_pw(int dtype, int epi, const void* x, const void* wt, const fl
                          : pw_dispatch<BF16>(epi, x, wt, bias, r, y, M, K, N, s);
 }
 
-hipError_t launch_dw(int dtype, const void* x, const float* w9, const float* bias, void* y, int B, int H, int W, int C,
+hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias, void* y, int B, int H, int W, int C,
                      int stride, int OH, int OW, hipStream_t s) {
   if (C & 7) return hipErrorInvalidValue;
   const unsigned g = blocks_for((int64_t)B * OH * OW * (C / 8), 256);
   if (dtype == DT_F16) {
     if (stride == 1)
-      dw_kernel<F16, 1><<<g, 256, 0, s>>>((const _Float16*)x, w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
+      dw_kernel<F16, 1><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
     else
-      dw_kernel<F16, 2><<<g, 256, 0, s>>>((const _Float16*)x, w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
+      dw_kernel<F16, 2><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
   } else {
     if (stride == 1)
-      dw_kernel<BF16, 1><<<g, 256, 0, s>>>((const __bf16*)x, w9, bias, (__bf16*)y, B, H, W, C, OH, OW);
+      dw_kernel<BF16, 1><<<g, 256, 0, s>>>((const __bf16*)x, (const float*)w9, bias, (__bf16*)y, B, H, W, C, OH, OW);
     else
-      dw_kernel<BF16, 2><<<g, 256, 0, s>>>((const __bf16*)x, w9, bias, (__bf16*)y, B, H, W, C, OH, OW);
+      dw_kernel<BF16, 2><<<g, 256, 0, s>>>((const __bf16*)x, (const float*)w9, bias, (__bf16*)y, B, H, W, C, OH, OW);
   }
   return hipGetLastError();
 }

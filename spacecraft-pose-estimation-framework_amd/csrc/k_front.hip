@@ -16,7 +16,7 @@ namespace spef {
 template <typename DT, int TH, int TW, int NW>
 __global__ __launch_bounds__(NW * 64) void front_kernel(
     const uint8_t* __restrict__ X, const typename DT::T* __restrict__ wsp, const float* __restrict__ bs,
-    const float* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
+    const typename DT::DW* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int SH_img, int SW_img,
     int tiles_x, int tiles_y, uint32_t nwg) {
   using T = typename DT::T;
@@ -31,7 +31,9 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   static_assert(POUT16 % NW == 0, "tile split");
   __shared__ __attribute__((aligned(16))) uint8_t In[IH * IRS];
   __shared__ __attribute__((aligned(16))) T Xs[PSP * XS];
-  __shared__ __attribute__((aligned(16))) float Sl[9 * 32 + 32];
+  using DW = typename DT::DW;
+  __shared__ __attribute__((aligned(16))) DW Sl[9 * 32];     // block-1 depthwise weights
+  __shared__ __attribute__((aligned(16))) float Sb[32];      // block-1 depthwise bias
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
@@ -104,7 +106,10 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
         }
       }
     }
-    for (int u = tid; u < 9 * 32 + 32; u += NW * 64) Sl[u] = u < 9 * 32 ? Wd[(u >> 5) * 32 + (u & 31)] : bd[u - 9 * 32];
+    for (int u = tid; u < 9 * 32 + 32; u += NW * 64) {
+      if (u < 9 * 32) Sl[u] = Wd[u];
+      else Sb[u - 9 * 32] = bd[u - 9 * 32];
+    }
   }
   // stem weight fragments: /255-folded weights split hi + lo, [2][32 ch][32 k] from the blob; tiles t = 0, 1
   x8 ahi[2], alo[2];
@@ -162,15 +167,16 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
     const int oy = o / TW, ox = o - (o / TW) * TW;
     float a8[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) a8[e] = Sl[9 * 32 + 8 * kg + e];
+    for (int e = 0; e < 8; ++e) a8[e] = Sb[8 * kg + e];
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
         const x8 v = *reinterpret_cast<const x8*>(Xs + ((oy + ky) * SW + (ox + kx)) * XS + 8 * kg);
-        const float* w = Sl + (ky * 3 + kx) * 32 + 8 * kg;
+        DW8<DT> wt;
+        wt.load(Sl + (ky * 3 + kx) * 32 + 8 * kg);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], w[e], a8[e]);
+        for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wt[e], a8[e]);
       }
     x8 bf;
 #pragma unroll
@@ -189,7 +195,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   }
 }
 
-hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* bs, const float* wd, const float* bd,
+hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* bs, const void* wd, const float* bd,
                         const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                         hipStream_t s) {
   constexpr int TH = 16, TW = 16, NW = 8;
@@ -198,10 +204,10 @@ hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* 
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   if (dtype == DT_F16)
-    front_kernel<F16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, (const _Float16*)wsp, bs, wd, bd, (const _Float16*)wp, bp,
+    front_kernel<F16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, (const _Float16*)wsp, bs, (const _Float16*)wd, bd, (const _Float16*)wp, bp,
                                                           (_Float16*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   else
-    front_kernel<BF16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, (const __bf16*)wsp, bs, wd, bd, (const __bf16*)wp, bp,
+    front_kernel<BF16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, (const __bf16*)wsp, bs, (const float*)wd, bd, (const __bf16*)wp, bp,
                                                            (__bf16*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   return hipGetLastError();
 }

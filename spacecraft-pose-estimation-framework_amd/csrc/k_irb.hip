@@ -23,7 +23,7 @@
 namespace spef {
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
-          bool STW>
+          bool STW, int DWB = 4>
 struct IrbGeom {
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW;
@@ -36,7 +36,8 @@ struct IrbGeom {
   // but less LDS. The wide padding is used only when it costs no workgroups per CU.
   static constexpr int NBUF = EXPAND ? (DBUF ? 2 : 1) : 0;
   static constexpr int NCH_ = (HID + 31) / 32;
-  static constexpr int SLAB = 9 * 32;             // floats: depthwise weights [9][32] of one hidden chunk
+  static constexpr int SLAB = 9 * 32;             // depthwise weights [9][32] of one hidden chunk (DWB bytes each)
+  static constexpr int SLAB_PIECES = SLAB * DWB / 16;   // 16-B pieces of one slab
   static constexpr int BIAS = 2 * NCH_ * 32;      // floats: dw bias + expand bias of every hidden channel
   // STW: per-chunk expand / project weights staged once per workgroup in LDS (3 + 2 buffers) instead of every
   // wave fetching its own fragments from L2 (8x less L2 traffic for an 8-wave workgroup)
@@ -51,7 +52,7 @@ struct IrbGeom {
   static constexpr int WP_PIECES = STW ? NCTP * 4 : 0;
   static constexpr int W_PPT = (WE_PIECES + WP_PIECES + NW * 64 - 1) / (NW * 64);   // 16-B pieces per thread
   static constexpr int bytes_for(int xs, int es) {
-    return (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 + (2 * SLAB + BIAS) * 4;
+    return (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 + 2 * SLAB * DWB + BIAS * 4;
   }
   static constexpr bool WIDE = (163840 / bytes_for(CINP + 16, 48)) >= (163840 / bytes_for(CINP + 8, 40));
   static constexpr int XS = WIDE ? CINP + 16 : CINP + 8;   // Xs row stride (elements)
@@ -71,7 +72,7 @@ struct IrbGeom {
   static_assert(CIN % 8 == 0 && HID % 8 == 0 && COUT % 4 == 0, "channel counts must be multiples of 8");
   static_assert(EXPAND || HID == 32, "t == 1 blocks are supported for 32 channels (MobileNet-V2 block 1)");
   static_assert(!RES || (S == 1 && CIN == COUT), "residual needs stride 1 and cin == cout");
-  static_assert(NW * 64 >= SLAB / 4, "slab fill needs one float4 per thread");
+  static_assert(NW * 64 >= SLAB_PIECES, "slab fill needs one 16-B piece per thread");
   static_assert(SLAB % 4 == 0 && (NCH_ * 32) % 4 == 0, "float4 slabs");
   static_assert(EPT <= 32, "validity mask is 32 bits");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -81,10 +82,11 @@ template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool E
           bool DBUF, bool STW>
 __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const typename DT::T* __restrict__ X, const typename DT::T* __restrict__ We, const float* __restrict__ be,
-    const float* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
+    const typename DT::DW* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
     int tiles_y, uint32_t nwg) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW>;
+  using DW = typename DT::DW;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW)>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
   using x4 = typename DT::x4;
@@ -94,8 +96,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   T* Es1 = Es0 + (G::NBUF == 2 ? G::PINP * G::ES : 0);
   T* WEs = Es0 + G::NBUF * G::PINP * G::ES;                                // [3][32][WES] expand weights
   T* WPs = WEs + G::WE_ELEMS;                                               // [2][NCTP][WPS] project weights
-  float* Sl = reinterpret_cast<float*>(WPs + G::WP_ELEMS);                  // [2][SLAB] dw weights
-  float* Bd = Sl + 2 * G::SLAB;                                             // [HIDP] dw bias
+  DW* Sl = reinterpret_cast<DW*>(WPs + G::WP_ELEMS);                        // [2][SLAB] dw weights
+  float* Bd = reinterpret_cast<float*>(Sl + 2 * G::SLAB);                   // [HIDP] dw bias
   float* Be = Bd + G::NCH * 32;                                             // [HIDP] expand bias
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -108,17 +110,18 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
 
-  // depthwise-weight slab of chunk cc: thread t < SLAB/4 moves one float4 of [9][32]
-  auto slab_load = [&](int cc) -> float4 {
-    float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (tid < G::SLAB / 4 && cc < G::NCH) {
-      const int f = tid * 4, tap = f >> 5, ch = 32 * cc + (f & 31);
-      if (ch < HID) v = *reinterpret_cast<const float4*>(Wd + tap * HID + ch);
+  // depthwise-weight slab of chunk cc: thread t < SLAB_PIECES moves one 16-B piece of [9][32]
+  constexpr int EPP = 16 / (int)sizeof(DW);      // weights per piece
+  auto slab_load = [&](int cc) -> uint4 {
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (tid < G::SLAB_PIECES && cc < G::NCH) {
+      const int f = tid * EPP, tap = f >> 5, ch = 32 * cc + (f & 31);
+      if (ch < HID) v = *reinterpret_cast<const uint4*>(Wd + tap * HID + ch);
     }
     return v;
   };
-  auto slab_store = [&](int cc, float4 v) {
-    if (tid < G::SLAB / 4) *reinterpret_cast<float4*>(Sl + (cc & 1) * G::SLAB + tid * 4) = v;
+  auto slab_store = [&](int cc, uint4 v) {
+    if (tid < G::SLAB_PIECES) *reinterpret_cast<uint4*>(Sl + (cc & 1) * G::SLAB + tid * EPP) = v;
   };
 
   // weight staging: pieces [0, WE_PIECES) = expand rows of chunk ce, then project rows of chunk cp
@@ -228,8 +231,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
-    const float4 slab_next = slab_load(c + 1);     // issued now, stored after this chunk's depthwise
-    const float* sl = Sl + (c & 1) * G::SLAB;
+    const uint4 slab_next = slab_load(c + 1);      // issued now, stored after this chunk's depthwise
+    const DW* sl = Sl + (c & 1) * G::SLAB;
     // project weight fragments of this chunk (no STW): issued before the expand so their latency hides under it
     x8 pa[G::NCTW];
     if constexpr (!STW) {
@@ -339,16 +342,10 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
           for (int kx = 0; kx < 3; ++kx) {
             const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
             const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + 8 * kg);
-            const float4 w0 = *reinterpret_cast<const float4*>(sl + (ky * 3 + kx) * 32 + 8 * kg);
-            const float4 w1 = *reinterpret_cast<const float4*>(sl + (ky * 3 + kx) * 32 + 8 * kg + 4);
-            a8[0] = fmaf((float)v[0], w0.x, a8[0]);
-            a8[1] = fmaf((float)v[1], w0.y, a8[1]);
-            a8[2] = fmaf((float)v[2], w0.z, a8[2]);
-            a8[3] = fmaf((float)v[3], w0.w, a8[3]);
-            a8[4] = fmaf((float)v[4], w1.x, a8[4]);
-            a8[5] = fmaf((float)v[5], w1.y, a8[5]);
-            a8[6] = fmaf((float)v[6], w1.z, a8[6]);
-            a8[7] = fmaf((float)v[7], w1.w, a8[7]);
+            DW8<DT> wt;   // fp16 weights: one ds_read_b128 per tap, consumed by v_fma_mix directly
+            wt.load(sl + (ky * 3 + kx) * 32 + 8 * kg);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wt[e], a8[e]);
           }
 #pragma unroll
         for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
@@ -394,44 +391,42 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 // SPEF_OPT_IRB_VARIANT); a geometry without the requested variant uses variant 0.
 #define SPEF_IRB_TABLE(X)                                                   \
   X(0, 32, 32, 16, 1, 16, 16, false, false, 8, 1, true, false)    /* block 1      */ \
-  X(1, 32, 32, 16, 1, 8, 16, false, false, 8, 1, true, false)                        \
   X(0, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false)     /* block 2      */ \
-  X(1, 16, 96, 24, 2, 8, 8, true, false, 4, 1, false, false)                         \
+  X(2, 16, 96, 24, 2, 4, 16, true, false, 4, 1, false, false)                        \
+  X(3, 16, 96, 24, 2, 8, 8, true, false, 4, 1, true, false)                          \
   X(0, 24, 144, 24, 1, 8, 16, true, true, 8, 1, false, false)     /* block 3      */ \
-  X(1, 24, 144, 24, 1, 8, 16, true, true, 8, 1, true, false)                         \
+  X(1, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false)                        \
   X(0, 24, 144, 32, 2, 8, 8, true, false, 4, 1, false, false)     /* block 4      */ \
-  X(1, 24, 144, 32, 2, 8, 16, true, false, 8, 1, false, false)                       \
-  X(0, 32, 192, 32, 1, 8, 16, true, true, 8, 1, false, false)     /* blocks 5-6   */ \
-  X(1, 32, 192, 32, 1, 8, 16, true, true, 8, 1, true, false)                         \
+  X(2, 24, 144, 32, 2, 8, 16, true, false, 8, 1, false, false)                       \
+  X(0, 32, 192, 32, 1, 16, 16, true, true, 8, 1, false, false)    /* blocks 5-6   */ \
+  X(1, 32, 192, 32, 1, 8, 16, true, true, 8, 1, false, false)                        \
+  X(2, 32, 192, 32, 1, 16, 16, true, true, 8, 1, true, false)                        \
+  X(3, 32, 192, 32, 1, 16, 16, true, true, 8, 1, false, true)                        \
   X(0, 32, 192, 64, 2, 8, 8, true, false, 8, 2, false, false)     /* block 7      */ \
-  X(1, 32, 192, 64, 2, 8, 8, true, false, 4, 1, false, false)                        \
-  X(0, 64, 384, 64, 1, 8, 16, true, true, 8, 1, false, true)     /* blocks 8-10  */ \
-  X(1, 64, 384, 64, 1, 8, 16, true, true, 8, 1, true, true)                          \
-  X(0, 64, 384, 96, 1, 8, 16, true, false, 8, 1, true, true)     /* block 11     */ \
-  X(1, 64, 384, 96, 1, 8, 16, true, false, 8, 1, false, true)                       \
-  X(0, 96, 576, 96, 1, 8, 16, true, true, 8, 1, true, true)      /* blocks 12-13 */ \
-  X(1, 96, 576, 96, 1, 8, 16, true, true, 8, 1, false, true)                        \
-  X(0, 96, 576, 160, 2, 4, 8, true, false, 4, 2, true, false)    /* block 14     */ \
-  X(1, 96, 576, 160, 2, 4, 8, true, false, 4, 2, true, true)                        \
-  X(0, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true)     /* blocks 15-16 */ \
-  X(1, 160, 960, 160, 1, 8, 8, true, true, 8, 2, false, true)                       \
-  X(0, 160, 960, 320, 1, 8, 8, true, false, 8, 2, false, true)   /* block 17     */ \
-  X(1, 160, 960, 320, 1, 8, 8, true, false, 8, 2, false, false)                      \
-  X(2, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, true)                         \
-  X(2, 24, 144, 24, 1, 8, 16, true, true, 8, 1, false, true)                         \
-  X(2, 24, 144, 32, 2, 8, 8, true, false, 4, 1, false, true)                         \
-  X(2, 32, 192, 32, 1, 8, 16, true, true, 8, 1, false, true)                         \
-  X(2, 32, 192, 64, 2, 8, 8, true, false, 8, 2, false, true)                         \
-  X(2, 64, 384, 64, 1, 8, 16, true, true, 8, 1, true, false)                         \
-  X(2, 96, 576, 96, 1, 8, 16, true, true, 8, 1, true, false)                         \
-  X(2, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, false)
+  X(2, 32, 192, 64, 2, 8, 16, true, false, 8, 1, false, false)                       \
+  X(0, 64, 384, 64, 1, 16, 16, true, true, 8, 1, true, true)      /* blocks 8-10  */ \
+  X(1, 64, 384, 64, 1, 8, 16, true, true, 8, 1, false, true)                         \
+  X(2, 64, 384, 64, 1, 16, 16, true, true, 8, 1, false, true)                        \
+  X(3, 64, 384, 64, 1, 8, 16, true, true, 4, 1, false, true)                         \
+  X(0, 64, 384, 96, 1, 16, 16, true, false, 8, 1, false, true)     /* block 11     */ \
+  X(2, 64, 384, 96, 1, 8, 16, true, false, 8, 1, true, true)                       \
+  X(0, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true)     /* blocks 12-13 */ \
+  X(1, 96, 576, 96, 1, 8, 16, true, true, 8, 1, true, true)                          \
+  X(2, 96, 576, 96, 1, 16, 16, true, true, 8, 2, false, true)                        \
+  X(0, 96, 576, 160, 2, 8, 8, true, false, 8, 2, false, true)     /* block 14     */ \
+  X(2, 96, 576, 160, 2, 4, 8, true, false, 4, 2, true, false)                        \
+  X(0, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true)      /* blocks 15-16 */ \
+  X(2, 160, 960, 160, 1, 4, 8, true, true, 4, 2, true, true)                       \
+  X(0, 160, 960, 320, 1, 8, 8, true, false, 8, 2, false, true)    /* block 17     */ \
+  X(2, 160, 960, 320, 1, 4, 8, true, false, 4, 2, true, true)                     
 
 template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
           bool DBUF, bool STW>
-static hipError_t irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
+static hipError_t irb_go(const void* x, const void* we, const float* be, const void* wd, const float* bd,
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                          hipStream_t s) {
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW>;
+  using DW = typename DT::DW;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW)>;
   using T = typename DT::T;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
@@ -445,7 +440,7 @@ static hipError_t irb_go(const void* x, const void* we, const float* be, const f
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  k<<<nwg, NW * 64, lds, s>>>((const T*)x, (const T*)we, be, wd, bd, (const T*)wp, bp, (T*)y, H, W, OH, OW, tiles_x,
+  k<<<nwg, NW * 64, lds, s>>>((const T*)x, (const T*)we, be, (const DW*)wd, bd, (const T*)wp, bp, (T*)y, H, W, OH, OW, tiles_x,
                               tiles_y, nwg);
   return hipGetLastError();
 }
@@ -460,7 +455,7 @@ static bool irb_has(int variant, int cin, int hid, int cout, int stride, bool ex
 
 template <typename DT>
 static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stride, bool expand, bool res,
-                               const void* x, const void* we, const float* be, const float* wd, const float* bd,
+                               const void* x, const void* we, const float* be, const void* wd, const float* bd,
                                const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                                hipStream_t s) {
   if (!irb_has(variant, cin, hid, cout, stride, expand, res)) variant = 0;
@@ -478,7 +473,7 @@ bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res
 }
 
 hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int stride, bool expand, bool res,
-                      const void* x, const void* we, const float* be, const float* wd, const float* bd, const void* wp,
+                      const void* x, const void* we, const float* be, const void* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
   return dtype == DT_F16 ? irb_dispatch<F16>(variant, cin, hid, cout, stride, expand, res, x, we, be, wd, bd, wp, bp,
                                              y, B, H, W, OH, OW, s)

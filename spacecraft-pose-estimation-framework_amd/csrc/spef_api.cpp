@@ -238,7 +238,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const double px = (double)B * OH * OW;
         HIP_TRY(prof_launch(c, s, "front_kernel<stem+block1>", (double)B * h * w * 3 + px * 16 * 2,
                             px * (2 * 27 * 32 + 18 * 32 + 2 * 32 * 16), [&] {
-          return launch_front(dt, input, ptr<void>(c, op.x0), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
+          return launch_front(dt, input, ptr<void>(c, op.x0), ptr<float>(c, op.b0), ptr<void>(c, nx->w1),
                               ptr<float>(c, nx->b1), ptr<void>(c, nx->w2), ptr<float>(c, nx->b2), y, B, h, w, OH, OW, s);
         }));
         cur = y;
@@ -278,7 +278,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         snprintf(key, sizeof(key), "irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
           return launch_irb(c->irb_variant, dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
-                            ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
+                            ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<void>(c, op.w1), ptr<float>(c, op.b1),
                             ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
         }));
         cur = y;
@@ -299,7 +299,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const double opx = (double)B * OH * OW;
         HIP_TRY(prof_launch(c, s, op.stride == 1 ? "dw_kernel<1>" : "dw_kernel<2>",
                             ((double)B * h * w + opx) * op.hidden * 2 + 40.0 * op.hidden, opx * op.hidden * 18.0, [&] {
-          return launch_dw(dt, h1, ptr<float>(c, op.w1), ptr<float>(c, op.b1), h2, B, h, w, (int)op.hidden,
+          return launch_dw(dt, h1, ptr<void>(c, op.w1), ptr<float>(c, op.b1), h2, B, h, w, (int)op.hidden,
                            (int)op.stride, OH, OW, s);
         }));
         void* y = res ? pick({x, h2}) : pick({h2});

@@ -20,6 +20,7 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 // mfma16: K = 16 form, lane holds A[i = l&15][k = 4(l>>4)+e], B[k = 4(l>>4)+e][j = l&15] (4 elements).
 struct F16 {
   using T = _Float16;
+  using DW = _Float16;   // depthwise weights: fp16 (one v_fma_mix per tap with fp16 x and w, fp32 accumulate)
   using x8 = f16x8;
   using x4 = f16x4;
   static __device__ __forceinline__ f32x4 mfma(x8 a, x8 b, f32x4 c) {
@@ -31,6 +32,7 @@ struct F16 {
 };
 struct BF16 {
   using T = __bf16;
+  using DW = float;      // depthwise weights stay fp32 (v_fma_mix has no bf16 form)
   using x8 = bf16x8;
   using x4 = bf16x4;
   static __device__ __forceinline__ f32x4 mfma(x8 a, x8 b, f32x4 c) {
@@ -46,6 +48,38 @@ template <typename DT>
 __device__ __forceinline__ typename DT::x8 load8(const typename DT::T* p) {
   return *reinterpret_cast<const typename DT::x8*>(p);
 }
+// 8 consecutive depthwise weights kept in their storage type (fp16: 4 VGPRs, read by v_fma_mix directly)
+template <typename DT, bool H = (sizeof(typename DT::DW) == 2)>
+struct DW8 {
+  f16x8 v;
+  __device__ __forceinline__ void load(const typename DT::DW* p) { v = *reinterpret_cast<const f16x8*>(p); }
+  __device__ __forceinline__ float operator[](int e) const { return (float)v[e]; }
+};
+template <typename DT>
+struct DW8<DT, false> {
+  float v[8];
+  __device__ __forceinline__ void load(const typename DT::DW* p) {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+    v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+  }
+  __device__ __forceinline__ float operator[](int e) const { return v[e]; }
+};
+
+// 8 consecutive depthwise weights -> fp32 (exact conversion from fp16)
+template <typename DT>
+__device__ __forceinline__ void load_dw8(const typename DT::DW* p, float w[8]) {
+  if constexpr (sizeof(typename DT::DW) == 2) {
+    const f16x8 v = *reinterpret_cast<const f16x8*>(p);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) w[e] = (float)v[e];
+  } else {
+    const float4 a = *reinterpret_cast<const float4*>(p), b = *reinterpret_cast<const float4*>(p + 4);
+    w[0] = a.x; w[1] = a.y; w[2] = a.z; w[3] = a.w;
+    w[4] = b.x; w[5] = b.y; w[6] = b.z; w[7] = b.w;
+  }
+}
+
 template <typename DT>
 __device__ __forceinline__ typename DT::x8 zero8() {
   typename DT::x8 z;

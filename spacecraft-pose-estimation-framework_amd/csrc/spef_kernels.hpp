@@ -24,8 +24,9 @@ hipError_t launch_gemm_pw(int dtype, int epi, const void* x, const void* wt, con
                           void* y, int64_t M, int K, int N, hipStream_t s);
 const char* gemm_key(int dtype, int epi, int N);
 
-// Depthwise 3x3 conv, pad 1, stride 1|2, BN folded, ReLU. W9: fp32 [9][C], bias fp32 [C].
-hipError_t launch_dw(int dtype, const void* x, const float* w9, const float* bias, void* y, int B, int H, int W,
+// Depthwise 3x3 conv, pad 1, stride 1|2, BN folded, ReLU. W9: [9][C] (fp16 for fp16 blobs, fp32 for bf16),
+// bias fp32 [C].
+hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias, void* y, int B, int H, int W,
                      int C, int stride, int OH, int OW, hipStream_t s);
 
 // Last 1x1 conv (+BN, ReLU) fused with the global mean over HW: pooled fp32 [B][N].
@@ -44,12 +45,12 @@ hipError_t launch_fc(const float* x, const float* w, const float* bias, float* o
 // Fused InvertedResidual block (expand -> depthwise -> project [+x]) for the geometries in k_irb.hip's table.
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
 hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
-                      const void* we, const float* be, const float* wd, const float* bd, const void* wp,
+                      const void* we, const float* be, const void* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 
 // Stem (u8 NHWC input) fused with inverted-residual block 1 (32 -> dw -> 16), k_front.hip. wsp: /255-folded stem
 // weights split hi + lo in the activation dtype, [2][32][32] (blob OP_STEM x0).
-hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* bs, const float* wd, const float* bd,
+hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* bs, const void* wd, const float* bd,
                         const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 
 // Split-K fp32 head GEMM for very long K: part = workspace [splits][B][round_up(n,16)] floats.

@@ -9,7 +9,7 @@ Folding (eval-mode ``BatchNorm2d``, eps 1e-5, ``pytorch_layers.py:53-56``), done
     w' = w * s[:, None, None, None]         b' = beta - running_mean * s
 Pointwise weights are stored [Np][Kp] in the activation dtype (fp16 default, bf16 variant), zero padded
 (Kp = K up to a multiple of 32, Np = N up to a multiple of 16) so the MFMA kernels never mask weight loads.
-Stem, depthwise, bias and head weights stay fp32.
+Depthwise weights are fp16 in fp16 blobs (fp32 in bf16 blobs); stem, bias and head weights stay fp32.
 """
 from __future__ import annotations
 
@@ -91,10 +91,13 @@ def _pw_tensor(w: np.ndarray, b: np.ndarray, dtype: str, data: _Data):
     return data.add(_to_act(wp, dtype)), data.add(bp.tobytes())
 
 
-def _dw_tensor(w: np.ndarray, b: np.ndarray, data: _Data):
+def _dw_tensor(w: np.ndarray, b: np.ndarray, data: _Data, dtype: str):
+    """Depthwise weights [9][C] (tap = ky*3+kx): fp16 in fp16 blobs (the kernels' v_fma_mix operand), fp32 in
+    bf16 blobs; bias fp32."""
     c = w.shape[0]
-    w9 = np.ascontiguousarray(w[:, 0].reshape(c, 9).T, dtype=np.float32)   # [9][C], tap = ky*3+kx
-    return data.add(w9.tobytes()), data.add(np.asarray(b, np.float32).tobytes())
+    w9 = np.ascontiguousarray(w[:, 0].reshape(c, 9).T, dtype=np.float32)
+    w9b = w9.astype(np.float16).tobytes() if dtype == 'fp16' else w9.tobytes()
+    return data.add(w9b), data.add(np.asarray(b, np.float32).tobytes())
 
 
 def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=(8, 12)) -> bytes:
@@ -124,7 +127,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
         e = (ABSENT, ABSENT)
         if blk.expand != 1:
             e = _pw_tensor(*fold_bn(sd, convs.pop(0)), dtype, data)
-        d = _dw_tensor(*fold_bn(sd, convs[0]), data)
+        d = _dw_tensor(*fold_bn(sd, convs[0]), data, dtype)
         p = _pw_tensor(*fold_bn(sd, convs[1]), dtype, data)
         ops.append((OP_IRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, 1 if blk.residual else 0,
                     e[0], e[1], d[0], d[1], p[0], p[1]))

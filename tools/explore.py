@@ -47,8 +47,8 @@ def main():
     fr = torch.from_numpy(rng.integers(0, 256, (B, S, S, 3), dtype=np.uint8)).cuda()
     ori = torch.empty((B, 1728), device='cuda')
     pos = torch.empty((B, 3), device='cuda')
-    if os.environ.get('SWEEP'):
-        for v in (0, 1, 2):
+    if os.environ.get("SWEEP"):
+        for v in [int(x) for x in os.environ.get("SWEEP", "0,1,2").split(",")]:
             run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 1, L.OPT_IRB_VARIANT: v}, label=f'fused variant {v}')
         return
     ref = run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 0, L.OPT_PW_GEMM: 0}, label='unfused, direct pw')
