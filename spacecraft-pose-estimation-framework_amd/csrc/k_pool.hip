@@ -25,7 +25,11 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
   __shared__ __attribute__((aligned(16))) T Bs[2][BM * RS];
   __shared__ float red[4][BN];
 
-  const int b = blockIdx.y, n0 = blockIdx.x * BN;
+  // XCD-aware order: the channel blocks of one image run on one XCD, so its 320-channel map is fetched from
+  // HBM once into that XCD's L2 instead of once per XCD (blocks are dealt round-robin over the 8 XCDs).
+  const uint32_t nblk = gridDim.x * gridDim.y;
+  const uint32_t L = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nblk);
+  const int b = (int)(L / gridDim.x), n0 = (int)(L % gridDim.x) * BN;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
   const int wn = wave & 1, wm = wave >> 1;
