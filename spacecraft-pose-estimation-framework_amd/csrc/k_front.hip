@@ -120,41 +120,47 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   }
   const float4 sb0 = *reinterpret_cast<const float4*>(bs + 4 * kg);
   const float4 sb1 = *reinterpret_cast<const float4*>(bs + 16 + 4 * kg);
-  // per-lane tap offsets inside the input tile for k = 8kg + e: (k / 9) * IRS + k % 9
+  // per-lane tap offsets inside the input tile for k = 8kg + e: (k / 9) * IRS + k % 9. The K padding slots
+  // k = 27..31 have zero weights, so they may read any finite byte (offset 0): no per-tap select.
   int koff[8];
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int k = 8 * kg + e;
-    koff[e] = k < 27 ? (k / 9) * IRS + (k % 9) : -1;
+    koff[e] = k < 27 ? (k / 9) * IRS + (k % 9) : 0;
   }
+  // interior tiles: every stem position of the tile lies inside the stem map (no zero padding to apply)
+  const bool interior = sy0 >= 0 && sx0 >= 0 && sy0 + SH <= SH_img && sx0 + SW <= SW_img;
   __syncthreads();
 
   // ---- 2. stem tile on MFMA -> Xs (fp16/bf16, ReLU; zero outside the stem map = block-1 depthwise padding)
   for (int pt = wave; pt < PS16; pt += NW) {
     const int p = pt * 16 + r16;
-    const int spy = p / SW, spx = p - (p / SW) * SW;
+    const int pc = p < PS ? p : PS - 1;             // padding lanes of the last tile: any in-tile address
+    const int spy = pc / SW, spx = pc - spy * SW;
     const int base = (2 * spy) * IRS + 2 * spx * 3 + mis;
     x8 bx;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) bx[e] = (koff[e] >= 0 && p < PS) ? (T)(float)In[base + koff[e]] : (T)0.0f;
-    f32x4 e0 = {0.f, 0.f, 0.f, 0.f}, e1 = {0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < 8; ++e) bx[e] = (T)(float)In[base + koff[e]];
+    f32x4 e0 = {sb0.x, sb0.y, sb0.z, sb0.w}, e1 = {sb1.x, sb1.y, sb1.z, sb1.w};   // bias as MFMA C
     e0 = DT::mfma(ahi[0], bx, e0);
     e0 = DT::mfma(alo[0], bx, e0);
     e1 = DT::mfma(ahi[1], bx, e1);
     e1 = DT::mfma(alo[1], bx, e1);
-    const int gy = sy0 + spy, gx = sx0 + spx;
-    const bool pv = p < PS && gy >= 0 && gy < SH_img && gx >= 0 && gx < SW_img;
+    bool pv = true;
+    if (!interior) {
+      const int gy = sy0 + spy, gx = sx0 + spx;
+      pv = gy >= 0 && gy < SH_img && gx >= 0 && gx < SW_img;
+    }
     x4 o0, o1;
-    o0[0] = (T)(pv ? fmaxf(e0[0] + sb0.x, 0.f) : 0.f);
-    o0[1] = (T)(pv ? fmaxf(e0[1] + sb0.y, 0.f) : 0.f);
-    o0[2] = (T)(pv ? fmaxf(e0[2] + sb0.z, 0.f) : 0.f);
-    o0[3] = (T)(pv ? fmaxf(e0[3] + sb0.w, 0.f) : 0.f);
-    o1[0] = (T)(pv ? fmaxf(e1[0] + sb1.x, 0.f) : 0.f);
-    o1[1] = (T)(pv ? fmaxf(e1[1] + sb1.y, 0.f) : 0.f);
-    o1[2] = (T)(pv ? fmaxf(e1[2] + sb1.z, 0.f) : 0.f);
-    o1[3] = (T)(pv ? fmaxf(e1[3] + sb1.w, 0.f) : 0.f);
-    *reinterpret_cast<x4*>(Xs + p * XS + 4 * kg) = o0;
-    *reinterpret_cast<x4*>(Xs + p * XS + 16 + 4 * kg) = o1;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      o0[r] = (T)(pv ? fmaxf(e0[r], 0.f) : 0.f);
+      o1[r] = (T)(pv ? fmaxf(e1[r], 0.f) : 0.f);
+    }
+    if (p < PS) {
+      *reinterpret_cast<x4*>(Xs + p * XS + 4 * kg) = o0;
+      *reinterpret_cast<x4*>(Xs + p * XS + 16 + 4 * kg) = o1;
+    }
   }
   __syncthreads();
 
