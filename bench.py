@@ -42,8 +42,14 @@ def pmc_traffic(kernel_key: str, path: str):
         return None
     if kernel_key in kernels:
         return kernels[kernel_key]['hbm_bytes_per_launch']
-    prefix = kernel_key.split('<')[0] + '<'
-    hits = [v for k, v in kernels.items() if k.startswith(prefix)]
+    import re
+    m = re.fullmatch(r'irb_kernel<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
+    if m:   # fused block key -> the one template instantiation profiled for that geometry
+        geo = ','.join(m.groups()) + ','
+        hits = [v for k, v in kernels.items() if re.match(r'irb_kernel<B?F16,' + re.escape(geo), k)]
+    else:
+        prefix = kernel_key.split('<')[0] + '<'
+        hits = [v for k, v in kernels.items() if k.startswith(prefix)]
     return hits[0]['hbm_bytes_per_launch'] if len(hits) == 1 else None
 
 
