@@ -177,13 +177,13 @@ __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restric
     acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
   }
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky) {
-    const int iy = oy * S - 1 + ky;
-    if (iy < 0 || iy >= H) continue;
+  for (int kx = 0; kx < 3; ++kx) {        // kx outer, ky inner: the fused kernels' accumulation order
+    const int ix = ox * S - 1 + kx;
+    if (ix < 0 || ix >= W) continue;
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int ix = ox * S - 1 + kx;
-      if (ix < 0 || ix >= W) continue;
+    for (int ky = 0; ky < 3; ++ky) {
+      const int iy = oy * S - 1 + ky;
+      if (iy < 0 || iy >= H) continue;
       const typename DT::x8 v = load8<DT>(X + (((int64_t)b * H + iy) * W + ix) * C + c);
       float wv[8];
       load_dw8<DT>(W9 + (ky * 3 + kx) * C + c, wv);

@@ -175,9 +175,9 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
 #pragma unroll
     for (int e = 0; e < 8; ++e) a8[e] = Sb[8 * kg + e];
 #pragma unroll
-    for (int ky = 0; ky < 3; ++ky)
+    for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
+      for (int ky = 0; ky < 3; ++ky) {
         const x8 v = *reinterpret_cast<const x8*>(Xs + ((oy + ky) * SW + (ox + kx)) * XS + 8 * kg);
         DW8<DT> wt;
         wt.load(Sl + (ky * 3 + kx) * 32 + 8 * kg);

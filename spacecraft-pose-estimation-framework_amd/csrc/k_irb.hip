@@ -67,6 +67,8 @@ struct IrbGeom {
   static constexpr int NCT = (COUT + 15) / 16;
   static constexpr int NCTW = NCT / WCO;       // output-channel tiles per wave
   static constexpr int KS = K16 ? 1 : CINP / 32;
+  // depthwise row pairs: a wave's consecutive pixel tiles are vertically adjacent rows (16-wide, stride 1)
+  static constexpr bool PAIR = S == 1 && TW == 16 && QPW % 2 == 0;
   static constexpr int LDS_BYTES = bytes_for(XS, ES);
   static_assert(POUT % 16 == 0 && POUT16 % WP == 0 && NW % WCO == 0 && NCT % WCO == 0, "tile split");
   static_assert(CIN % 8 == 0 && HID % 8 == 0 && COUT % 4 == 0, "channel counts must be multiples of 8");
@@ -324,7 +326,56 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     }
 
     // ---- 3. depthwise 3x3 on this hidden chunk -> project B fragment in registers; 4. project MFMA
+    // Tap order everywhere (here, the front kernel, the unfused dw_kernel): kx outer, ky inner -- the fused
+    // and unfused schedules accumulate in the same order and stay bit-identical.
     const bool hv = 32 * c + 8 * kg < HID;    // this lane's 8 hidden channels exist
+    if constexpr (G::PAIR) {
+      // Two vertically adjacent output rows per step (tiles qi, qi+1 = rows oy, oy+1 of the same 16 columns):
+      // per tap column the 3 weights and the 4 input rows are read once and feed both rows -- 21 instead of
+      // 36 ds_read_b128 per 2 x 16 pixels x 8 channels.
+#pragma unroll
+      for (int qi = 0; qi < G::QPW; qi += 2) {
+        x8 bf0 = zero8<DT>(), bf1 = zero8<DT>();
+        if (hv) {
+          float a0[8], a1[8];
+          {
+            const float4 u0 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg);
+            const float4 u1 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg + 4);
+            a0[0] = u0.x; a0[1] = u0.y; a0[2] = u0.z; a0[3] = u0.w;
+            a0[4] = u1.x; a0[5] = u1.y; a0[6] = u1.z; a0[7] = u1.w;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a1[e] = a0[e];
+          }
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            DW8<DT> w[3];
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) w[ky].load(sl + (ky * 3 + kx) * 32 + 8 * kg);
+            x8 v[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              v[r] = *reinterpret_cast<const x8*>(Es + ((oyq[qi] + r) * G::IW + oxq[qi] + kx) * G::ES + 8 * kg);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                a0[e] = fmaf((float)v[ky][e], w[ky][e], a0[e]);
+                a1[e] = fmaf((float)v[ky + 1][e], w[ky][e], a1[e]);
+              }
+          }
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            bf0[e] = (T)fmaxf(a0[e], 0.f);
+            bf1[e] = (T)fmaxf(a1[e], 0.f);
+          }
+        }
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) {
+          acc[qi][t] = DT::mfma(pa[t], bf0, acc[qi][t]);
+          acc[qi + 1][t] = DT::mfma(pa[t], bf1, acc[qi + 1][t]);
+        }
+      }
+    } else
 #pragma unroll
     for (int qi = 0; qi < G::QPW; ++qi) {
       x8 bf = zero8<DT>();
@@ -337,9 +388,9 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
           a8[4] = u1.x; a8[5] = u1.y; a8[6] = u1.z; a8[7] = u1.w;
         }
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) {
+          for (int ky = 0; ky < 3; ++ky) {
             const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
             const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + 8 * kg);
             DW8<DT> wt;   // fp16 weights: one ds_read_b128 per tap, consumed by v_fma_mix directly
