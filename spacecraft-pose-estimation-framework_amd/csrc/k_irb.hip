@@ -80,8 +80,10 @@ struct IrbGeom {
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
+// ABL (timing ablations only, never dispatched by default): 1 = depthwise centre tap only, 2 = no expand
+// MFMA, 3 = no expand epilogue / slab store, 4 = no project MFMA. Results are wrong for ABL != 0.
 template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
-          bool DBUF, bool STW>
+          bool DBUF, bool STW, int ABL = 0>
 __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const typename DT::T* __restrict__ X, const typename DT::T* __restrict__ We, const float* __restrict__ be,
     const typename DT::DW* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
@@ -202,6 +204,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   __syncthreads();
 
   // per-lane validity of its expand pixels (inside the tile and the image): the depthwise zero padding
+  // interior tiles (whole input tile inside the image) need no padding mask in the expand epilogue
+  const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + G::IH <= H && ix0 + G::IW <= W;
   uint32_t pvmask = 0;
   if constexpr (EXPAND) {
 #pragma unroll
@@ -285,7 +289,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
         const int pt = wave + NW * j;
         if (pt >= G::PIN16) break;
         f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
-        if constexpr (G::K16) {
+        if constexpr (ABL == 2) {
+        } else if constexpr (G::K16) {
           const x4 bx = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
           e0 = DT::mfma16(q0, bx, e0);
           e1 = DT::mfma16(q1, bx, e1);
@@ -298,19 +303,18 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
             e1 = DT::mfma(a1[ks], bx, e1);
           }
         }
-        const uint32_t m0 = ((pvmask >> j) & 1u) ? 0xffffffffu : 0u;
-        const uint32_t m1 = vh > 16 ? m0 : 0u;
-        x4 o0, o1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          o0[r] = (T)fmaxf(e0[r], 0.f);
-          o1[r] = (T)fmaxf(e1[r], 0.f);
-        }
+        x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);
         uint2 u0 = *reinterpret_cast<uint2*>(&o0), u1 = *reinterpret_cast<uint2*>(&o1);
-        u0.x &= m0; u0.y &= m0; u1.x &= m1; u1.y &= m1;
+        if (!interior) {   // zero the expand outputs of pixels outside the image (the depthwise padding)
+          const uint32_t m0 = ((pvmask >> j) & 1u) ? 0xffffffffu : 0u;
+          u0.x &= m0; u0.y &= m0; u1.x &= m0; u1.y &= m0;
+        }
+        // channels >= HID of a partial chunk are already 0: zero weight rows and zero bias
         T* er = Ew + (pt * 16 + r16) * G::ES + 4 * kg;
-        *reinterpret_cast<uint2*>(er) = u0;
-        *reinterpret_cast<uint2*>(er + 16) = u1;
+        if constexpr (ABL != 3) {
+          *reinterpret_cast<uint2*>(er) = u0;
+          *reinterpret_cast<uint2*>(er + 16) = u1;
+        }
       }
       Es = Ew;
     } else {
@@ -329,7 +333,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     // Tap order everywhere (here, the front kernel, the unfused dw_kernel): kx outer, ky inner -- the fused
     // and unfused schedules accumulate in the same order and stay bit-identical.
     const bool hv = 32 * c + 8 * kg < HID;    // this lane's 8 hidden channels exist
-    if constexpr (G::PAIR) {
+    if constexpr (G::PAIR && ABL == 0) {
       // Two vertically adjacent output rows per step (tiles qi, qi+1 = rows oy, oy+1 of the same 16 columns):
       // per tap column the 3 weights and the 4 input rows are read once and feed both rows -- 21 instead of
       // 36 ds_read_b128 per 2 x 16 pixels x 8 channels.
@@ -391,6 +395,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
         for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky) {
+            if (ABL == 1 && !(ky == 1 && kx == 1)) continue;
             const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
             const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + 8 * kg);
             DW8<DT> wt;   // fp16 weights: one ds_read_b128 per tap, consumed by v_fma_mix directly
@@ -402,7 +407,10 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
         for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
       }
 #pragma unroll
-      for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
+      for (int t = 0; t < G::NCTW; ++t) {
+        if constexpr (ABL == 4) acc[qi][t][0] += (float)bf[t & 7];
+        else acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
+      }
     }
     // next chunk's depthwise weights: buffer (c+1)&1 was last read by dw(c-1), which every wave finished
     // before the barrier of this chunk; the barrier of chunk c+1 publishes it before dw(c+1) reads it.
@@ -472,7 +480,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   X(2, 160, 960, 320, 1, 4, 8, true, false, 4, 2, true, true)                     
 
 template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
-          bool DBUF, bool STW>
+          bool DBUF, bool STW, int ABL = 0>
 static hipError_t irb_go(const void* x, const void* we, const float* be, const void* wd, const float* bd,
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                          hipStream_t s) {
@@ -484,7 +492,7 @@ static hipError_t irb_go(const void* x, const void* we, const float* be, const v
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   const size_t lds = (size_t)G::LDS_BYTES;
-  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW>;
+  auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, ABL>;
   static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
   if (!attr_set && lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
@@ -505,10 +513,29 @@ static bool irb_has(int variant, int cin, int hid, int cout, int stride, bool ex
 }
 
 template <typename DT>
+// timing ablations of the variant-0 configurations (tools/explore.py ABL=1): variant 100 + 10 * ABL
+#define SPEF_IRB_ABL(X)                                                                                      \
+  X(1, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) X(2, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) \
+  X(3, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) X(4, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) \
+  X(1, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(2, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
+  X(3, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(4, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
+  X(1, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) X(2, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) \
+  X(3, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) X(4, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false)
+
 static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stride, bool expand, bool res,
                                const void* x, const void* we, const float* be, const void* wd, const float* bd,
                                const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                                hipStream_t s) {
+  if (variant >= 100) {
+    const int abl = (variant - 100) / 10;
+#define SPEF_IRB_ABL_CASE(A, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_)                         \
+    if (abl == A && cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)      \
+      return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_, A>(x, we, be, wd, bd, wp, bp, y, B, H, \
+                                                                             W, OH, OW, s);
+    SPEF_IRB_ABL(SPEF_IRB_ABL_CASE)
+#undef SPEF_IRB_ABL_CASE
+    variant = 0;
+  }
   if (!irb_has(variant, cin, hid, cout, stride, expand, res)) variant = 0;
 #define SPEF_IRB_CASE(V, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_)                            \
   if (variant == V && cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)   \

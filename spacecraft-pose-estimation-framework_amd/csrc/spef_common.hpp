@@ -48,6 +48,25 @@ template <typename DT>
 __device__ __forceinline__ typename DT::x8 load8(const typename DT::T* p) {
   return *reinterpret_cast<const typename DT::x8*>(p);
 }
+// ReLU + round 4 fp32 values to the activation type: fp16 converts pairs (v_cvt_pk_f16_f32, RNE) and clamps
+// with one v_pk_max_f16 per pair -- the same values as fmaxf-then-convert (conversion is monotonic, 0 -> 0).
+template <typename DT>
+__device__ __forceinline__ typename DT::x4 relu_cvt4(f32x4 v) {
+  typename DT::x4 o;
+  if constexpr (sizeof(typename DT::T) == 2 && __is_same(typename DT::T, _Float16)) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 z = {(_Float16)0.0f, (_Float16)0.0f};
+    h2 a = {(_Float16)v[0], (_Float16)v[1]}, b = {(_Float16)v[2], (_Float16)v[3]};
+    a = __builtin_elementwise_max(a, z);
+    b = __builtin_elementwise_max(b, z);
+    o[0] = a[0]; o[1] = a[1]; o[2] = b[0]; o[3] = b[1];
+  } else {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) o[r] = (typename DT::T)fmaxf(v[r], 0.f);
+  }
+  return o;
+}
+
 // 8 consecutive depthwise weights kept in their storage type (fp16: 4 VGPRs, read by v_fma_mix directly)
 template <typename DT, bool H = (sizeof(typename DT::DW) == 2)>
 struct DW8 {
