@@ -121,12 +121,16 @@ __device__ void sym4_top_eigvec(double a[4][4], double out[4]) {
   double v[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
   for (int sweep = 0; sweep < 32; ++sweep) {
     double off = 0.0, diag = 0.0;
+#pragma unroll
     for (int p = 0; p < 4; ++p) {
       diag += a[p][p] * a[p][p];
+#pragma unroll
       for (int q = p + 1; q < 4; ++q) off += a[p][q] * a[p][q];
     }
     if (off <= 1e-34 * diag || off == 0.0) break;
+#pragma unroll
     for (int p = 0; p < 3; ++p)
+#pragma unroll
       for (int q = p + 1; q < 4; ++q) {
         const double apq = a[p][q];
         if (apq == 0.0) continue;
@@ -150,13 +154,21 @@ __device__ void sym4_top_eigvec(double a[4][4], double out[4]) {
         }
       }
   }
-  int best = 0;
+  // column of the largest diagonal entry, selected with static indices only (no scratch)
+  double bd = a[0][0], col[4] = {v[0][0], v[1][0], v[2][0], v[3][0]};
+#pragma unroll
   for (int p = 1; p < 4; ++p)
-    if (a[p][p] > a[best][best]) best = p;
+    if (a[p][p] > bd) {
+      bd = a[p][p];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) col[k] = v[k][p];
+    }
   double n = 0.0;
-  for (int k = 0; k < 4; ++k) n += v[k][best] * v[k][best];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) n += col[k] * col[k];
   n = sqrt(n);
-  for (int k = 0; k < 4; ++k) out[k] = v[k][best] / n;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) out[k] = col[k] / n;
 }
 
 // ------------------------------------------------------------------------------------------ decode ori

@@ -1,0 +1,325 @@
+// Fused INT8 inverted-residual block (QInvertedResidual, src/modeling/common/brevitas_layers.py:57-136) with
+// the integer semantics of oracle/int8_ref.py, bit-exact like the unfused k_q8.hip kernels:
+//
+//   expand   acc = sum q_x q_we (v_mfma_i32_16x16x32_i8) -> requant + ReLU -> u8, kept in LDS as fp16
+//   depthwise acc = sum u8 * q_wd over 9 taps by v_fma_mix_f32 on fp16 operands: every product and partial
+//            sum is an integer below 2^19, so the fp32 accumulation is exact -> requant + ReLU -> u8
+//   project  acc = 128 * sum q_wp + sum (u8 - 128) q_wp (int8 MFMA, unsigned operand offset by -128)
+//            -> requant to the shared signed quantizer (+ residual join + rescale) -> int8
+//
+// Structure follows the fp16 fused kernel (k_irb.hip): the input tile + halo is staged in LDS once, the hidden
+// tensor is produced 32 channels at a time into an LDS slab, the depthwise writes the project MFMA's B fragment
+// directly in registers, the project accumulates in int32 MFMA accumulators over hidden chunks. Per chunk the
+// workgroup stages its requant tables (RQ16 {int32 M, int32 S, int64 B}) and fp16 depthwise weights in LDS.
+#include "spef_common.hpp"
+#include "spef_kernels.hpp"
+
+namespace spef {
+
+namespace {
+
+typedef int i32x4_t __attribute__((ext_vector_type(4)));
+
+struct RQ16 {
+  int32_t M, S;
+  int64_t B;
+};
+
+__device__ __forceinline__ int rq_apply(int acc, const RQ16& r, int lo, int hi) {
+  const int64_t v = ((int64_t)acc * r.M + r.B) >> r.S;
+  return (int)(v < lo ? lo : (v > hi ? hi : v));
+}
+
+__device__ __forceinline__ i32x4_t mfma_i8(long a, long b, i32x4_t c) {
+  return __builtin_amdgcn_mfma_i32_16x16x32_i8(a, b, c, 0, 0, 0);
+}
+
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW>
+struct QGeom {
+  static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
+  static constexpr int PIN = IH * IW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
+  static constexpr int CINP = (CIN + 31) / 32 * 32, KSE = CINP / 32;
+  static constexpr int XSB = CINP + 8;                 // Xs row stride (bytes)
+  static constexpr int ES = 40;                        // hidden slab row stride (fp16 elements, 80 B)
+  static constexpr int H32 = (HID + 31) / 32 * 32, NCH = H32 / 32;
+  static constexpr int KPE = (CIN + 63) / 64 * 64;     // blob row length of the expand weights
+  static constexpr int KPP = (HID + 63) / 64 * 64;     // blob row length of the project weights
+  static constexpr int NPO = (COUT + 15) / 16 * 16, NCT = NPO / 16;
+  static constexpr int EPT = (PIN16 + NW - 1) / NW;
+  static constexpr int POUT16 = TH * TW / 16, QPW = POUT16 / NW;
+  static constexpr int TAB = 32 * 16 * 2 + 9 * 32 * 2;   // bytes per chunk: RQ16 expand + depthwise, fp16 weights
+  static constexpr int LDS_BYTES = PINP * XSB + PINP * ES * 2 + 2 * TAB + NPO * 16;
+  static_assert(POUT16 % NW == 0, "tile split");
+  static_assert(EPT <= 32, "validity mask is 32 bits");
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+  static_assert(!RES || (S == 1 && CIN == COUT), "residual geometry");
+};
+
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW>
+__global__ __launch_bounds__(NW * 64) void q_irb_kernel(
+    const int8_t* __restrict__ X, const int8_t* __restrict__ We, const int8_t* __restrict__ Wp,
+    const int32_t* __restrict__ pinit, const uint8_t* __restrict__ tabs, int64_t RM, int64_t RB, int RSH,
+    int8_t* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y, uint32_t nwg) {
+  using G = QGeom<CIN, HID, COUT, S, TH, TW, RES, NW>;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  int8_t* Xs = reinterpret_cast<int8_t*>(smem);
+  _Float16* Es = reinterpret_cast<_Float16*>(smem + G::PINP * G::XSB);
+  uint8_t* Tb = reinterpret_cast<uint8_t*>(Es + G::PINP * G::ES);          // [2][TAB]
+  RQ16* RqP = reinterpret_cast<RQ16*>(Tb + 2 * G::TAB);                      // [NPO]
+
+  // x2 table layout (spef_blob.hpp): RQ16 expand [H32] | RQ16 depthwise [H32] | RQ16 project [NPO] | fp16 [9][H32]
+  const RQ16* gRqE = reinterpret_cast<const RQ16*>(tabs);
+  const RQ16* gRqD = gRqE + G::H32;
+  const RQ16* gRqP = gRqD + G::H32;
+  const _Float16* gWd = reinterpret_cast<const _Float16*>(gRqP + G::NPO);
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int tx = (int)(L % (uint32_t)tiles_x);
+  L /= (uint32_t)tiles_x;
+  const int ty = (int)(L % (uint32_t)tiles_y);
+  const int b = (int)(L / (uint32_t)tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+
+  // per-chunk tables -> LDS buffer (cc & 1): 16-B pieces, RQ16 expand (32), RQ16 depthwise (32), weights (36)
+  auto stage_tables = [&](int cc) {
+    uint4* dst = reinterpret_cast<uint4*>(Tb + (cc & 1) * G::TAB);
+    for (int u = tid; u < 32 + 32 + 36; u += NW * 64) {
+      uint4 v;
+      if (u < 32) v = *reinterpret_cast<const uint4*>(gRqE + 32 * cc + u);
+      else if (u < 64) v = *reinterpret_cast<const uint4*>(gRqD + 32 * cc + (u - 32));
+      else {
+        const int f = (u - 64) * 8, tap = f >> 5, ch = f & 31;   // 8 fp16 weights of one tap
+        v = *reinterpret_cast<const uint4*>(gWd + tap * G::H32 + 32 * cc + ch);
+      }
+      dst[u] = v;
+    }
+  };
+
+  // ---- 1. input tile (+halo) -> LDS (int8; zero outside the image and in the K padding), tables of chunk 0
+  {
+    constexpr int GPR = G::CINP / 8, CG = CIN / 8;
+    constexpr int NU = G::PINP * GPR, NIT = (NU + NW * 64 - 1) / (NW * 64);
+    const int8_t* Xb = X + (size_t)b * H * W * CIN;
+    long xin[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int u = tid + NW * 64 * i;
+      const int p = u / GPR, g = u - p * GPR;
+      xin[i] = 0;
+      if (u < NU && p < G::PIN && g < CG) {
+        const int py = p / G::IW, px = p - py * G::IW;
+        const int iy = iy0 + py, ix = ix0 + px;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W)
+          xin[i] = *reinterpret_cast<const long*>(Xb + ((size_t)iy * W + ix) * CIN + g * 8);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int u = tid + NW * 64 * i;
+      if (u < NU) {
+        const int p = u / GPR, g = u - p * GPR;
+        *reinterpret_cast<long*>(Xs + p * G::XSB + g * 8) = xin[i];
+      }
+    }
+    for (int u = tid; u < G::NPO; u += NW * 64) RqP[u] = gRqP[u];
+    stage_tables(0);
+  }
+
+  uint32_t pvmask = 0;   // validity of this lane's expand pixels (inside the image): the depthwise zero padding
+#pragma unroll
+  for (int j = 0; j < G::EPT; ++j) {
+    const int p = (wave + NW * j) * 16 + r16;
+    if (p < G::PIN) {
+      const int py = p / G::IW, px = p - py * G::IW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      if (iy >= 0 && iy < H && ix >= 0 && ix < W) pvmask |= 1u << j;
+    }
+  }
+  int oyq[G::QPW], oxq[G::QPW];
+#pragma unroll
+  for (int qi = 0; qi < G::QPW; ++qi) {
+    const int o = (wave * G::QPW + qi) * 16 + r16;
+    oyq[qi] = o / TW;
+    oxq[qi] = o - oyq[qi] * TW;
+  }
+  i32x4_t acc[G::QPW][G::NCT];   // project accumulators start at the offset correction 128 * sum_k q_wp
+#pragma unroll
+  for (int t = 0; t < G::NCT; ++t) {
+    const int4 v = *reinterpret_cast<const int4*>(pinit + 16 * t + 4 * kg);
+#pragma unroll
+    for (int qi = 0; qi < G::QPW; ++qi) acc[qi][t] = i32x4_t{v.x, v.y, v.z, v.w};
+  }
+  __syncthreads();
+
+#pragma unroll 1
+  for (int c = 0; c < G::NCH; ++c) {
+    const uint8_t* tb = Tb + (c & 1) * G::TAB;
+    const RQ16* rqE = reinterpret_cast<const RQ16*>(tb);
+    const RQ16* rqD = rqE + 32;
+    const _Float16* wd = reinterpret_cast<const _Float16*>(rqD + 32);
+    // project weight fragments of this chunk, in flight across the expand
+    long pa[G::NCT];
+#pragma unroll
+    for (int t = 0; t < G::NCT; ++t)
+      pa[t] = *reinterpret_cast<const long*>(Wp + (size_t)(16 * t + r16) * G::KPP + 32 * c + 8 * kg);
+    if (c > 0) __syncthreads();   // every wave's depthwise reads of the previous chunk's slab are done
+
+    // ---- 2. expand (32 hidden channels) -> requant -> u8 as fp16 in the slab
+    {
+      long a0[G::KSE], a1[G::KSE];
+      const int h0 = 32 * c + r16, h1 = 32 * c + 16 + r16;
+#pragma unroll
+      for (int ks = 0; ks < G::KSE; ++ks) {
+        a0[ks] = h0 < HID ? *reinterpret_cast<const long*>(We + (size_t)h0 * G::KPE + 32 * ks + 8 * kg) : 0;
+        a1[ks] = h1 < HID ? *reinterpret_cast<const long*>(We + (size_t)h1 * G::KPE + 32 * ks + 8 * kg) : 0;
+      }
+      RQ16 r0[4], r1[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        r0[r] = rqE[4 * kg + r];
+        r1[r] = rqE[16 + 4 * kg + r];
+      }
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        const int pt = wave + NW * j;
+        if (pt >= G::PIN16) break;
+        i32x4_t e0 = {0, 0, 0, 0}, e1 = {0, 0, 0, 0};
+#pragma unroll
+        for (int ks = 0; ks < G::KSE; ++ks) {
+          const long bx = *reinterpret_cast<const long*>(Xs + (pt * 16 + r16) * G::XSB + 32 * ks + 8 * kg);
+          e0 = mfma_i8(a0[ks], bx, e0);
+          e1 = mfma_i8(a1[ks], bx, e1);
+        }
+        const bool pv = (pvmask >> j) & 1u;
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 o0, o1;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          o0[r] = (_Float16)(pv ? rq_apply(e0[r], r0[r], 0, 255) : 0);
+          o1[r] = (_Float16)(pv ? rq_apply(e1[r], r1[r], 0, 255) : 0);
+        }
+        _Float16* er = Es + (pt * 16 + r16) * G::ES + 4 * kg;
+        *reinterpret_cast<h4*>(er) = o0;
+        *reinterpret_cast<h4*>(er + 16) = o1;
+      }
+    }
+    __syncthreads();   // slab and this chunk's tables visible
+
+    // ---- 3. depthwise (exact fp32 sums of integer products) -> requant -> offset int8 B fragment; 4. project
+    {
+      RQ16 rd[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) rd[e] = rqD[8 * kg + e];
+#pragma unroll
+      for (int qi = 0; qi < G::QPW; ++qi) {
+        float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
+            const f16x8 v = *reinterpret_cast<const f16x8*>(Es + p * G::ES + 8 * kg);
+            const f16x8 w = *reinterpret_cast<const f16x8*>(wd + (ky * 3 + kx) * 32 + 8 * kg);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], (float)w[e], a8[e]);
+          }
+        uint32_t lo = 0, hi = 0;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          const uint32_t q = (uint32_t)(rq_apply((int)a8[e], rd[e], 0, 255) ^ 0x80) & 0xffu;
+          if (e < 4) lo |= q << (8 * e);
+          else hi |= q << (8 * (e - 4));
+        }
+        const long bf = (long)(((uint64_t)hi << 32) | lo);
+#pragma unroll
+        for (int t = 0; t < G::NCT; ++t) acc[qi][t] = mfma_i8(pa[t], bf, acc[qi][t]);
+      }
+    }
+    if (c + 1 < G::NCH) stage_tables(c + 1);   // buffer (c+1)&1 was last read in chunk c-1
+  }
+
+  // ---- 5. epilogue: requant to the block's output scale (+ residual join + rescale) -> int8 NHWC
+#pragma unroll
+  for (int qi = 0; qi < G::QPW; ++qi) {
+    const int oy = oyq[qi], ox = oxq[qi];
+    const int gy = oy0 + oy, gx = ox0 + ox;
+    if (gy >= OH || gx >= OW) continue;
+    int8_t* yr = Y + (((size_t)b * OH + gy) * OW + gx) * COUT;
+#pragma unroll
+    for (int t = 0; t < G::NCT; ++t) {
+      const int o = 16 * t + 4 * kg;
+      if (o >= COUT) continue;
+      uint32_t packed = 0;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        int q = rq_apply(acc[qi][t][r], RqP[o + r], -128, 127);
+        if constexpr (RES) {
+          q += (int)Xs[((oy + 1) * G::IW + (ox + 1)) * G::XSB + o + r];
+          const int64_t v = ((int64_t)q * RM + RB) >> RSH;
+          q = (int)(v < -128 ? -128 : (v > 127 ? 127 : v));
+        }
+        packed |= ((uint32_t)q & 0xffu) << (8 * r);
+      }
+      *reinterpret_cast<uint32_t*>(yr + o) = packed;
+    }
+  }
+}
+
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW>
+hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const int32_t* pinit, const uint8_t* tabs,
+                    int64_t rm, int64_t rb, int rs, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
+  using G = QGeom<CIN, HID, COUT, S, TH, TW, RES, NW>;
+  const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
+  const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
+  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+  const uint32_t nwg = (uint32_t)nwg64;
+  auto k = q_irb_kernel<CIN, HID, COUT, S, TH, TW, RES, NW>;
+  static bool attr_set = false;
+  if (!attr_set && G::LDS_BYTES > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  k<<<nwg, NW * 64, G::LDS_BYTES, s>>>(x, we, wp, pinit, tabs, rm, rb, rs, y, H, W, OH, OW, tiles_x, tiles_y, nwg);
+  return hipGetLastError();
+}
+
+// (cin, hidden, cout, stride, TH, TW, residual, waves) for MobileNet-V2 blocks 2-17
+#define SPEF_QIRB_TABLE(X)                                                              \
+  X(16, 96, 24, 2, 8, 16, false, 8)     /* block 2      */                             \
+  X(24, 144, 24, 1, 8, 16, true, 4)     /* block 3      */                             \
+  X(24, 144, 32, 2, 8, 8, false, 4)     /* block 4      */                             \
+  X(32, 192, 32, 1, 16, 16, true, 8)    /* blocks 5-6   */                             \
+  X(32, 192, 64, 2, 8, 8, false, 4)     /* block 7      */                             \
+  X(64, 384, 64, 1, 16, 16, true, 8)    /* blocks 8-10  */                             \
+  X(64, 384, 96, 1, 16, 16, false, 8)   /* block 11     */                             \
+  X(96, 576, 96, 1, 16, 16, true, 8)    /* blocks 12-13 */                             \
+  X(96, 576, 160, 2, 8, 8, false, 4)    /* block 14     */                             \
+  X(160, 960, 160, 1, 8, 8, true, 4)    /* blocks 15-16 */                             \
+  X(160, 960, 320, 1, 8, 8, false, 4)   /* block 17     */
+
+}  // namespace
+
+bool q_irb_supported(int cin, int hid, int cout, int stride, bool res) {
+#define SPEF_QIRB_HAS(CI, HI, CO, ST, TH_, TW_, RS, NW_) \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS) return true;
+  SPEF_QIRB_TABLE(SPEF_QIRB_HAS)
+#undef SPEF_QIRB_HAS
+  return false;
+}
+
+hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, const int8_t* x, const int8_t* we,
+                        const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm, int64_t rb, int rs,
+                        int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
+#define SPEF_QIRB_CASE(CI, HI, CO, ST, TH_, TW_, RS, NW_)                                              \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS)                               \
+    return q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, OH, OW, s);
+  SPEF_QIRB_TABLE(SPEF_QIRB_CASE)
+#undef SPEF_QIRB_CASE
+  return hipErrorNotSupported;
+}
+
+}  // namespace spef

@@ -397,6 +397,27 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
       const int64_t M2 = (int64_t)B * OH * OW;
       const bool res = op.flags & 1u;
       void* x = cur;
+      if (c->fuse && op.expand != 1 && op.x2 != kAbsent &&
+          q_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res)) {
+        void* y = pick({x});
+        const std::array<int64_t, 3>& r3 = c->q8_res[&op - c->ops.data()];
+        char key[96];
+        snprintf(key, sizeof(key), "q_irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
+        HIP_TRY(prof_launch(c, s, key, (double)M * op.cin + (double)M2 * op.cout + (double)op.hidden * (op.cin + op.cout + 9),
+                            2.0 * M * op.cin * op.hidden + 18.0 * M2 * op.hidden + 2.0 * M2 * op.hidden * op.cout, [&] {
+          return launch_q_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, (const int8_t*)x,
+                              ptr<int8_t>(c, op.w0), ptr<int8_t>(c, op.w2), ptr<int32_t>(c, op.x0),
+                              ptr<uint8_t>(c, op.x2), r3[0], r3[1], (int)r3[2], (int8_t*)y, B, h, w, OH, OW, s);
+        }));
+        cur = y;
+        h = OH;
+        w = OW;
+        ch = (int)op.cout;
+        uns = 0;
+        if (mode == 1 && op_index == stop) break;
+        ++op_index;
+        continue;
+      }
       void* h1 = x;
       if (op.expand != 1) {
         h1 = pick({x});
@@ -581,7 +602,7 @@ static int parse_blob(spef_ctx* c, const uint8_t* head_bytes, size_t bytes) {
   std::vector<OpDesc> ops(h.n_ops);
   memcpy(ops.data(), head_bytes + h.ops_off, h.n_ops * sizeof(OpDesc));
   for (const OpDesc& op : ops) {
-    for (uint64_t off : {op.w0, op.b0, op.w1, op.b1, op.w2, op.b2, op.x0, op.x1})
+    for (uint64_t off : {op.w0, op.b0, op.w1, op.b1, op.w2, op.b2, op.x0, op.x1, op.x2})
       if (off != kAbsent && (off >= h.data_bytes || (off & 15)))
         return fail(SPEF_ERR_BLOB, "tensor offset out of range / misaligned");
     if ((op.kind == OP_IRB || op.kind == OP_QIRB) &&

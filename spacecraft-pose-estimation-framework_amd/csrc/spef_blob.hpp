@@ -17,7 +17,9 @@
 //            quant), x0 fp32 [1] input scale (f32 NCHW path)
 //   OP_QIRB  w0/b0 expand int8 [Np][Kp64] + RQ (absent if t==1); w1/b1 dw int8 [9][hidden] + RQ;
 //            w2/b2 project int8 [Np][Kp64] + RQ; x0 int32 [Np] project accumulator init (128 * sum_k q_w);
-//            x1 int64 [3] residual-join rescale (R, RB, RS) when flags & 1; flags & 2: unsigned block input
+//            x1 int64 [3] residual-join rescale (R, RB, RS) when flags & 1; flags & 2: unsigned block input;
+//            x2 fused-kernel tables (expand ops): RQ16 expand [H32] | RQ16 depthwise [H32] | RQ16 project [Np] |
+//            depthwise weights fp16 [9][H32] (H32 = hidden rounded up to 32; RQ16 = {int32 M, int32 S, int64 B})
 //   OP_QLAST w0 int8 [Np][Kp64], b0 RQ
 //   OP_QFC   w0 int8 [Np][1280] (ori rows then pos), b0 fp64 [Np] weight scales, w1 fp64 [Np] float bias,
 //            x0 int32 [Np] 128 * sum_k q_w, x1 fp64 [1] last-conv activation scale
@@ -49,8 +51,8 @@ struct BlobHeader {
 struct OpDesc {
   uint32_t kind, cin, cout, hidden, stride, expand, flags, pad0;
   uint64_t w0, b0, w1, b1, w2, b2;
-  uint64_t x0, x1;   // int8 ops only (kAbsent otherwise)
-  uint8_t reserved[32];
+  uint64_t x0, x1, x2;   // extra tensors (int8 ops; kAbsent otherwise)
+  uint8_t reserved[24];
 };
 #pragma pack(pop)
 static_assert(sizeof(BlobHeader) == 128, "BlobHeader must be 128 bytes");

@@ -29,7 +29,7 @@ OP_QSTEM, OP_QIRB, OP_QLAST, OP_QFC = 11, 12, 13, 14
 HEAD_URSONET, HEAD_KEYPOINTS = 0, 1
 ABSENT = (1 << 64) - 1
 _HDR = struct.Struct('<8sIIII' + 'IIIIII' + 'QQQ' + '56s')
-_OP = struct.Struct('<IIIIIIII' + 'QQQQQQ' + 'QQ' + '32s')
+_OP = struct.Struct('<IIIIIIII' + 'QQQQQQ' + 'QQQ' + '24s')
 assert _HDR.size == 128 and _OP.size == 128
 
 
@@ -170,7 +170,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
 
 def assemble(dtype_code: int, head: int, n0: int, n1: int, fh: int, fw: int, ops, data: _Data) -> bytes:
     """Header + op table + data section. An op is (kind, cin, cout, hidden, stride, expand, flags,
-    w0, b0, w1, b1, w2, b2[, x0, x1])."""
+    w0, b0, w1, b1, w2, b2[, x0, x1, x2])."""
     ops_off = _HDR.size
     data_off = ops_off + _OP.size * len(ops)
     data_off += (-data_off) % 256
@@ -178,8 +178,8 @@ def assemble(dtype_code: int, head: int, n0: int, n1: int, fh: int, fw: int, ops
                     ops_off, data_off, data.size, b'\0' * 56)
     out = bytearray(hdr)
     for o in ops:
-        x = tuple(o[13:15]) + (ABSENT,) * (15 - max(13, len(o)))
-        out += _OP.pack(*o[:7], 0, *o[7:13], *x, b'\0' * 32)
+        x = tuple(o[13:16]) + (ABSENT,) * (16 - max(13, len(o)))
+        out += _OP.pack(*o[:7], 0, *o[7:13], *x, b'\0' * 24)
     out += b'\0' * (data_off - len(out))
     for ch in data.chunks:
         out += ch
@@ -193,5 +193,5 @@ def describe(blob: bytes) -> dict:
         raise ValueError('not a SPEF MI355X blob')
     info = dict(version=h[1], dtype=h[2], head=h[3], n_ops=h[4], n_out0=h[5], n_out1=h[6], feat_c=h[7],
                 kp_fh=h[8], kp_fw=h[9], ops_off=h[11], data_off=h[12], data_bytes=h[13])
-    info['ops'] = [_OP.unpack_from(blob, info['ops_off'] + i * _OP.size)[:16] for i in range(info['n_ops'])]
+    info['ops'] = [_OP.unpack_from(blob, info['ops_off'] + i * _OP.size)[:17] for i in range(info['n_ops'])]
     return info

@@ -84,6 +84,25 @@ def _pw(data: _Data, q):
     return data.add(w.tobytes()), init
 
 
+def _rq16(M, B, S, n_pad: int) -> bytes:
+    """RQ16 records {int32 M, int32 S, int64 B} over n_pad channels (padding: M = B = 0, S = 1 -> 0)."""
+    rec = np.zeros(n_pad, dtype=[('M', '<i4'), ('S', '<i4'), ('B', '<i8')])
+    rec['S'] = 1
+    n = M.size
+    assert np.all(np.abs(M) < 2 ** 31)
+    rec['M'][:n], rec['S'][:n], rec['B'][:n] = M, S, B
+    return rec.tobytes()
+
+
+def _fused_tables(e_rq, d_rq, p_rq, qdw, hidden: int, cout: int) -> bytes:
+    """x2 of an expand block: the fused int8 kernel's per-channel tables (spef_blob.hpp)."""
+    h32 = (hidden + 31) // 32 * 32
+    np_ = (cout + 15) // 16 * 16
+    wd = np.zeros((9, h32), np.float16)
+    wd[:, :hidden] = qdw[:, 0].reshape(hidden, 9).T          # int8 values, exact in fp16
+    return _rq16(*e_rq, h32) + _rq16(*d_rq, h32) + _rq16(*p_rq, np_) + wd.tobytes()
+
+
 def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None) -> bytes:
     """Pack a reference-layout FP32 state_dict + activation scales into an int8 blob (URSONet head)."""
     arch = arch or arch_from_state_dict(sd)
@@ -112,27 +131,31 @@ def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None) -> bytes:
         s_in = s_q if s_q is not None else s_x
         j = 0
         e_w = e_b = ABSENT
+        e_rq = None
         if blk.expand != 1:
-            q, (M, B, S) = _conv(sd, f'{fp}.{blk.index}.conv.0', s_in, bq['expand'])
+            q, e_rq = _conv(sd, f'{fp}.{blk.index}.conv.0', s_in, bq['expand'])
             e_w, _ = _pw(data, q)
-            e_b = _rq(data, M, B, S)
+            e_b = _rq(data, *e_rq)
             s_y, j = bq['expand'], 1
         else:
             s_y = s_in
-        q, (M, B, S) = _conv(sd, f'{fp}.{blk.index}.conv.{j}', s_y, bq['dw'])
-        w9 = np.ascontiguousarray(q[:, 0].reshape(q.shape[0], 9).T.astype(np.int8))     # [9][C], tap = ky*3+kx
-        d_w, d_b = data.add(w9.tobytes()), _rq(data, M, B, S)
+        qdw, d_rq = _conv(sd, f'{fp}.{blk.index}.conv.{j}', s_y, bq['dw'])
+        w9 = np.ascontiguousarray(qdw[:, 0].reshape(qdw.shape[0], 9).T.astype(np.int8))   # [9][C], tap = ky*3+kx
+        d_w, d_b = data.add(w9.tobytes()), _rq(data, *d_rq)
         p_out = s_q if blk.residual else s_next
-        q, (M, B, S) = _conv(sd, f'{fp}.{blk.index}.conv.{j + 1}', bq['dw'], p_out)
+        q, p_rq = _conv(sd, f'{fp}.{blk.index}.conv.{j + 1}', bq['dw'], p_out)
         p_w, init = _pw(data, q)
-        p_b = _rq(data, M, B, S)
+        p_b = _rq(data, *p_rq)
+        x2 = ABSENT
+        if e_rq is not None:
+            x2 = data.add(_fused_tables(e_rq, d_rq, p_rq, qdw, blk.hidden, blk.cout))
         x1 = ABSENT
         if blk.residual:
             R, RB, RS = fixed(s_q / s_next, 0.0)
             x1 = data.add(np.array([R[0], RB[0], RS[0]], np.int64).tobytes())
         flags = (1 if blk.residual else 0) | (2 if s_q is None else 0)
         ops.append((OP_QIRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, flags,
-                    e_w, e_b, d_w, d_b, p_w, p_b, data.add(init.tobytes()), x1))
+                    e_w, e_b, d_w, d_b, p_w, p_b, data.add(init.tobytes()), x1, x2))
 
     q, (M, B, S) = _conv(sd, arch.last.prefix, qp['final'], qp['last'])
     l_w, _ = _pw(data, q)
