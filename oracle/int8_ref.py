@@ -80,7 +80,9 @@ def bn(sd, prefix):
 
 def fixed(m, b):
     """Per-channel fixed-point form of ``x * m + b``: -> (M int64, B int64 incl. the rounding half, sh int64)
-    with q = (x * M + B) >> sh. |m| * 2**sh in [2**29, 2**30); sh capped so |b| * 2**sh < 2**61."""
+    with q = (x * M + B) >> sh. |m| * 2**sh in [2**29, 2**30), raised to sh = 32 when |m| < 0.5 (so sh >= 32 and
+    |M| < 2**31 for every realistic conv scale: the fused kernel's 3-instruction requant); sh capped so
+    |b| * 2**sh < 2**61."""
     m = np.atleast_1d(np.asarray(m, np.float64))
     b = np.broadcast_to(np.atleast_1d(np.asarray(b, np.float64)), m.shape)
     M = np.zeros(m.shape, np.int64)
@@ -89,7 +91,10 @@ def fixed(m, b):
     for i in range(m.size):
         em = math.frexp(abs(m[i]))[1] if m[i] != 0 else -30
         eb = math.frexp(abs(b[i]))[1] if b[i] != 0 else -200
-        sh = int(min(30 - em, 61 - eb, 62))
+        sh0 = 30 - em
+        if sh0 < 32 and abs(m[i]) < 0.5:
+            sh0 = 32           # |M| < 2**31 still: the kernels take the high word of acc * M + B and shift by sh - 32
+        sh = int(min(sh0, 61 - eb, 62))
         assert sh >= 1, (m[i], b[i])
         M[i] = int(np.rint(math.ldexp(m[i], sh)))
         B[i] = int(np.rint(math.ldexp(b[i], sh))) + (1 << (sh - 1))

@@ -25,9 +25,12 @@ struct RQ16 {
   int64_t B;
 };
 
+// The packer guarantees S >= 32 for fused blocks (blob_q8.py), so (acc * M + B) >> S is the high word of the
+// 64-bit v_mad_i64_i32 result shifted by S - 32: three VALU ops with the clamp (v_med3_i32).
 __device__ __forceinline__ int rq_apply(int acc, const RQ16& r, int lo, int hi) {
-  const int64_t v = ((int64_t)acc * r.M + r.B) >> r.S;
-  return (int)(v < lo ? lo : (v > hi ? hi : v));
+  const int64_t t = (int64_t)acc * r.M + r.B;
+  const int v = (int)(t >> 32) >> (r.S - 32);
+  return min(max(v, lo), hi);   // v_med3_i32
 }
 
 __device__ __forceinline__ i32x4_t mfma_i8(long a, long b, i32x4_t c) {
@@ -55,7 +58,7 @@ struct QGeom {
   static_assert(!RES || (S == 1 && CIN == COUT), "residual geometry");
 };
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, bool EXPAND>
 __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
     const int8_t* __restrict__ X, const int8_t* __restrict__ We, const int8_t* __restrict__ Wp,
     const int32_t* __restrict__ pinit, const uint8_t* __restrict__ tabs, int64_t RM, int64_t RB, int RSH,
@@ -167,8 +170,19 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
       pa[t] = *reinterpret_cast<const long*>(Wp + (size_t)(16 * t + r16) * G::KPP + 32 * c + 8 * kg);
     if (c > 0) __syncthreads();   // every wave's depthwise reads of the previous chunk's slab are done
 
-    // ---- 2. expand (32 hidden channels) -> requant -> u8 as fp16 in the slab
-    {
+    // ---- 2. expand (32 hidden channels) -> requant -> u8 as fp16 in the slab. t == 1 (block 1): the hidden
+    // tensor is the unsigned stem output itself, converted to fp16 (zero outside the image from the staging).
+    if constexpr (!EXPAND) {
+      static_assert(HID == 32 && CIN == 32, "t == 1 is MobileNet-V2 block 1");
+      for (int u = tid; u < G::PIN * 4; u += NW * 64) {
+        const int p = u >> 2, g = u & 3;
+        const uint2 v = *reinterpret_cast<const uint2*>(Xs + p * G::XSB + 8 * g);
+        f16x8 o;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) o[e] = (_Float16)(int)(((e < 4 ? v.x : v.y) >> (8 * (e & 3))) & 0xffu);
+        *reinterpret_cast<f16x8*>(Es + p * G::ES + 8 * g) = o;
+      }
+    } else {
       long a0[G::KSE], a1[G::KSE];
       const int h0 = 32 * c + r16, h1 = 32 * c + 16 + r16;
 #pragma unroll
@@ -268,7 +282,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
   }
 }
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, bool EXPAND>
 hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const int32_t* pinit, const uint8_t* tabs,
                     int64_t rm, int64_t rb, int rs, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
   using G = QGeom<CIN, HID, COUT, S, TH, TW, RES, NW>;
@@ -276,7 +290,7 @@ hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  auto k = q_irb_kernel<CIN, HID, COUT, S, TH, TW, RES, NW>;
+  auto k = q_irb_kernel<CIN, HID, COUT, S, TH, TW, RES, NW, EXPAND>;
   static bool attr_set = false;
   if (!attr_set && G::LDS_BYTES > 65536) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
@@ -289,34 +303,35 @@ hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
 
 // (cin, hidden, cout, stride, TH, TW, residual, waves) for MobileNet-V2 blocks 2-17
 #define SPEF_QIRB_TABLE(X)                                                              \
-  X(16, 96, 24, 2, 8, 16, false, 8)     /* block 2      */                             \
-  X(24, 144, 24, 1, 8, 16, true, 4)     /* block 3      */                             \
-  X(24, 144, 32, 2, 8, 8, false, 4)     /* block 4      */                             \
-  X(32, 192, 32, 1, 16, 16, true, 8)    /* blocks 5-6   */                             \
-  X(32, 192, 64, 2, 8, 8, false, 4)     /* block 7      */                             \
-  X(64, 384, 64, 1, 16, 16, true, 8)    /* blocks 8-10  */                             \
-  X(64, 384, 96, 1, 16, 16, false, 8)   /* block 11     */                             \
-  X(96, 576, 96, 1, 16, 16, true, 8)    /* blocks 12-13 */                             \
-  X(96, 576, 160, 2, 8, 8, false, 4)    /* block 14     */                             \
-  X(160, 960, 160, 1, 8, 8, true, 4)    /* blocks 15-16 */                             \
-  X(160, 960, 320, 1, 8, 8, false, 4)   /* block 17     */
+  X(32, 32, 16, 1, 16, 16, false, 8, false)     /* block 1 (t = 1) */                  \
+  X(16, 96, 24, 2, 8, 16, false, 8, true)       /* block 2      */                     \
+  X(24, 144, 24, 1, 8, 16, true, 4, true)       /* block 3      */                     \
+  X(24, 144, 32, 2, 8, 8, false, 4, true)       /* block 4      */                     \
+  X(32, 192, 32, 1, 16, 16, true, 8, true)      /* blocks 5-6   */                     \
+  X(32, 192, 64, 2, 8, 8, false, 4, true)       /* block 7      */                     \
+  X(64, 384, 64, 1, 16, 16, true, 8, true)      /* blocks 8-10  */                     \
+  X(64, 384, 96, 1, 16, 16, false, 8, true)     /* block 11     */                     \
+  X(96, 576, 96, 1, 16, 16, true, 8, true)      /* blocks 12-13 */                     \
+  X(96, 576, 160, 2, 8, 8, false, 4, true)      /* block 14     */                     \
+  X(160, 960, 160, 1, 8, 8, true, 4, true)      /* blocks 15-16 */                     \
+  X(160, 960, 320, 1, 8, 8, false, 4, true)     /* block 17     */
 
 }  // namespace
 
-bool q_irb_supported(int cin, int hid, int cout, int stride, bool res) {
-#define SPEF_QIRB_HAS(CI, HI, CO, ST, TH_, TW_, RS, NW_) \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS) return true;
+bool q_irb_supported(int cin, int hid, int cout, int stride, bool res, bool expand) {
+#define SPEF_QIRB_HAS(CI, HI, CO, ST, TH_, TW_, RS, NW_, EX) \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS && expand == EX) return true;
   SPEF_QIRB_TABLE(SPEF_QIRB_HAS)
 #undef SPEF_QIRB_HAS
   return false;
 }
 
-hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, const int8_t* x, const int8_t* we,
+hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, const int8_t* x, const int8_t* we,
                         const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm, int64_t rb, int rs,
                         int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
-#define SPEF_QIRB_CASE(CI, HI, CO, ST, TH_, TW_, RS, NW_)                                              \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS)                               \
-    return q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, OH, OW, s);
+#define SPEF_QIRB_CASE(CI, HI, CO, ST, TH_, TW_, RS, NW_, EX)                                          \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS && expand == EX)                 \
+    return q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, OH, OW, s);
   SPEF_QIRB_TABLE(SPEF_QIRB_CASE)
 #undef SPEF_QIRB_CASE
   return hipErrorNotSupported;

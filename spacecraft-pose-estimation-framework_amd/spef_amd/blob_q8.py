@@ -39,7 +39,8 @@ def _bn(sd, prefix):
 
 
 def fixed(m, b):
-    """x * m + b in fixed point: (M, B incl. rounding half, sh), |m| 2**sh in [2**29, 2**30), |b| 2**sh < 2**61."""
+    """x * m + b in fixed point: (M, B incl. rounding half, sh), |m| 2**sh in [2**29, 2**30) raised to sh = 32 when
+    |m| < 0.5, |b| 2**sh < 2**61 (oracle/int8_ref.fixed states the same rule)."""
     m = np.atleast_1d(np.asarray(m, np.float64))
     b = np.broadcast_to(np.atleast_1d(np.asarray(b, np.float64)), m.shape)
     M = np.zeros(m.shape, np.int64)
@@ -48,7 +49,10 @@ def fixed(m, b):
     for i in range(m.size):
         em = math.frexp(abs(m[i]))[1] if m[i] != 0 else -30
         eb = math.frexp(abs(b[i]))[1] if b[i] != 0 else -200
-        sh = int(min(30 - em, 61 - eb, 62))
+        sh0 = 30 - em
+        if sh0 < 32 and abs(m[i]) < 0.5:
+            sh0 = 32           # |M| < 2**31 still: the kernels take the high word of acc * M + B and shift by sh - 32
+        sh = int(min(sh0, 61 - eb, 62))
         if sh < 1:
             raise ValueError(f'requant scale out of range (m={m[i]}, b={b[i]})')
         M[i] = int(np.rint(math.ldexp(m[i], sh)))
@@ -147,7 +151,11 @@ def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None) -> bytes:
         p_w, init = _pw(data, q)
         p_b = _rq(data, *p_rq)
         x2 = ABSENT
-        if e_rq is not None:
+        # the fused kernel's requant takes the high word of acc * M + B: every shift must be >= 32 and |M| < 2**31
+        if e_rq is None:     # t == 1: no expand table (zero records, unused by the kernel)
+            e_rq = (np.zeros(blk.hidden, np.int64), np.zeros(blk.hidden, np.int64), np.full(blk.hidden, 32))
+        fusable = all(np.all(r[2] >= 32) and np.all(np.abs(r[0]) < 2 ** 31) for r in (e_rq, d_rq, p_rq))
+        if fusable:
             x2 = data.add(_fused_tables(e_rq, d_rq, p_rq, qdw, blk.hidden, blk.cout))
         x1 = ABSENT
         if blk.residual:
