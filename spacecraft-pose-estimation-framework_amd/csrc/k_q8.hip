@@ -299,24 +299,32 @@ __global__ __launch_bounds__(256) void q_gemm_kernel(const int8_t* __restrict__ 
 
 // ------------------------------------------------------------------------------------------------ pool
 // QuantAvgPool2d + TruncTo8bit over the whole map (ursonet.py:61-62, 88): pooled = (sum_hw q) >> tb, stored
-// offset (u - 128) as the FC's int8 B operand. One thread per (image, 4 channels).
+// offset (u - 128) as the FC's int8 B operand. Workgroup = (image, 64 channels): 16 lanes x 4 channels per row
+// of pixels, 16 pixel rows strided over the map, integer partial sums reduced through LDS (exact, any order).
 __global__ __launch_bounds__(256) void q_pool_kernel(const uint8_t* __restrict__ X, int8_t* __restrict__ P, int B,
                                                      int HW, int C, int tb) {
-  const int cg = C >> 2;
-  const int t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= B * cg) return;
-  const int b = t / cg, c0 = 4 * (t % cg);
+  __shared__ int part[16][64];
+  const int b = blockIdx.y, c0 = blockIdx.x * 64;
+  const int cl = threadIdx.x & 15, pg = threadIdx.x >> 4;
   int s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  for (int p = 0; p < HW; ++p) {
-    const uint32_t v = *reinterpret_cast<const uint32_t*>(X + ((size_t)b * HW + p) * C + c0);
+  for (int p = pg; p < HW; p += 16) {
+    const uint32_t v = *reinterpret_cast<const uint32_t*>(X + ((size_t)b * HW + p) * C + c0 + 4 * cl);
     s0 += v & 0xff;
     s1 += (v >> 8) & 0xff;
     s2 += (v >> 16) & 0xff;
     s3 += v >> 24;
   }
-  const uint32_t o = (((uint32_t)(s0 >> tb) ^ 0x80) & 0xff) | ((((uint32_t)(s1 >> tb) ^ 0x80) & 0xff) << 8) |
-                     ((((uint32_t)(s2 >> tb) ^ 0x80) & 0xff) << 16) | ((((uint32_t)(s3 >> tb) ^ 0x80) & 0xff) << 24);
-  *reinterpret_cast<uint32_t*>(P + (size_t)b * C + c0) = o;
+  part[pg][4 * cl] = s0;
+  part[pg][4 * cl + 1] = s1;
+  part[pg][4 * cl + 2] = s2;
+  part[pg][4 * cl + 3] = s3;
+  __syncthreads();
+  if (threadIdx.x < 64) {
+    int t = 0;
+#pragma unroll
+    for (int g = 0; g < 16; ++g) t += part[g][threadIdx.x];
+    P[(size_t)b * C + c0 + threadIdx.x] = (int8_t)(uint8_t)(((uint32_t)(t >> tb) ^ 0x80) & 0xff);
+  }
 }
 
 // int8 / u8 codes -> fp32 (probes, dequantized feature export): y = (code) * scale
@@ -408,9 +416,8 @@ hipError_t launch_q_gemm(const QGemmArgs& a, hipStream_t s) {
 }
 
 hipError_t launch_q_pool(const uint8_t* x, int8_t* p, int B, int HW, int C, int tb, hipStream_t s) {
-  if (C & 3) return hipErrorInvalidValue;
-  const int n = B * (C >> 2);
-  q_pool_kernel<<<(n + 255) / 256, 256, 0, s>>>(x, p, B, HW, C, tb);
+  if (C & 63) return hipErrorInvalidValue;
+  q_pool_kernel<<<dim3(C / 64, B), 256, 0, s>>>(x, p, B, HW, C, tb);
   return hipGetLastError();
 }
 
