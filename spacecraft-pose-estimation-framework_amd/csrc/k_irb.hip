@@ -81,7 +81,8 @@ struct IrbGeom {
 };
 
 // ABL (timing ablations only, never dispatched by default): 1 = depthwise centre tap only, 2 = no expand
-// MFMA, 3 = no expand epilogue / slab store, 4 = no project MFMA. Results are wrong for ABL != 0.
+// MFMA, 3 = no expand epilogue / slab store, 4 = no project MFMA, 5 = no per-chunk barrier, 6 = no weight-staging
+// global loads, 7 = no depthwise-slab global loads. Results are wrong for ABL != 0.
 template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
           bool DBUF, bool STW, int ABL = 0>
 __global__ __launch_bounds__(NW * 64) void irb_kernel(
@@ -118,7 +119,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   constexpr int EPP = 16 / (int)sizeof(DW);      // weights per piece
   auto slab_load = [&](int cc) -> uint4 {
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (tid < G::SLAB_PIECES && cc < G::NCH) {
+    if (ABL != 7 && tid < G::SLAB_PIECES && cc < G::NCH) {
       const int f = tid * EPP, tap = f >> 5, ch = 32 * cc + (f & 31);
       if (ch < HID) v = *reinterpret_cast<const uint4*>(Wd + tap * HID + ch);
     }
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     if constexpr (STW) {
 #pragma unroll
       for (int i = 0; i < G::W_PPT; ++i) {
-        const int p = tid + NW * 64 * i;
+        const int p = ABL == 6 ? 1 << 30 : tid + NW * 64 * i;
         x8 v = zero8<DT>();
         if (p < G::WE_PIECES) {
           const int row = p / (G::WEK / 8), g = p - row * (G::WEK / 8);
@@ -321,7 +322,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       Es = Xs;
     }
     wst_store(c + 1, c);      // expand weights of chunk c+1, project weights of chunk c
-    __syncthreads();
+    if constexpr (ABL != 5) __syncthreads();
     wst_load(c + 2, c + 1);   // next stage in flight across this depthwise/project and the next expand
     if constexpr (STW) {
       const T* wpp = WPs + (c & 1) * G::NCTP * G::WPS + (wc * G::NCTW * 16 + r16) * G::WPS + 8 * kg;
@@ -520,7 +521,13 @@ template <typename DT>
   X(1, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(2, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
   X(3, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(4, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
   X(1, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) X(2, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) \
-  X(3, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) X(4, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false)
+  X(3, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) X(4, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) \
+  X(5, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(6, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
+  X(7, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(5, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) \
+  X(1, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) X(2, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) \
+  X(3, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) X(4, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) \
+  X(5, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) X(6, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) \
+  X(7, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true)
 
 static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stride, bool expand, bool res,
                                const void* x, const void* we, const float* be, const void* wd, const float* bd,
