@@ -43,10 +43,10 @@ def pmc_traffic(kernel_key: str, path: str):
     if kernel_key in kernels:
         return kernels[kernel_key]['hbm_bytes_per_launch']
     import re
-    m = re.fullmatch(r'irb_kernel<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
+    m = re.fullmatch(r'(ir[bsw]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
     if m:   # fused block key -> the one template instantiation profiled for that geometry
-        geo = ','.join(m.groups()) + ','
-        hits = [v for k, v in kernels.items() if re.match(r'irb_kernel<B?F16,' + re.escape(geo), k)]
+        geo = ','.join(m.groups()[1:]) + ','
+        hits = [v for k, v in kernels.items() if re.match(m.group(1) + r'<B?F16,' + re.escape(geo), k)]
     else:
         prefix = kernel_key.split('<')[0] + '<'
         hits = [v for k, v in kernels.items() if k.startswith(prefix)]

@@ -118,8 +118,19 @@ int spef_preprocess(spef_ctx* ctx, const uint8_t* frames, int B, int Hin, int Wi
 /* SPEF_OPT_FUSE_MIN_HW: fuse only blocks whose input has at least this many pixels per image (late,
  * low-resolution blocks then run as GEMM + depthwise + GEMM with the hidden tensor L2/MALL-resident).
  * SPEF_OPT_PW_GEMM (default 1): LDS-tiled MFMA GEMM for unfused 1x1 convs; 0 = register-direct kernel. */
-/* SPEF_OPT_IRB_VARIANT: fused-block tile variant (0 = tuned default; others for tuning sweeps). */
-enum spef_option { SPEF_OPT_FUSE_BLOCKS = 1, SPEF_OPT_FUSE_MIN_HW = 2, SPEF_OPT_PW_GEMM = 3, SPEF_OPT_IRB_VARIANT = 4 };
+/* SPEF_OPT_IRB_VARIANT: fused-block tile variant (0 = tuned default; others for tuning sweeps).
+ * SPEF_OPT_STRIP (default 0, experimental): register-streaming fused blocks for the high-resolution geometries; 0 = LDS-slab
+ * fused blocks everywhere.
+ * SPEF_OPT_WAVESPEC (default 1): wave-specialised fused blocks for the low-resolution geometries (expand waves
+ * and depthwise/project waves pipelined over hidden chunks); 0 = LDS-slab fused blocks. */
+enum spef_option {
+  SPEF_OPT_FUSE_BLOCKS = 1,
+  SPEF_OPT_FUSE_MIN_HW = 2,
+  SPEF_OPT_PW_GEMM = 3,
+  SPEF_OPT_IRB_VARIANT = 4,
+  SPEF_OPT_STRIP = 5,
+  SPEF_OPT_WAVESPEC = 6
+};
 int spef_set_option(spef_ctx* ctx, int option, int value);
 
 /* Per-launch HIP-event profiling of every kernel the context enqueues between begin and end (bench.py's

@@ -1,0 +1,411 @@
+// Wave-specialised fused InvertedResidual block (src/modeling/common/pytorch_layers.py:65-98) for the
+// low-resolution MobileNet-V2 blocks (32x32 and 16x16 maps, 384-960 hidden channels).
+//
+// The slab kernel (k_irb.hip) runs expand, barrier, depthwise+project on every wave in lock step: all waves of
+// a SIMD are in the MFMA-heavy expand or in the VALU-heavy depthwise at the same time, and at one workgroup per
+// CU (these blocks have 256 tiles for 256 CUs) nothing else fills the other pipe. Here the workgroup's waves
+// take fixed roles and form a two-stage pipeline over 32-channel hidden chunks:
+//
+//   expand waves  [0, NE):   chunk c+1: hidden = relu(x We^T + be) on MFMA -> LDS slab Es[(c+1) & 1]
+//   depthwise waves [NE, NW): chunk c:   3x3 depthwise (+BN, ReLU) from Es[c & 1] on VALU -> project MFMA
+//
+// with one barrier per chunk, so every SIMD holds one wave of each role and its matrix and vector pipes work
+// concurrently. The input tile (+halo), all depthwise weights and all biases are staged in LDS once; the expand
+// and project weight fragments stream from L2 into registers one chunk ahead (each role reads only its own).
+//
+// Arithmetic and rounding are those of the slab kernel (and of the unfused kernels): bias as the MFMA C input,
+// fp16/bf16 after expand, fp32 depthwise in kx-outer/ky-inner tap order, fp16/bf16 after the depthwise, fp32
+// project accumulation over chunks in order -> bit-identical to the one-kernel-per-conv schedule.
+#include "spef_common.hpp"
+#include "spef_kernels.hpp"
+
+namespace spef {
+
+template <int CIN, int HID, int COUT, int S, int TH, int TW, int NE, int ND, int WCO, int DWB>
+struct IrwGeom {
+  static constexpr int NW = NE + ND;
+  static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
+  static constexpr int PIN = IH * IW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
+  static constexpr int CINP = (CIN + 31) / 32 * 32;
+  static constexpr int KS = CINP / 32;
+  static constexpr int ES = 48;                   // 16-B granules per row = 2 mod 4: conflict-free b128 reads
+  static constexpr int HIDP_ = (HID + 31) / 32 * 32;
+  static constexpr int bytes_for(int xs) {
+    return (PINP * xs + 2 * PINP * ES) * 2 + 9 * HIDP_ * DWB + 2 * HIDP_ * 4;
+  }
+  static constexpr int XS = bytes_for(CINP + 16) <= 163840 ? CINP + 16 : CINP + 8;   // input row stride
+  static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
+  static constexpr int NCT = (COUT + 15) / 16;
+  static constexpr int EPT = (PIN16 + NE - 1) / NE;     // expand pixel tiles per expand wave
+  static constexpr int POUT16 = TH * TW / 16;
+  static constexpr int WP = ND / WCO;                   // pixel groups among the depthwise waves
+  static constexpr int QPW = POUT16 / WP;               // output pixel tiles per depthwise wave
+  static constexpr int NCTW = NCT / WCO;                // output-channel tiles per depthwise wave
+  static constexpr bool PAIR = S == 1 && TW == 16 && QPW % 2 == 0;
+  static constexpr int LDS_BYTES = bytes_for(XS);
+  static_assert(CIN % 32 == 0, "expand K is a whole number of 32-channel steps");
+  static_assert(HID % 16 == 0 && COUT % 16 == 0, "channel counts");
+  static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
+  static_assert(EPT <= 32, "validity mask is 32 bits");
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+};
+
+template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NE, int ND, int WCO>
+__global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
+    const typename DT::T* __restrict__ X, const typename DT::T* __restrict__ We, const float* __restrict__ be,
+    const typename DT::DW* __restrict__ Wd, const float* __restrict__ bd, const typename DT::T* __restrict__ Wp,
+    const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
+    int tiles_y, uint32_t nwg) {
+  using DW = typename DT::DW;
+  using G = IrwGeom<CIN, HID, COUT, S, TH, TW, NE, ND, WCO, (int)sizeof(DW)>;
+  using T = typename DT::T;
+  using x8 = typename DT::x8;
+  using x4 = typename DT::x4;
+  constexpr int NW = G::NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  T* Xs = reinterpret_cast<T*>(smem);                          // [PINP][XS] input tile (+halo)
+  T* Es0 = Xs + G::PINP * G::XS;                               // [2][PINP][ES] hidden chunk slabs
+  DW* Wds = reinterpret_cast<DW*>(Es0 + 2 * G::PINP * G::ES);  // [9][HIDP] depthwise weights (0 past HID)
+  float* Be = reinterpret_cast<float*>(Wds + 9 * G::HIDP);     // [HIDP] expand bias
+  float* Bd = Be + G::HIDP;                                    // [HIDP] depthwise bias
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int tx = (int)(L % (uint32_t)tiles_x);
+  L /= (uint32_t)tiles_x;
+  const int ty = (int)(L % (uint32_t)tiles_y);
+  const int b = (int)(L / (uint32_t)tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+
+  // ---- 1. input tile, depthwise weights and biases -> LDS (16-B pieces, all loads before the stores)
+  {
+    constexpr int GPR = G::CINP / 8;
+    constexpr int NXP = G::PINP * GPR;
+    constexpr int EPP = 16 / (int)sizeof(DW);
+    constexpr int DPR = G::HIDP / EPP;                 // depthwise pieces per tap
+    constexpr int NDP = 9 * DPR;
+    constexpr int NBP = G::HIDP / 4;
+    constexpr int NTOT = NXP + NDP + 2 * NBP;
+    constexpr int NIT = (NTOT + NW * 64 - 1) / (NW * 64);
+    const T* Xb = X + (size_t)b * H * W * CIN;
+    uint4 v[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      int u = tid + NW * 64 * i;
+      const void* src = nullptr;
+      if (u < NXP) {
+        const int p = u / GPR, g = u - p * GPR;
+        if (p < G::PIN) {
+          const int py = p / G::IW, px = p - py * G::IW;
+          const int iy = iy0 + py, ix = ix0 + px;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + ((size_t)iy * W + ix) * CIN + g * 8;
+        }
+      } else if ((u -= NXP) < NDP) {
+        const int tap = u / DPR, g = u - tap * DPR;
+        if (g * EPP < HID) src = Wd + (size_t)tap * HID + g * EPP;
+      } else if ((u -= NDP) < 2 * NBP) {
+        const int which = u / NBP, g = u - which * NBP;
+        if (4 * g < HID) src = (which ? bd : be) + 4 * g;
+      }
+      v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      int u = tid + NW * 64 * i;
+      char* dst = nullptr;
+      if (u < NXP) {
+        const int p = u / GPR, g = u - p * GPR;
+        dst = reinterpret_cast<char*>(Xs + p * G::XS + g * 8);
+      } else if ((u -= NXP) < NDP) {
+        const int tap = u / DPR, g = u - tap * DPR;
+        dst = reinterpret_cast<char*>(Wds + tap * G::HIDP + g * EPP);
+      } else if ((u -= NDP) < 2 * NBP) {
+        const int which = u / NBP, g = u - which * NBP;
+        dst = reinterpret_cast<char*>((which ? Bd : Be) + 4 * g);
+      }
+      if (dst) *reinterpret_cast<uint4*>(dst) = v[i];
+    }
+  }
+
+  const bool is_expand = wave < NE;   // wave-uniform role
+
+  // ---- expand role state: weight fragments of the next chunk (prefetched from L2), pixel validity
+  const int ew = wave;                                   // expand wave index (valid when is_expand)
+  const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + G::IH <= H && ix0 + G::IW <= W;
+  uint32_t pvmask = 0;
+  x8 ea0[G::KS], ea1[G::KS];                             // expand A fragments of the chunk being produced
+  auto load_ea = [&](int c) {
+#pragma unroll
+    for (int ks = 0; ks < G::KS; ++ks) {
+      const T* w0 = We + (size_t)(32 * c + r16) * G::CINP + 32 * ks + 8 * kg;
+      ea0[ks] = c < G::NCH ? load8<DT>(w0) : zero8<DT>();
+      ea1[ks] = c < G::NCH && 32 * c + 16 < HID ? load8<DT>(w0 + 16 * G::CINP) : zero8<DT>();
+    }
+  };
+  // expand of chunk c into slab Es[c & 1] by this expand wave
+  auto expand = [&](int c) {
+    T* Ew = Es0 + (c & 1) * G::PINP * G::ES;
+    const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
+    const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
+#pragma unroll
+    for (int jj = 0; jj < G::EPT; ++jj) {
+      const int pt = ew + NE * jj;
+      if (pt >= G::PIN16) break;
+      f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
+      const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
+#pragma unroll
+      for (int ks = 0; ks < G::KS; ++ks) {
+        const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
+        e0 = DT::mfma(ea0[ks], bx, e0);
+        e1 = DT::mfma(ea1[ks], bx, e1);
+      }
+      x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);
+      uint2 u0 = *reinterpret_cast<uint2*>(&o0), u1 = *reinterpret_cast<uint2*>(&o1);
+      if (!interior) {   // the depthwise zero padding: hidden values of pixels outside the image are 0
+        const uint32_t m0 = ((pvmask >> jj) & 1u) ? 0xffffffffu : 0u;
+        u0.x &= m0; u0.y &= m0; u1.x &= m0; u1.y &= m0;
+      }
+      T* er = Ew + (pt * 16 + r16) * G::ES + 4 * kg;
+      *reinterpret_cast<uint2*>(er) = u0;
+      *reinterpret_cast<uint2*>(er + 16) = u1;
+    }
+  };
+
+  // ---- depthwise role state
+  const int dwv = wave - NE;                             // depthwise wave index (valid when !is_expand)
+  const int wp = dwv % G::WP, wc = dwv / G::WP;
+  int oyq[G::QPW], oxq[G::QPW];
+#pragma unroll
+  for (int qi = 0; qi < G::QPW; ++qi) {
+    const int o = (wp * G::QPW + qi) * 16 + r16;
+    oyq[qi] = o / TW;
+    oxq[qi] = o - oyq[qi] * TW;
+  }
+  f32x4 acc[G::QPW][G::NCTW];
+  x8 pa[G::NCTW];                                        // project A fragments of the chunk being consumed
+  auto load_pa = [&](int c) {
+    const T* wpp = Wp + (size_t)(wc * G::NCTW * 16 + r16) * G::HIDP + 32 * c + 8 * kg;
+#pragma unroll
+    for (int t = 0; t < G::NCTW; ++t) pa[t] = c < G::NCH ? load8<DT>(wpp + (size_t)t * 16 * G::HIDP) : zero8<DT>();
+  };
+
+  // The two roles run separate loops with the same barrier count (2 + NCH), so each role's registers (the
+  // project accumulators, the expand fragments) are allocated independently.
+  if (is_expand) {
+#pragma unroll
+    for (int jj = 0; jj < G::EPT; ++jj) {
+      const int p = (ew + NE * jj) * 16 + r16;
+      if (p < G::PIN) {
+        const int py = p / G::IW, px = p - py * G::IW;
+        const int iy = iy0 + py, ix = ix0 + px;
+        if (iy >= 0 && iy < H && ix >= 0 && ix < W) pvmask |= 1u << jj;
+      }
+    }
+    load_ea(0);
+    __syncthreads();                                      // input tile, depthwise weights, biases visible
+    expand(0);
+    load_ea(1);
+    __syncthreads();                                      // Es[0] visible
+#pragma unroll 1
+    for (int c = 0; c < G::NCH; ++c) {
+      if (c + 1 < G::NCH) {
+        expand(c + 1);          // into Es[(c+1) & 1]: last read by the depthwise of chunk c-1, before the barrier
+        load_ea(c + 2);
+      }
+      __syncthreads();          // Es[(c+1) & 1] complete; Es[c & 1] free for chunk c+2
+    }
+  } else {
+#pragma unroll
+    for (int t = 0; t < G::NCTW; ++t) {
+      const float4 bb = *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg);
+#pragma unroll
+      for (int qi = 0; qi < G::QPW; ++qi) acc[qi][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
+    }
+    load_pa(0);
+    __syncthreads();
+    __syncthreads();
+#pragma unroll 1
+    for (int c = 0; c < G::NCH; ++c) {
+      const T* Es = Es0 + (c & 1) * G::PINP * G::ES;
+      const DW* sl = Wds + 32 * c;                        // tap t of chunk c: sl[t * HIDP + ch]
+      const bool hv = 32 * c + 8 * kg < HID;
+      x8 pn[G::NCTW];
+      // next chunk's project fragments: issued now, consumed after this chunk's MFMAs
+      {
+        const T* wpp = Wp + (size_t)(wc * G::NCTW * 16 + r16) * G::HIDP + 32 * (c + 1) + 8 * kg;
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t)
+          pn[t] = c + 1 < G::NCH ? load8<DT>(wpp + (size_t)t * 16 * G::HIDP) : zero8<DT>();
+      }
+      float db[8];
+      {
+        const float4 u0 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg);
+        const float4 u1 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg + 4);
+        db[0] = u0.x; db[1] = u0.y; db[2] = u0.z; db[3] = u0.w;
+        db[4] = u1.x; db[5] = u1.y; db[6] = u1.z; db[7] = u1.w;
+      }
+      if constexpr (G::PAIR) {
+#pragma unroll
+        for (int qi = 0; qi < G::QPW; qi += 2) {
+          x8 bf0 = zero8<DT>(), bf1 = zero8<DT>();
+          if (hv) {
+            float a0[8], a1[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a0[e] = a1[e] = db[e];
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              DW8<DT> w[3];
+#pragma unroll
+              for (int ky = 0; ky < 3; ++ky) w[ky].load(sl + (ky * 3 + kx) * G::HIDP + 8 * kg);
+              x8 v[4];
+#pragma unroll
+              for (int r = 0; r < 4; ++r)
+                v[r] = *reinterpret_cast<const x8*>(Es + ((oyq[qi] + r) * G::IW + oxq[qi] + kx) * G::ES + 8 * kg);
+#pragma unroll
+              for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  a0[e] = fmaf((float)v[ky][e], w[ky][e], a0[e]);
+                  a1[e] = fmaf((float)v[ky + 1][e], w[ky][e], a1[e]);
+                }
+            }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              bf0[e] = (T)fmaxf(a0[e], 0.f);
+              bf1[e] = (T)fmaxf(a1[e], 0.f);
+            }
+          }
+#pragma unroll
+          for (int t = 0; t < G::NCTW; ++t) {
+            acc[qi][t] = DT::mfma(pa[t], bf0, acc[qi][t]);
+            acc[qi + 1][t] = DT::mfma(pa[t], bf1, acc[qi + 1][t]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int qi = 0; qi < G::QPW; ++qi) {
+          x8 bf = zero8<DT>();
+          if (hv) {
+            float a8[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a8[e] = db[e];
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+              for (int ky = 0; ky < 3; ++ky) {
+                const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
+                const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + 8 * kg);
+                DW8<DT> wt;
+                wt.load(sl + (ky * 3 + kx) * G::HIDP + 8 * kg);
+#pragma unroll
+                for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wt[e], a8[e]);
+              }
+#pragma unroll
+            for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
+          }
+#pragma unroll
+          for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
+        }
+      }
+#pragma unroll
+      for (int t = 0; t < G::NCTW; ++t) pa[t] = pn[t];
+      __syncthreads();
+    }
+  }
+
+  // ---- epilogue (depthwise waves): + residual from the staged input tile -> y (NHWC)
+  if (!is_expand) {
+#pragma unroll
+    for (int qi = 0; qi < G::QPW; ++qi) {
+      const int oy = oyq[qi], ox = oxq[qi];
+      const int gy = oy0 + oy, gx = ox0 + ox;
+      if (gy >= OH || gx >= OW) continue;
+      T* yr = Y + (((size_t)b * OH + gy) * OW + gx) * COUT;
+#pragma unroll
+      for (int t = 0; t < G::NCTW; ++t) {
+        const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
+        f32x4 v = acc[qi][t];
+        if constexpr (RES) {
+          const x4 r = *reinterpret_cast<const x4*>(Xs + ((oy + 1) * G::IW + (ox + 1)) * G::XS + co);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) v[e] += (float)r[e];
+        }
+        x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = (T)v[e];
+        *reinterpret_cast<x4*>(yr + co) = o;
+      }
+    }
+  }
+}
+
+// (variant, cin, hidden, cout, stride, TH x TW tile, residual, expand waves, depthwise waves, cout groups).
+// Variant 0 is the default; others are alternatives for tuning sweeps (SPEF_OPT_IRB_VARIANT).
+#define SPEF_IRW_TABLE(X)                                                   \
+  X(0, 64, 384, 64, 1, 16, 16, true, 4, 8, 1)      /* blocks 8-10  */       \
+  X(1, 64, 384, 64, 1, 16, 16, true, 4, 4, 1)                               \
+  X(0, 64, 384, 96, 1, 16, 16, false, 4, 8, 1)     /* block 11     */       \
+  X(1, 64, 384, 96, 1, 16, 16, false, 4, 4, 1)                              \
+  X(0, 96, 576, 96, 1, 16, 16, true, 4, 8, 1)      /* blocks 12-13 */       \
+  X(1, 96, 576, 96, 1, 16, 16, true, 4, 4, 1)                               \
+  X(0, 96, 576, 160, 2, 8, 8, false, 4, 4, 2)      /* block 14     */       \
+  X(1, 96, 576, 160, 2, 8, 8, false, 4, 8, 2)                               \
+  X(0, 160, 960, 160, 1, 8, 8, true, 4, 4, 2)      /* blocks 15-16 */       \
+  X(1, 160, 960, 160, 1, 8, 8, true, 4, 8, 2)
+// Block 17 (160 -> 960 -> 320) stays on the slab kernel: with 20 output-channel tiles the depthwise waves carry
+// too many accumulators (measured 72-80 us here vs 61 us slab).
+
+template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NE, int ND, int WCO>
+static hipError_t irw_go(const void* x, const void* we, const float* be, const void* wd, const float* bd,
+                         const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
+  using DW = typename DT::DW;
+  using T = typename DT::T;
+  using G = IrwGeom<CIN, HID, COUT, S, TH, TW, NE, ND, WCO, (int)sizeof(DW)>;
+  const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
+  const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
+  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+  const uint32_t nwg = (uint32_t)nwg64;
+  const size_t lds = (size_t)G::LDS_BYTES;
+  auto k = irw_kernel<DT, CIN, HID, COUT, S, TH, TW, RES, NE, ND, WCO>;
+  static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
+  if (!attr_set && lds > 65536) {
+    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  k<<<nwg, G::NW * 64, lds, s>>>((const T*)x, (const T*)we, be, (const DW*)wd, bd, (const T*)wp, bp, (T*)y, H, W, OH,
+                                 OW, tiles_x, tiles_y, nwg);
+  return hipGetLastError();
+}
+
+static bool irw_has(int variant, int cin, int hid, int cout, int stride, bool expand, bool res) {
+#define SPEF_IRW_HAS(V, CI, HI, CO, ST, TH_, TW_, RS, NE_, ND_, WC_) \
+  if (variant == V && cin == CI && hid == HI && cout == CO && stride == ST && expand && res == RS) return true;
+  SPEF_IRW_TABLE(SPEF_IRW_HAS)
+#undef SPEF_IRW_HAS
+  return false;
+}
+
+bool irw_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
+  return irw_has(0, cin, hid, cout, stride, expand, res);
+}
+
+hipError_t launch_irw(int variant, int dtype, int cin, int hid, int cout, int stride, bool res, const void* x,
+                      const void* we, const float* be, const void* wd, const float* bd, const void* wp, const float* bp,
+                      void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
+  if (dtype != DT_F16 || !irw_has(variant, cin, hid, cout, stride, true, res)) variant = 0;
+#define SPEF_IRW_CASE(V, CI, HI, CO, ST, TH_, TW_, RS, NE_, ND_, WC_)                                               \
+  if (variant == V && cin == CI && hid == HI && cout == CO && stride == ST && res == RS)                            \
+    return dtype == DT_F16                                                                                          \
+               ? irw_go<F16, CI, HI, CO, ST, TH_, TW_, RS, NE_, ND_, WC_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
+                                                                        OW, s)                                     \
+               : irw_go<BF16, CI, HI, CO, ST, TH_, TW_, RS, NE_, ND_, WC_>(x, we, be, wd, bd, wp, bp, y, B, H, W,   \
+                                                                         OH, OW, s);
+  SPEF_IRW_TABLE(SPEF_IRW_CASE)
+#undef SPEF_IRW_CASE
+  return hipErrorNotSupported;
+}
+
+}  // namespace spef

@@ -28,7 +28,10 @@ CXXFLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-Wall', '-W
 # Convolution kernels never see NaN (finite frames, finite folded weights): dropping NaN semantics lets the
 # compiler emit a single v_max_f32 per ReLU instead of canonicalize + max (~18 % fewer VALU ops in the fused
 # block loop). Decode / EPnP keep IEEE NaN semantics (they detect NaNs, classification_utils.py:134).
-NO_NAN_SOURCES = {'k_irb.hip', 'k_front.hip', 'k_conv.hip', 'k_gemm.hip', 'k_pool.hip'}
+NO_NAN_SOURCES = {'k_irb.hip', 'k_irs.hip', 'k_front.hip', 'k_conv.hip', 'k_gemm.hip', 'k_pool.hip'}
+# The SLP vectorizer packs the strip kernel's independent depthwise FMAs into v_pk_fma_f32 with explicit fp16->fp32
+# converts; scalar v_fma_mix_f32 (fp16 weight operand read in place) is fewer instructions.
+NO_SLP_SOURCES = {'k_irs.hip'}
 
 
 def lib_path() -> str:
@@ -44,8 +47,9 @@ def _headers():
 
 
 def _compile(src: str, verbose: bool) -> str:
-    extra = ['-fno-honor-nans'] if os.path.basename(src) in NO_NAN_SOURCES else []
-    obj = os.path.join(OBJDIR, os.path.basename(src) + ('.nn' if extra else '') + '.o')
+    base = os.path.basename(src)
+    extra = (['-fno-honor-nans'] if base in NO_NAN_SOURCES else []) + (['-fno-slp-vectorize'] if base in NO_SLP_SOURCES else [])
+    obj = os.path.join(OBJDIR, base + ('.nn' if extra else '') + '.o')
     newest_dep = max([os.path.getmtime(src)] + [os.path.getmtime(h) for h in _headers()])
     if os.path.exists(obj) and os.path.getmtime(obj) >= newest_dep:
         return obj

@@ -12,7 +12,7 @@ from . import _build
 OK, ERR_ARG, ERR_HIP, ERR_BLOB, ERR_STATE, ERR_NUMERIC = range(6)
 IN_U8_NHWC, IN_F32_NCHW = 0, 1
 REGRESSION, CLASSIFICATION, KEYPOINTS = 0, 1, 2
-OPT_FUSE_BLOCKS, OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT = 1, 2, 3, 4
+OPT_FUSE_BLOCKS, OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT, OPT_STRIP, OPT_WAVESPEC = 1, 2, 3, 4, 5, 6
 
 # name -> (restype, argtypes); keep in sync with include/spef.h (tests/test_abi.py checks the header)
 _vp, _i, _sz = C.c_void_p, C.c_int, C.c_size_t

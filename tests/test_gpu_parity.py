@@ -208,3 +208,36 @@ def test_front_kernel_vs_stem_block1(engine, sd, b, h, w):
     scale = np.abs(ref).max()
     assert np.abs(got - sep).max() / scale < 4e-3
     assert np.abs(got - ref).max() / scale < 4e-3
+
+
+@pytest.mark.parametrize('b,h,w', [(2, 512, 512), (2, 100, 136)])
+def test_wave_specialised_blocks_bit_identical_to_slab(engine, b, h, w):
+    """k_irw.hip (expand waves pipelined against depthwise/project waves) keeps the slab kernel's rounding points
+    and accumulation order: every late-block output is bit-identical with SPEF_OPT_WAVESPEC on and off."""
+    from spef_amd import _lib as L
+    fr = torch.from_numpy(_frames(b, h, w, 31 + w)).cuda()
+    try:
+        for op in range(8, 18):
+            engine.set_option(L.OPT_WAVESPEC, 0)
+            u = engine.probe(fr, op).cpu().numpy()
+            engine.set_option(L.OPT_WAVESPEC, 1)
+            f = engine.probe(fr, op).cpu().numpy()
+            assert np.array_equal(u, f), (op, np.abs(u.astype(np.float32) - f.astype(np.float32)).max())
+    finally:
+        engine.set_option(L.OPT_WAVESPEC, 1)
+
+
+@pytest.mark.parametrize('b,h,w', [(2, 512, 512), (3, 240, 384)])
+def test_strip_blocks_vs_oracle(engine, sd, b, h, w):
+    """Experimental register-streaming blocks (k_irs.hip, SPEF_OPT_STRIP=1) keep the expand output in fp32 and
+    permute the project's K order, so they are compared with the FP32 oracle at the logit tolerance."""
+    from spef_amd import _lib as L
+    fr = _frames(b, h, w, 5 + h)
+    try:
+        engine.set_option(L.OPT_STRIP, 1)
+        ori, pos = engine.forward(torch.from_numpy(fr).cuda())
+    finally:
+        engine.set_option(L.OPT_STRIP, 0)
+    ro, rp = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd)
+    assert float((ori.cpu() - ro).abs().max()) < 1e-3
+    assert float((pos.cpu() - rp).abs().max()) < 1e-3
