@@ -478,26 +478,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   X(0, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true)      /* blocks 15-16 */ \
   X(2, 160, 960, 160, 1, 4, 8, true, true, 4, 2, true, true)                       \
   X(0, 160, 960, 320, 1, 8, 8, true, false, 8, 2, false, true)    /* block 17     */ \
-  X(2, 160, 960, 320, 1, 4, 8, true, false, 4, 2, true, true)                       \
-  X(4, 64, 384, 64, 1, 8, 8, true, true, 4, 1, true, false)                          \
-  X(5, 64, 384, 64, 1, 8, 8, true, true, 4, 1, true, true)                           \
-  X(6, 64, 384, 64, 1, 8, 16, true, true, 8, 1, false, false)                        \
-  X(7, 64, 384, 64, 1, 8, 8, true, true, 8, 2, true, false)                          \
-  X(4, 64, 384, 96, 1, 8, 8, true, false, 4, 1, true, false)                         \
-  X(6, 64, 384, 96, 1, 8, 16, true, false, 8, 1, false, false)                       \
-  X(7, 64, 384, 96, 1, 8, 8, true, false, 8, 2, true, false)                         \
-  X(4, 96, 576, 96, 1, 8, 8, true, true, 4, 1, true, false)                          \
-  X(5, 96, 576, 96, 1, 8, 8, true, true, 4, 1, true, true)                           \
-  X(6, 96, 576, 96, 1, 8, 16, true, true, 8, 1, false, false)                        \
-  X(7, 96, 576, 96, 1, 8, 8, true, true, 8, 2, true, false)                          \
-  X(4, 96, 576, 160, 2, 4, 8, true, false, 4, 2, true, false)                        \
-  X(6, 96, 576, 160, 2, 8, 8, true, false, 4, 1, true, false)                        \
-  X(4, 160, 960, 160, 1, 4, 8, true, true, 4, 2, true, false)                        \
-  X(5, 160, 960, 160, 1, 8, 8, true, true, 4, 1, true, false)                        \
-  X(6, 160, 960, 160, 1, 8, 8, true, true, 4, 1, true, true)                         \
-  X(4, 160, 960, 320, 1, 4, 8, true, false, 4, 2, true, false)                       \
-  X(5, 160, 960, 320, 1, 8, 8, true, false, 4, 1, true, false)                       \
-  X(6, 160, 960, 320, 1, 8, 8, true, false, 8, 4, true, false)
+  X(2, 160, 960, 320, 1, 4, 8, true, false, 4, 2, true, true)
 
 template <typename DT, int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO,
           bool DBUF, bool STW, int ABL = 0>
@@ -542,11 +523,7 @@ template <typename DT>
   X(1, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) X(2, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) \
   X(3, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) X(4, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false) \
   X(5, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(6, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
-  X(7, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(5, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) \
-  X(1, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) X(2, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) \
-  X(3, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) X(4, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) \
-  X(5, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) X(6, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true) \
-  X(7, 160, 960, 160, 1, 8, 8, true, true, 8, 2, true, true)
+  X(7, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(5, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false)
 
 static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stride, bool expand, bool res,
                                const void* x, const void* we, const float* be, const void* wd, const float* bd,

@@ -1,5 +1,5 @@
 // Wave-specialised fused InvertedResidual block (src/modeling/common/pytorch_layers.py:65-98) for the
-// low-resolution MobileNet-V2 blocks (32x32 and 16x16 maps, 384-960 hidden channels).
+// mid- and low-resolution MobileNet-V2 blocks (64x64 down to 16x16 maps, 192-960 hidden channels).
 //
 // The slab kernel (k_irb.hip) runs expand, barrier, depthwise+project on every wave in lock step: all waves of
 // a SIMD are in the MFMA-heavy expand or in the VALU-heavy depthwise at the same time, and at one workgroup per
@@ -26,8 +26,10 @@ struct IrwGeom {
   static constexpr int NW = NE + ND;
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
-  static constexpr int CINP = (CIN + 31) / 32 * 32;
-  static constexpr int KS = CINP / 32;
+  static constexpr bool K16 = CIN == 16;          // 16-channel input: K = 16 MFMA
+  static constexpr int CINP = K16 ? 16 : (CIN + 31) / 32 * 32;
+  static constexpr int KS = K16 ? 1 : CINP / 32;
+  static constexpr int WKP = (CIN + 31) / 32 * 32;   // blob row length of the expand weights
   static constexpr int ES = 48;                   // 16-B granules per row = 2 mod 4: conflict-free b128 reads
   static constexpr int HIDP_ = (HID + 31) / 32 * 32;
   static constexpr int bytes_for(int xs) {
@@ -43,8 +45,7 @@ struct IrwGeom {
   static constexpr int NCTW = NCT / WCO;                // output-channel tiles per depthwise wave
   static constexpr bool PAIR = S == 1 && TW == 16 && QPW % 2 == 0;
   static constexpr int LDS_BYTES = bytes_for(XS);
-  static_assert(CIN % 32 == 0, "expand K is a whole number of 32-channel steps");
-  static_assert(HID % 16 == 0 && COUT % 16 == 0, "channel counts");
+  static_assert(CIN % 8 == 0 && HID % 16 == 0 && COUT % 8 == 0, "channel counts");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
   static_assert(EPT <= 32, "validity mask is 32 bits");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -81,7 +82,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 
   // ---- 1. input tile, depthwise weights and biases -> LDS (16-B pieces, all loads before the stores)
   {
-    constexpr int GPR = G::CINP / 8;
+    constexpr int GPR = G::CINP / 8, CG = CIN / 8;
     constexpr int NXP = G::PINP * GPR;
     constexpr int EPP = 16 / (int)sizeof(DW);
     constexpr int DPR = G::HIDP / EPP;                 // depthwise pieces per tap
@@ -97,7 +98,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       const void* src = nullptr;
       if (u < NXP) {
         const int p = u / GPR, g = u - p * GPR;
-        if (p < G::PIN) {
+        if (p < G::PIN && g < CG) {
           const int py = p / G::IW, px = p - py * G::IW;
           const int iy = iy0 + py, ix = ix0 + px;
           if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + ((size_t)iy * W + ix) * CIN + g * 8;
@@ -136,12 +137,20 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + G::IH <= H && ix0 + G::IW <= W;
   uint32_t pvmask = 0;
   x8 ea0[G::KS], ea1[G::KS];                             // expand A fragments of the chunk being produced
+  x4 eq0, eq1;                                           // (16-channel input: K = 16 fragments)
   auto load_ea = [&](int c) {
+    const bool ok0 = c < G::NCH, ok1 = ok0 && 32 * c + 16 < HID;
+    if constexpr (G::K16) {
+      const T* w0 = We + (size_t)(32 * c + r16) * G::WKP + 4 * kg;
+      eq0 = ok0 ? *reinterpret_cast<const x4*>(w0) : x4{};
+      eq1 = ok1 ? *reinterpret_cast<const x4*>(w0 + 16 * G::WKP) : x4{};
+    } else {
 #pragma unroll
-    for (int ks = 0; ks < G::KS; ++ks) {
-      const T* w0 = We + (size_t)(32 * c + r16) * G::CINP + 32 * ks + 8 * kg;
-      ea0[ks] = c < G::NCH ? load8<DT>(w0) : zero8<DT>();
-      ea1[ks] = c < G::NCH && 32 * c + 16 < HID ? load8<DT>(w0 + 16 * G::CINP) : zero8<DT>();
+      for (int ks = 0; ks < G::KS; ++ks) {
+        const T* w0 = We + (size_t)(32 * c + r16) * G::WKP + 32 * ks + 8 * kg;
+        ea0[ks] = ok0 ? load8<DT>(w0) : zero8<DT>();
+        ea1[ks] = ok1 ? load8<DT>(w0 + 16 * G::WKP) : zero8<DT>();
+      }
     }
   };
   // expand of chunk c into slab Es[c & 1] by this expand wave
@@ -154,12 +163,18 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       const int pt = ew + NE * jj;
       if (pt >= G::PIN16) break;
       f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
-      const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
+      if constexpr (G::K16) {
+        const x4 bx = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
+        e0 = DT::mfma16(eq0, bx, e0);
+        e1 = DT::mfma16(eq1, bx, e1);
+      } else {
+        const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
 #pragma unroll
-      for (int ks = 0; ks < G::KS; ++ks) {
-        const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
-        e0 = DT::mfma(ea0[ks], bx, e0);
-        e1 = DT::mfma(ea1[ks], bx, e1);
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
+          e0 = DT::mfma(ea0[ks], bx, e0);
+          e1 = DT::mfma(ea1[ks], bx, e1);
+        }
       }
       x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);
       uint2 u0 = *reinterpret_cast<uint2*>(&o0), u1 = *reinterpret_cast<uint2*>(&o1);
@@ -326,6 +341,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) {
         const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
+        if (co >= COUT) continue;
         f32x4 v = acc[qi][t];
         if constexpr (RES) {
           const x4 r = *reinterpret_cast<const x4*>(Xs + ((oy + 1) * G::IW + (ox + 1)) * G::XS + co);
@@ -344,6 +360,8 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 // (variant, cin, hidden, cout, stride, TH x TW tile, residual, expand waves, depthwise waves, cout groups).
 // Variant 0 is the default; others are alternatives for tuning sweeps (SPEF_OPT_IRB_VARIANT).
 #define SPEF_IRW_TABLE(X)                                                   \
+  X(0, 32, 192, 32, 1, 8, 16, true, 4, 4, 1)       /* blocks 5-6   */       \
+  X(1, 32, 192, 32, 1, 8, 16, true, 2, 4, 1)                                \
   X(0, 64, 384, 64, 1, 16, 16, true, 4, 8, 1)      /* blocks 8-10  */       \
   X(1, 64, 384, 64, 1, 16, 16, true, 4, 4, 1)                               \
   X(0, 64, 384, 96, 1, 16, 16, false, 4, 8, 1)     /* block 11     */       \
@@ -354,6 +372,8 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   X(1, 96, 576, 160, 2, 8, 8, false, 4, 8, 2)                               \
   X(0, 160, 960, 160, 1, 8, 8, true, 4, 4, 2)      /* blocks 15-16 */       \
   X(1, 160, 960, 160, 1, 8, 8, true, 4, 8, 2)
+// Blocks 2-4 stay on the slab kernel (measured: the wave-specialised form is 0-70 % slower there -- the stride-2
+// input tiles make the double-buffered slab too large for more than one or two workgroups per CU).
 // Block 17 (160 -> 960 -> 320) stays on the slab kernel: with 20 output-channel tiles the depthwise waves carry
 // too many accumulators (measured 72-80 us here vs 61 us slab).
 
