@@ -4,7 +4,9 @@ A "step" = one pass of the hot path over one batch: uint8 NHWC frames already re
 MobileNet-V2 backbone -> URSONet head -> on-device decode (softmax + Markley orientation average, position
 regression), i.e. SPEMi355x.predict minus the host copies. Weights: seeded synthetic (spef_amd.weights),
 BN folded, fp16 storage / fp32 accumulate. Frames: synthetic SPEED-style (dark background + noise + bright
-target), generated once per rank from (seed, global frame index).
+target), generated once per rank from (seed, global frame index). Consecutive steps alternate over --inflight
+HIP streams (spef_amd.pipeline.StreamPipeline, default 3 batches in flight): every step is still the complete
+forward + decode of its batch, but one batch's low-occupancy tail overlaps the next batch's front kernels.
 
 Multi-GPU (python -m torch.distributed.run --nproc-per-node N bench.py --gpus N): one process per GPU,
 rank 0 packs the weight blob and RCCL-broadcasts it (torch.distributed 'nccl' = RCCL over xGMI); every rank
@@ -105,6 +107,8 @@ def main():
     ap.add_argument('--size', type=int, default=512)
     ap.add_argument('--dtype', default='fp16', choices=['fp16', 'bf16', 'int8'],
                     help='int8 = the Brevitas-mirroring C5 path (calibrated activation scales)')
+    ap.add_argument('--inflight', type=int, default=3,
+                    help='batches in flight: consecutive steps alternate over this many HIP streams (spef_amd.pipeline)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--cpu-batch', type=int, default=64)
@@ -129,7 +133,8 @@ def main():
 
     from spef_amd import blob as Bl
     from spef_amd.arch import flops_per_image, mobilenet_v2
-    from spef_amd.engine import Engine
+    from spef_amd import _lib as L
+    from spef_amd.pipeline import StreamPipeline
     from spef_amd.shard import broadcast_blob, max_over_ranks, shard_range
     from spef_amd.spe.spe_utils import SPEUtils
     from spef_amd.weights import synthetic_state_dict
@@ -145,23 +150,27 @@ def main():
         else:
             blob = Bl.pack(sd, dtype=args.dtype)
     dblob = broadcast_blob(blob, dev)                 # RCCL over xGMI
-    eng = Engine(dblob, dev)
     su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
-    eng.set_decode_tables(su.orientation.histogram, None)
+    pipe = StreamPipeline(dblob, dev, depth=max(1, args.inflight), ori_bins=su.orientation.histogram)
+    eng = pipe.engine
 
     B, S = args.batch, args.size
     first, stop = shard_range(B * world, rank, world)          # this rank's global frame indices
     frames = torch.from_numpy(synth_frames(stop - first, S, S, first)).to(dev)
-    eng.reserve(B, S, S)
+    pipe.reserve(B, S, S)
     ori = torch.empty((B, eng.n_out0), dtype=torch.float32, device=dev)
     pos = torch.empty((B, eng.n_out1), dtype=torch.float32, device=dev)
 
-    def step():
+    def step():   # one batch: forward + decode, on the next of --inflight streams
+        return pipe.submit(frames, L.CLASSIFICATION, L.REGRESSION, want_soft=True)
+
+    def step_single():   # the same work on one stream (the per-kernel HIP-event leg)
         eng.forward(frames, ori, pos)
         return eng.decode(1, 0, ori, pos, want_soft=True)
 
     for _ in range(args.warmup):
         step()
+    pipe.synchronize()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -169,6 +178,7 @@ def main():
     t0 = time.perf_counter()
     for _ in range(args.steps):
         out = step()
+    pipe.synchronize()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
@@ -180,7 +190,7 @@ def main():
     # roofline leg: per-kernel HIP events on the engine's stream, K more steps
     eng.profile_begin()
     for _ in range(args.steps):
-        step()
+        step_single()
     prof = eng.profile_end()
 
     if rank == 0:
@@ -212,7 +222,8 @@ def main():
             'config': {'workload': (f'C5: INT8 (Brevitas-mirroring, calibrated scales) full net + decode, {S}x{S}, '
                                     f'batch {B} per GPU' if args.dtype == 'int8' else
                                     f'C3: full net + decode, {S}x{S}, batch {B} per GPU'), 'global_batch': B * world,
-                       'image_size': S, 'parallelism': f'frame-parallel x{world} (RCCL weight bcast)'},
+                       'image_size': S, 'parallelism': f'frame-parallel x{world} (RCCL weight bcast)',
+                       'inflight_batches': max(1, args.inflight)},
             'roofline': {'bound': 'hbm', 'kernel': dom_key, 'achieved': round(ach_gbs, 1), 'peak': HBM_PEAK_GBS,
                          'unit': 'GB/s', 'frac': round(ach_gbs / HBM_PEAK_GBS, 4),
                          'traffic': None if traffic is None else round(traffic),

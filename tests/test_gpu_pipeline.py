@@ -1,0 +1,38 @@
+"""StreamPipeline (batches alternating over HIP streams, spef_amd/pipeline.py): every batch's pose equals the
+single-stream engine's, bit for bit, whatever the interleaving."""
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def test_pipeline_matches_single_stream():
+    from oracle import decode_ref as D
+    from spef_amd import blob as Bl
+    from spef_amd.arch import mobilenet_v2
+    from spef_amd.engine import Engine
+    from spef_amd.pipeline import StreamPipeline
+    from spef_amd.weights import synthetic_state_dict
+
+    blob = Bl.pack(synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=7), dtype='fp16')
+    h, _ = D.orientation_histogram(12, False)
+    rng = np.random.Generator(np.random.PCG64(3))
+    batches = [torch.from_numpy(rng.integers(0, 256, (4, 128, 160, 3), dtype=np.uint8)).cuda() for _ in range(7)]
+    ref = Engine(blob, 'cuda:0')
+    ref.set_decode_tables(h, None)
+    want = []
+    for x in batches:
+        o, p = ref.forward(x)
+        d = ref.decode(1, 0, o, p)
+        want.append((d['ori'].cpu().numpy(), d['pos'].cpu().numpy(), d['ori_soft'].cpu().numpy()))
+    ref.close()
+    pipe = StreamPipeline(blob, 'cuda:0', depth=3, ori_bins=h)
+    got = [pipe.submit(x) for x in batches]
+    pipe.synchronize()
+    for (q, t, s), d in zip(want, got):
+        assert np.array_equal(q, d['ori'].cpu().numpy())
+        assert np.array_equal(t, d['pos'].cpu().numpy())
+        assert np.array_equal(s, d['ori_soft'].cpu().numpy())
+        assert not d['status'].any().item()
+    pipe.close()
