@@ -21,8 +21,10 @@ OBJDIR = os.path.join(ROOT, 'build', 'obj')
 LIBNAME = 'libspef_mi355x.so'
 ARCH = 'gfx950'
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+# -amdgpu-mfma-vgpr-form: MFMA results go straight to VGPRs (gfx950's register file is unified) instead of AGPRs
+# that every epilogue then copies back with v_accvgpr_read -- fewer VALU ops and fewer registers per wave.
 CXXFLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-Wall', '-Wno-unused-function',
-            '-munsafe-fp-atomics', f'-I{INCLUDE}', f'-I{CSRC}']
+            '-munsafe-fp-atomics', '-mllvm', '-amdgpu-mfma-vgpr-form', f'-I{INCLUDE}', f'-I{CSRC}']
 
 
 # Convolution kernels never see NaN (finite frames, finite folded weights): dropping NaN semantics lets the
