@@ -52,24 +52,26 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
   // reader offsets by the common misalignment `mis`; edge tiles scatter bytes and zero the outside columns.
   int mis = 0;
   {
+    // Half a wave per input row (lane & 31 = dword k of the row, rows 2 (wave + NW i) + (lane >> 5)): no
+    // divisions, and 32-bit in-frame byte offsets (the launcher checks H * W * 3 < 2^31).
     constexpr int RB = IW * 3;                        // bytes per input-tile row
     constexpr int DPR = (RB + 3) / 4 + 1;             // dwords covering a row at any byte alignment
-    constexpr int ND = IH * DPR, NIT = (ND + NW * 64 - 1) / (NW * 64);
-    static_assert(4 * DPR <= IRS, "LDS row holds the dword-aligned run");
+    constexpr int NIT = (IH + 2 * NW - 1) / (2 * NW);
+    static_assert(4 * DPR <= IRS && DPR <= 32, "LDS row holds the dword-aligned run; one half-wave per row");
     const uint8_t* Xb = X + (size_t)b * H * W * 3;
-    const int64_t img_bytes = (int64_t)H * W * 3;
+    const int img_bytes = H * W * 3;
+    const int k = lane & 31;
     const bool fast = (W & 3) == 0 && ix0 >= 0 && ix0 + IW <= W;
     uint32_t v[NIT];
-    int64_t a[NIT];
+    int a[NIT], rs[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int d = tid + NW * 64 * i;
-      const int r = d / DPR, k = d - r * DPR;
+      const int r = 2 * (wave + NW * i) + (lane >> 5);
       const int iy = iy0 + r;
-      const int64_t rs = ((int64_t)iy * W + ix0) * 3;
-      a[i] = (rs & ~(int64_t)3) + 4 * k;
+      rs[i] = (iy * W + ix0) * 3;
+      a[i] = (rs[i] & ~3) + 4 * k;
       v[i] = 0;
-      if (d < ND && iy >= 0 && iy < H && a[i] >= 0) {
+      if (r < IH && k < DPR && iy >= 0 && iy < H && a[i] >= 0) {
         if (a[i] + 4 <= img_bytes) {
           v[i] = *reinterpret_cast<const uint32_t*>(Xb + a[i]);
         } else {
@@ -79,27 +81,22 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
       }
     }
     if (fast) {
-      mis = (int)((((int64_t)iy0 * W + ix0) * 3) & 3);   // the same for every row when W % 4 == 0
+      mis = ((iy0 * W + ix0) * 3) & 3;   // the same for every row when W % 4 == 0
 #pragma unroll
       for (int i = 0; i < NIT; ++i) {
-        const int d = tid + NW * 64 * i;
-        if (d < ND) {
-          const int r = d / DPR, k = d - r * DPR;
-          *reinterpret_cast<uint32_t*>(In + r * IRS + 4 * k) = v[i];
-        }
+        const int r = 2 * (wave + NW * i) + (lane >> 5);
+        if (r < IH && k < DPR) *reinterpret_cast<uint32_t*>(In + r * IRS + 4 * k) = v[i];
       }
     } else {
 #pragma unroll
       for (int i = 0; i < NIT; ++i) {
-        const int d = tid + NW * 64 * i;
-        if (d >= ND) continue;
-        const int r = d / DPR;
+        const int r = 2 * (wave + NW * i) + (lane >> 5);
+        if (r >= IH || k >= DPR) continue;
         const int iy = iy0 + r;
-        const int64_t rs = ((int64_t)iy * W + ix0) * 3;
         const bool row_ok = iy >= 0 && iy < H;
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int o = (int)(a[i] + j - rs);             // byte offset inside the tile row
+          const int o = a[i] + j - rs[i];               // byte offset inside the tile row
           if (o < 0 || o >= RB) continue;
           const int ix = ix0 + o / 3;
           In[r * IRS + o] = (row_ok && ix >= 0 && ix < W) ? (uint8_t)(v[i] >> (8 * j)) : (uint8_t)0;
@@ -146,27 +143,74 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
     e0 = DT::mfma(alo[0], bx, e0);
     e1 = DT::mfma(ahi[1], bx, e1);
     e1 = DT::mfma(alo[1], bx, e1);
-    bool pv = true;
+    const x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);   // packed convert + ReLU (fp16)
+    uint2 u0 = __builtin_bit_cast(uint2, o0), u1 = __builtin_bit_cast(uint2, o1);
     if (!interior) {
       const int gy = sy0 + spy, gx = sx0 + spx;
-      pv = gy >= 0 && gy < SH_img && gx >= 0 && gx < SW_img;
-    }
-    x4 o0, o1;
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      o0[r] = (T)(pv ? fmaxf(e0[r], 0.f) : 0.f);
-      o1[r] = (T)(pv ? fmaxf(e1[r], 0.f) : 0.f);
+      const uint32_t m = (gy >= 0 && gy < SH_img && gx >= 0 && gx < SW_img) ? 0xffffffffu : 0u;
+      u0.x &= m; u0.y &= m; u1.x &= m; u1.y &= m;
     }
     if (p < PS) {
-      *reinterpret_cast<x4*>(Xs + p * XS + 4 * kg) = o0;
-      *reinterpret_cast<x4*>(Xs + p * XS + 16 + 4 * kg) = o1;
+      *reinterpret_cast<uint2*>(Xs + p * XS + 4 * kg) = u0;
+      *reinterpret_cast<uint2*>(Xs + p * XS + 16 + 4 * kg) = u1;
     }
   }
   __syncthreads();
 
-  // ---- 3. block 1: depthwise 3x3 (32 ch) -> project 32 -> 16 (+BN), one 16-pixel tile per wave step
+  // ---- 3. block 1: depthwise 3x3 (32 ch) -> project 32 -> 16 (+BN)
   const x8 pa = load8<DT>(Wp + (size_t)r16 * 32 + 8 * kg);
   const float4 pb = *reinterpret_cast<const float4*>(bp + 4 * kg);
+  auto store = [&](int oy, int ox, const f32x4& acc) {
+    const int gy = oy0 + oy, gx = ox0 + ox;
+    if (gy < SH_img && gx < SW_img) {
+      x4 out;
+      out[0] = (T)acc[0];
+      out[1] = (T)acc[1];
+      out[2] = (T)acc[2];
+      out[3] = (T)acc[3];
+      *reinterpret_cast<x4*>(Y + (((size_t)b * SH_img + gy) * SW_img + gx) * 16 + 4 * kg) = out;
+    }
+  };
+  if constexpr (TW == 16 && QPW % 2 == 0) {
+    // Two vertically adjacent output rows per step (a wave's tiles qi, qi+1 are rows oy, oy+1 of the same 16
+    // columns): per tap column the 3 weights and 4 stem rows are read once and feed both rows -- 21 instead of 36
+    // ds_read_b128 per 2 x 16 pixels x 8 channels. Same tap order (kx outer, ky inner) as the one-row loop.
+#pragma unroll
+    for (int qi = 0; qi < QPW; qi += 2) {
+      const int oy = wave * QPW + qi, ox = r16;
+      float a0[8], a1[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) a0[e] = a1[e] = Sb[8 * kg + e];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        DW8<DT> w[3];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) w[ky].load(Sl + (ky * 3 + kx) * 32 + 8 * kg);
+        x8 v[4];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) v[r] = *reinterpret_cast<const x8*>(Xs + ((oy + r) * SW + (ox + kx)) * XS + 8 * kg);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            a0[e] = fmaf((float)v[ky][e], w[ky][e], a0[e]);
+            a1[e] = fmaf((float)v[ky + 1][e], w[ky][e], a1[e]);
+          }
+      }
+      x8 bf0, bf1;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        bf0[e] = (T)fmaxf(a0[e], 0.f);
+        bf1[e] = (T)fmaxf(a1[e], 0.f);
+      }
+      f32x4 acc0 = {pb.x, pb.y, pb.z, pb.w}, acc1 = acc0;   // bias as MFMA C (same order as the block kernels)
+      acc0 = DT::mfma(pa, bf0, acc0);
+      acc1 = DT::mfma(pa, bf1, acc1);
+      store(oy, ox, acc0);
+      store(oy + 1, ox, acc1);
+    }
+    return;
+  }
 #pragma unroll
   for (int qi = 0; qi < QPW; ++qi) {
     const int o = (wave * QPW + qi) * 16 + r16;
@@ -189,15 +233,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
     for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
     f32x4 acc = {pb.x, pb.y, pb.z, pb.w};      // bias as MFMA C (same order as the block kernels)
     acc = DT::mfma(pa, bf, acc);
-    const int gy = oy0 + oy, gx = ox0 + ox;
-    if (gy < SH_img && gx < SW_img) {
-      x4 out;
-      out[0] = (T)acc[0];
-      out[1] = (T)acc[1];
-      out[2] = (T)acc[2];
-      out[3] = (T)acc[3];
-      *reinterpret_cast<x4*>(Y + (((size_t)b * SH_img + gy) * SW_img + gx) * 16 + 4 * kg) = out;
-    }
+    store(oy, ox, acc);
   }
 }
 
@@ -209,6 +245,7 @@ hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* 
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
+  if ((int64_t)H * W * 3 + 4 > 0x7fffffff) return hipErrorInvalidValue;   // 32-bit in-frame byte offsets
   if (dtype == DT_F16)
     front_kernel<F16, TH, TW, NW><<<nwg, NW * 64, 0, s>>>((const uint8_t*)x, (const _Float16*)wsp, bs, (const _Float16*)wd, bd, (const _Float16*)wp, bp,
                                                           (_Float16*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);

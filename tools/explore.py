@@ -48,8 +48,11 @@ def main():
     ori = torch.empty((B, 1728), device='cuda')
     pos = torch.empty((B, 3), device='cuda')
     if os.environ.get("SWEEP"):
+        # OPTS="7:1,6:0" -> extra spef_set_option(option, value) pairs for every sweep point
+        extra = {int(k): int(v) for k, v in (kv.split(':') for kv in os.environ.get('OPTS', '').split(',') if kv)}
         for v in [int(x) for x in os.environ.get("SWEEP", "0,1,2").split(",")]:
-            run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 1, L.OPT_IRB_VARIANT: v}, label=f'fused variant {v}')
+            run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 1, L.OPT_IRB_VARIANT: v, **extra},
+                label=f'fused variant {v} {extra}')
         return
     ref = run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 0, L.OPT_PW_GEMM: 0}, label='unfused, direct pw')
     g = run(eng, fr, ori, pos, {L.OPT_FUSE_BLOCKS: 0, L.OPT_PW_GEMM: 1}, label='unfused, LDS GEMM')
