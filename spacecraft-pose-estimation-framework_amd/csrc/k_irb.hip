@@ -208,7 +208,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   // interior tiles (whole input tile inside the image) need no padding mask in the expand epilogue
   const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + G::IH <= H && ix0 + G::IW <= W;
   uint32_t pvmask = 0;
-  if constexpr (EXPAND) {
+  if (EXPAND && !interior) {   // only edge tiles mask (workgroup-uniform branch)
 #pragma unroll
     for (int j = 0; j < G::EPT; ++j) {
       const int p = (wave + NW * j) * 16 + r16;

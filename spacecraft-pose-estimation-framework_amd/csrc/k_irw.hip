@@ -209,6 +209,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   // The two roles run separate loops with the same barrier count (2 + NCH), so each role's registers (the
   // project accumulators, the expand fragments) are allocated independently.
   if (is_expand) {
+    if (!interior)   // only edge tiles mask (workgroup-uniform branch)
 #pragma unroll
     for (int jj = 0; jj < G::EPT; ++jj) {
       const int p = (ew + NE * jj) * 16 + r16;
