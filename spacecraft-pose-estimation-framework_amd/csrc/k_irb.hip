@@ -115,37 +115,44 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
 
+  // Every global load below is branch-free (a load inside a divergent branch is waited for before the branch
+  // joins): out-of-range pieces read a valid address and are zeroed when stored to LDS, after all loads are issued.
+
   // depthwise-weight slab of chunk cc: thread t < SLAB_PIECES moves one 16-B piece of [9][32]
   constexpr int EPP = 16 / (int)sizeof(DW);      // weights per piece
+  auto slab_ok = [&](int cc) {
+    return ABL != 7 && tid < G::SLAB_PIECES && cc < G::NCH && 32 * cc + ((tid * EPP) & 31) < HID;
+  };
   auto slab_load = [&](int cc) -> uint4 {
-    uint4 v = make_uint4(0, 0, 0, 0);
-    if (ABL != 7 && tid < G::SLAB_PIECES && cc < G::NCH) {
-      const int f = tid * EPP, tap = f >> 5, ch = 32 * cc + (f & 31);
-      if (ch < HID) v = *reinterpret_cast<const uint4*>(Wd + tap * HID + ch);
-    }
-    return v;
+    const int f = tid * EPP, tap = f >> 5, ch = 32 * cc + (f & 31);
+    return *reinterpret_cast<const uint4*>(Wd + (slab_ok(cc) ? tap * HID + ch : 0));
   };
   auto slab_store = [&](int cc, uint4 v) {
-    if (tid < G::SLAB_PIECES) *reinterpret_cast<uint4*>(Sl + (cc & 1) * G::SLAB + tid * EPP) = v;
+    if (tid < G::SLAB_PIECES)
+      *reinterpret_cast<uint4*>(Sl + (cc & 1) * G::SLAB + tid * EPP) = slab_ok(cc) ? v : make_uint4(0, 0, 0, 0);
   };
 
   // weight staging: pieces [0, WE_PIECES) = expand rows of chunk ce, then project rows of chunk cp
   x8 wst[G::W_PPT > 0 ? G::W_PPT : 1];
+  auto wst_src = [&](int i, int ce, int cp) -> const T* {   // nullptr: piece not present (zero)
+    const int p = ABL == 6 ? 1 << 30 : tid + NW * 64 * i;
+    if (p < G::WE_PIECES) {
+      const int row = p / (G::WEK / 8), g = p - row * (G::WEK / 8);
+      const int h = 32 * ce + row;
+      return ce < G::NCH && h < (HID + 15) / 16 * 16 ? We + (size_t)h * G::WKP + 8 * g : nullptr;
+    }
+    if (p < G::WE_PIECES + G::WP_PIECES) {
+      const int q = p - G::WE_PIECES, row = q >> 2, g = q & 3;
+      return cp < G::NCH ? Wp + (size_t)row * G::HIDP + 32 * cp + 8 * g : nullptr;
+    }
+    return nullptr;
+  };
   auto wst_load = [&](int ce, int cp) {
     if constexpr (STW) {
 #pragma unroll
       for (int i = 0; i < G::W_PPT; ++i) {
-        const int p = ABL == 6 ? 1 << 30 : tid + NW * 64 * i;
-        x8 v = zero8<DT>();
-        if (p < G::WE_PIECES) {
-          const int row = p / (G::WEK / 8), g = p - row * (G::WEK / 8);
-          const int h = 32 * ce + row;
-          if (ce < G::NCH && h < (HID + 15) / 16 * 16) v = load8<DT>(We + (size_t)h * G::WKP + 8 * g);
-        } else if (p < G::WE_PIECES + G::WP_PIECES) {
-          const int q = p - G::WE_PIECES, row = q >> 2, g = q & 3;
-          if (cp < G::NCH) v = load8<DT>(Wp + (size_t)row * G::HIDP + 32 * cp + 8 * g);
-        }
-        wst[i] = v;
+        const T* s = wst_src(i, ce, cp);
+        wst[i] = load8<DT>(s ? s : We);
       }
     }
   };
@@ -154,51 +161,64 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 #pragma unroll
       for (int i = 0; i < G::W_PPT; ++i) {
         const int p = tid + NW * 64 * i;
+        const x8 v = wst_src(i, ce, cp) ? wst[i] : zero8<DT>();
         if (p < G::WE_PIECES) {
           const int row = p / (G::WEK / 8), g = p - row * (G::WEK / 8);
-          *reinterpret_cast<x8*>(WEs + (ce % 3) * 32 * G::WES + row * G::WES + 8 * g) = wst[i];
+          *reinterpret_cast<x8*>(WEs + (ce % 3) * 32 * G::WES + row * G::WES + 8 * g) = v;
         } else if (p < G::WE_PIECES + G::WP_PIECES) {
           const int q = p - G::WE_PIECES, row = q >> 2, g = q & 3;
-          *reinterpret_cast<x8*>(WPs + (cp & 1) * G::NCTP * G::WPS + row * G::WPS + 8 * g) = wst[i];
+          *reinterpret_cast<x8*>(WPs + (cp & 1) * G::NCTP * G::WPS + row * G::WPS + 8 * g) = v;
         }
       }
     }
   };
 
-  // ---- 1. stage the input tile (+halo) in LDS; outside the image (and K padding) -> 0
+  // ---- 1. prologue: the input tile (+halo; outside the image and K padding -> 0), depthwise slab 0, expand
+  // weights of chunk 0 and all biases -- every global load issued first, one wait, then the LDS stores
   {
     constexpr int GPR = G::CINP / 8;        // 16-B groups per LDS row (CIN 16: 2)
     constexpr int CG = CIN / 8;             // valid groups
     const T* Xb = X + (size_t)b * H * W * CIN;
     constexpr int NU = G::PINP * GPR, NIT = (NU + NW * 64 - 1) / (NW * 64);
     x8 xin[NIT];
+    uint32_t okm = 0;
 #pragma unroll
-    for (int i = 0; i < NIT; ++i) {   // all loads in flight before the first LDS store
+    for (int i = 0; i < NIT; ++i) {
       const int u = tid + NW * 64 * i;
       const int p = u / GPR, g = u - p * GPR;
-      xin[i] = zero8<DT>();
-      if (u < NU && p < G::PIN && g < CG) {
-        const int py = p / G::IW, px = p - py * G::IW;
-        const int iy = iy0 + py, ix = ix0 + px;
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W) xin[i] = load8<DT>(Xb + ((size_t)iy * W + ix) * CIN + g * 8);
-      }
+      const int py = p / G::IW, px = p - py * G::IW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const bool ok = u < NU && p < G::PIN && g < CG && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      xin[i] = load8<DT>(Xb + (ok ? ((size_t)iy * W + ix) * CIN + g * 8 : 0));
+      okm |= (uint32_t)ok << i;
+    }
+    const uint4 sl0 = slab_load(0);
+    if constexpr (STW && EXPAND) wst_load(0, G::NCH);   // expand weights of chunk 0 (project weights follow later)
+    constexpr int NBI = (G::NCH * 32 + NW * 64 - 1) / (NW * 64);
+    float bdv[NBI], bev[NBI];
+#pragma unroll
+    for (int j = 0; j < NBI; ++j) {
+      const int u = tid + NW * 64 * j, uc = u < HID ? u : HID - 1;
+      bdv[j] = bd[uc];
+      bev[j] = EXPAND ? be[uc] : 0.f;
     }
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int u = tid + NW * 64 * i;
       if (u < NU) {
         const int p = u / GPR, g = u - p * GPR;
-        *reinterpret_cast<x8*>(Xs + p * G::XS + g * 8) = xin[i];
+        *reinterpret_cast<x8*>(Xs + p * G::XS + g * 8) = ((okm >> i) & 1u) ? xin[i] : zero8<DT>();
       }
     }
-    slab_store(0, slab_load(0));
-    if constexpr (STW && EXPAND) {   // expand weights of chunk 0 (the project weights of chunk 0 follow the schedule)
-      wst_load(0, G::NCH);
-      wst_store(0, 0);
-    }
-    for (int u = tid; u < G::NCH * 32; u += NW * 64) {   // all biases, once
-      Bd[u] = u < HID ? bd[u] : 0.f;
-      if constexpr (EXPAND) Be[u] = u < HID ? be[u] : 0.f;
+    slab_store(0, sl0);
+    if constexpr (STW && EXPAND) wst_store(0, 0);
+#pragma unroll
+    for (int j = 0; j < NBI; ++j) {   // all biases, once
+      const int u = tid + NW * 64 * j;
+      if (u < G::NCH * 32) {
+        Bd[u] = u < HID ? bdv[j] : 0.f;
+        if constexpr (EXPAND) Be[u] = u < HID ? bev[j] : 0.f;
+      }
     }
   }
   wst_load(1, 0);      // in flight across the first expand

@@ -54,7 +54,7 @@ def load(path: str | None = None) -> C.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = path or _build.lib_path()
+    path = path or os.environ.get('SPEF_LIB') or _build.lib_path()   # SPEF_LIB: A/B timing of two builds
     if not os.path.exists(path):
         raise ImportError(f'SPEF HIP library not built: {path} (run __graft_entry__.build() or '
                           f'python -m spef_amd._build)')
