@@ -18,6 +18,7 @@
 // Synchronisation: ONE barrier per hidden chunk. Es is double-buffered; the per-chunk depthwise weight slab
 // (9x32 weights, dw bias, expand bias; fp32) is triple-buffered and filled one chunk ahead.
 #include "spef_common.hpp"
+#include <type_traits>
 #include "spef_kernels.hpp"
 
 namespace spef {
@@ -305,23 +306,45 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       }
       const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
       const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
+      // All of this wave's B fragments first, then the MFMAs and epilogues: the compiler cannot move an Xs read
+      // above the previous tile's slab store (both live in the same LDS array), so reading per tile serialised one
+      // LDS round trip + MFMA latency per tile.
+      // (Only while the fragments fit in 12 VGPRs: measured slower for blocks 4 and 17, where they do not.)
+      constexpr int NBX = G::K16 ? 1 : G::KS;
+      constexpr bool BATCH = G::EPT * NBX * (G::K16 ? 2 : 4) <= 12;
+      typename std::conditional<G::K16, x4, x8>::type bxs[G::EPT][NBX];
+      auto read_bx = [&](int j) {
+        const int pt = wave + NW * j;
+        if constexpr (G::K16) {
+          bxs[j][0] = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < G::KS; ++ks)
+            bxs[j][ks] = *reinterpret_cast<const x8*>(Xs + (pt * 16 + r16) * G::XS + 8 * kg + 32 * ks);
+        }
+      };
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        if (!BATCH) break;
+        const int pt = wave + NW * j;
+        if (pt >= G::PIN16) break;
+        read_bx(j);
+      }
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
         const int pt = wave + NW * j;
         if (pt >= G::PIN16) break;
+        if (!BATCH) read_bx(j);
         f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
         if constexpr (ABL == 2) {
         } else if constexpr (G::K16) {
-          const x4 bx = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
-          e0 = DT::mfma16(q0, bx, e0);
-          e1 = DT::mfma16(q1, bx, e1);
+          e0 = DT::mfma16(q0, bxs[j][0], e0);
+          e1 = DT::mfma16(q1, bxs[j][0], e1);
         } else {
-          const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
 #pragma unroll
           for (int ks = 0; ks < G::KS; ++ks) {
-            const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
-            e0 = DT::mfma(a0[ks], bx, e0);
-            e1 = DT::mfma(a1[ks], bx, e1);
+            e0 = DT::mfma(a0[ks], bxs[j][ks], e0);
+            e1 = DT::mfma(a1[ks], bxs[j][ks], e1);
           }
         }
         x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);

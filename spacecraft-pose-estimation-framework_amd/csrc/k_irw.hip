@@ -17,6 +17,7 @@
 // fp16/bf16 after expand, fp32 depthwise in kx-outer/ky-inner tap order, fp16/bf16 after the depthwise, fp32
 // project accumulation over chunks in order -> bit-identical to the one-kernel-per-conv schedule.
 #include "spef_common.hpp"
+#include <type_traits>
 #include "spef_kernels.hpp"
 
 namespace spef {
@@ -158,22 +159,40 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     T* Ew = Es0 + (c & 1) * G::PINP * G::ES;
     const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
     const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
+    // all of this wave's B fragments first, then MFMAs + epilogues (the compiler cannot hoist an Xs read above the
+    // previous tile's slab store: same LDS array), within a register budget for the expand role
+    constexpr int NBX = G::K16 ? 1 : G::KS;
+    constexpr bool BATCH = G::EPT * NBX * (G::K16 ? 2 : 4) <= 48;
+    typename std::conditional<G::K16, x4, x8>::type bxs[G::EPT][NBX];
+    auto read_bx = [&](int jj) {
+      const int pt = ew + NE * jj;
+      if constexpr (G::K16) {
+        bxs[jj][0] = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
+      } else {
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks)
+          bxs[jj][ks] = *reinterpret_cast<const x8*>(Xs + (pt * 16 + r16) * G::XS + 8 * kg + 32 * ks);
+      }
+    };
+#pragma unroll
+    for (int jj = 0; jj < G::EPT; ++jj) {
+      if (!BATCH || ew + NE * jj >= G::PIN16) break;
+      read_bx(jj);
+    }
 #pragma unroll
     for (int jj = 0; jj < G::EPT; ++jj) {
       const int pt = ew + NE * jj;
       if (pt >= G::PIN16) break;
+      if (!BATCH) read_bx(jj);
       f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
       if constexpr (G::K16) {
-        const x4 bx = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
-        e0 = DT::mfma16(eq0, bx, e0);
-        e1 = DT::mfma16(eq1, bx, e1);
+        e0 = DT::mfma16(eq0, bxs[jj][0], e0);
+        e1 = DT::mfma16(eq1, bxs[jj][0], e1);
       } else {
-        const T* xr = Xs + (pt * 16 + r16) * G::XS + 8 * kg;
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
-          const x8 bx = *reinterpret_cast<const x8*>(xr + 32 * ks);
-          e0 = DT::mfma(ea0[ks], bx, e0);
-          e1 = DT::mfma(ea1[ks], bx, e1);
+          e0 = DT::mfma(ea0[ks], bxs[jj][ks], e0);
+          e1 = DT::mfma(ea1[ks], bxs[jj][ks], e1);
         }
       }
       x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);
