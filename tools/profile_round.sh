@@ -4,7 +4,7 @@
 #   gpurun_out/prof_<tag>/         rocprofv3 --kernel-trace --stats of a short bench run
 #   gpurun_out/pmc_fetch_<tag>/, pmc_write_<tag>/   separate FETCH_SIZE / WRITE_SIZE passes (MI355X_MICROARCH.md)
 # then: python tools/rocprof_summary.py --tag <tag> --stats gpurun_out/prof_<tag> \
-#         --fetch gpurun_out/pmc_fetch_<tag> --write gpurun_out/pmc_write_<tag>
+#         --fetch gpurun_out/pmc_fetch_<tag> --write gpurun_out/pmc_write_<tag> --leg 10 --total 22
 set -e
 TAG=${1:-r01}
 export TMPDIR=/tmp

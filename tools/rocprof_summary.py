@@ -46,11 +46,31 @@ def main():
     ap.add_argument('--stats', required=True)
     ap.add_argument('--fetch')
     ap.add_argument('--write')
+    ap.add_argument('--leg', type=int, default=0,
+                    help="bench.py's single-stream HIP-event leg = the last LEG steps of the traced run")
+    ap.add_argument('--total', type=int, default=0, help='all steps of the traced run (warmup + steps + leg)')
     a = ap.parse_args()
     out = os.path.join(ROOT, 'profiles')
     os.makedirs(out, exist_ok=True)
     st = glob.glob(os.path.join(a.stats, '*kernel_stats.csv'))[0]
     shutil.copy(st, os.path.join(out, f'{a.tag}_kernel_stats.csv'))
+    if a.leg and a.total:
+        # Per kernel, the dispatches of bench.py's roofline leg (one stream, no overlap with other batches): the
+        # durations bench.py's HIP events measure. The pipelined steps before it overlap up to --inflight batches,
+        # which stretches their individual kernel durations in the --stats average.
+        tr = glob.glob(os.path.join(a.stats, '*kernel_trace.csv'))[0]
+        by = defaultdict(list)
+        for r in csv.DictReader(open(tr)):
+            by[short_name(r['Kernel_Name'])].append((int(r['Start_Timestamp']), int(r['End_Timestamp'])))
+        with open(os.path.join(out, f'{a.tag}_kernel_stats_leg.csv'), 'w', newline='') as f:
+            w = csv.writer(f)
+            w.writerow(['Name', 'LegCalls', 'AverageNs', 'MinNs', 'MaxNs', 'AllCalls', 'AllAverageNs'])
+            for k, v in sorted(by.items(), key=lambda kv: -sum(e - s for s, e in kv[1])):
+                v.sort()
+                n = max(1, round(len(v) * a.leg / a.total))
+                d = [e - s for s, e in v[-n:]]
+                alld = [e - s for s, e in v]
+                w.writerow([k, n, round(sum(d) / n, 1), min(d), max(d), len(v), round(sum(alld) / len(alld), 1)])
     if a.fetch and a.write:
         fe, n = per_kernel(a.fetch, 'FETCH_SIZE')
         wr, _ = per_kernel(a.write, 'WRITE_SIZE')
