@@ -101,8 +101,8 @@ def pose_error(eng, dev, fr, o_ref, p_ref, q_ref):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=30)
-    ap.add_argument('--warmup', type=int, default=5)
+    ap.add_argument('--steps', type=int, default=100)
+    ap.add_argument('--warmup', type=int, default=10)
     ap.add_argument('--batch', type=int, default=64)
     ap.add_argument('--size', type=int, default=512)
     ap.add_argument('--dtype', default='fp16', choices=['fp16', 'bf16', 'int8'],

@@ -6,11 +6,14 @@
 // summed in fp32 registers over the wave's pixel tiles, then over the 16 pixel lanes by shuffles and over the
 // 4 pixel waves through LDS: the 1280-channel map never exists in memory and the mean is deterministic.
 #include "spef_common.hpp"
+#include <type_traits>
 #include "spef_kernels.hpp"
 
 namespace spef {
 
-template <typename DT>
+// KSC > 0: the K step count is a compile-time constant (K = 32 * KSC, the URSONet last conv has K = 320) and the K loop
+// is fully unrolled, which lets the compiler track the two register stages' outstanding loads exactly.
+template <typename DT, int KSC>
 __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __restrict__ X,
                                                         const typename DT::T* __restrict__ Wt,
                                                         const float* __restrict__ bias, float* __restrict__ pooled,
@@ -34,7 +37,7 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
   const int r16 = lane & 15, kg = lane >> 4;
   const int wn = wave & 1, wm = wave >> 1;
   const T* Xb = X + (size_t)b * HW * K;
-  const int KS = Kp >> 5;
+  const int KS = KSC > 0 ? KSC : Kp >> 5;
 
   f32x4 bias4[NT];
 #pragma unroll
@@ -46,30 +49,40 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
 #pragma unroll
   for (int a = 0; a < NT; ++a) sum[a] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  x8 xr[XP], wr[WP];
+  // Two register stages of global fragments: step ks stores the fragments loaded during step ks-1 and loads
+  // those of step ks+2, so each load has two K steps of MFMAs and barriers to land in (one step was not enough to
+  // cover the L2/HBM latency). Loads are branch-free (out-of-range rows read row 0 and are zeroed at the LDS store):
+  // a load inside a divergent branch is waited for at the branch join.
+  x8 xr[2][XP], wr[2][WP];
   for (int m0 = 0; m0 < HW; m0 += BM) {
-    auto gload = [&](int ks) {
+    auto xok = [&](int i, int ks) {
+      const int p = tid + 512 * i, row = p >> 2, g = p & 3;
+      return m0 + row < HW && ks * 32 + 8 * g < K;
+    };
+    auto gload = [&](int ks, auto stc) {
+      constexpr int st = decltype(stc)::value;
 #pragma unroll
       for (int i = 0; i < XP; ++i) {
         const int p = tid + 512 * i, row = p >> 2, g = p & 3, k = ks * 32 + 8 * g;
-        xr[i] = (m0 + row < HW && k < K) ? load8<DT>(Xb + (size_t)(m0 + row) * K + k) : zero8<DT>();
+        xr[st][i] = load8<DT>(Xb + (xok(i, ks) ? (size_t)(m0 + row) * K + k : 0));
       }
 #pragma unroll
       for (int i = 0; i < WP; ++i) {
         const int p = tid + 512 * i, row = p >> 2, g = p & 3;
-        wr[i] = load8<DT>(Wt + (size_t)(n0 + row) * Kp + ks * 32 + 8 * g);
+        wr[st][i] = load8<DT>(Wt + (size_t)(n0 + row) * Kp + ks * 32 + 8 * g);
       }
     };
-    auto lstore = [&](int buf) {
+    auto lstore = [&](int buf, int ks, auto stc) {
+      constexpr int st = decltype(stc)::value;
 #pragma unroll
       for (int i = 0; i < XP; ++i) {
         const int p = tid + 512 * i;
-        *reinterpret_cast<x8*>(&Bs[buf][(p >> 2) * RS + 8 * (p & 3)]) = xr[i];
+        *reinterpret_cast<x8*>(&Bs[buf][(p >> 2) * RS + 8 * (p & 3)]) = xok(i, ks) ? xr[st][i] : zero8<DT>();
       }
 #pragma unroll
       for (int i = 0; i < WP; ++i) {
         const int p = tid + 512 * i;
-        *reinterpret_cast<x8*>(&As[buf][(p >> 2) * RS + 8 * (p & 3)]) = wr[i];
+        *reinterpret_cast<x8*>(&As[buf][(p >> 2) * RS + 8 * (p & 3)]) = wr[st][i];
       }
     };
     f32x4 acc[NT][MT];
@@ -78,27 +91,37 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
 #pragma unroll
       for (int q = 0; q < MT; ++q) acc[a][q] = bias4[a];
     __syncthreads();   // previous chunk's LDS reads done
-    gload(0);
-    lstore(0);
+    gload(0, std::integral_constant<int, 0>());
+    if (KS > 1) gload(1, std::integral_constant<int, 1>());
+    lstore(0, 0, std::integral_constant<int, 0>());
     __syncthreads();
-    for (int ks = 0; ks < KS; ++ks) {
-      const int buf = ks & 1;
-      if (ks + 1 < KS) gload(ks + 1);
+    // K step ks uses LDS buffer and register stage ks & 1; the loop is unrolled by two so both are compile-time
+    auto step = [&](int ks, auto par) {
+      constexpr int P = decltype(par)::value;
+      // stage P was stored to LDS at the end of step ks - 1. Issued unconditionally (the last two steps reload a
+      // valid step that is never stored) so the count of outstanding loads is the same on every path and the
+      // compiler's wait before the store below covers only the older stage.
+      gload(ks + 2 < KS ? ks + 2 : KS - 1, std::integral_constant<int, P>());
       x8 af[NT], bf[MT];
 #pragma unroll
       for (int a = 0; a < NT; ++a)
-        af[a] = *reinterpret_cast<const x8*>(&As[buf][((wn * NT + a) * 16 + r16) * RS + 8 * kg]);
+        af[a] = *reinterpret_cast<const x8*>(&As[P][((wn * NT + a) * 16 + r16) * RS + 8 * kg]);
 #pragma unroll
       for (int q = 0; q < MT; ++q)
-        bf[q] = *reinterpret_cast<const x8*>(&Bs[buf][((wm * MT + q) * 16 + r16) * RS + 8 * kg]);
+        bf[q] = *reinterpret_cast<const x8*>(&Bs[P][((wm * MT + q) * 16 + r16) * RS + 8 * kg]);
 #pragma unroll
       for (int a = 0; a < NT; ++a)
 #pragma unroll
         for (int q = 0; q < MT; ++q) acc[a][q] = DT::mfma(af[a], bf[q], acc[a][q]);
       if (ks + 1 < KS) {
-        lstore(buf ^ 1);
+        lstore(P ^ 1, ks + 1, std::integral_constant<int, P ^ 1>());
         __syncthreads();
       }
+    };
+#pragma unroll
+    for (int ks = 0; ks < KS; ks += 2) {
+      step(ks, std::integral_constant<int, 0>());
+      if (ks + 1 < KS) step(ks + 1, std::integral_constant<int, 1>());
     }
 #pragma unroll
     for (int q = 0; q < MT; ++q) {
@@ -133,10 +156,14 @@ hipError_t launch_pool_gemm(int dtype, const void* x, const void* wt, const floa
   const int Kp = (K + 31) & ~31, Np = (N + 15) & ~15;
   if ((K & 7) || (Np % 128)) return hipErrorInvalidValue;
   dim3 g(Np / 128, B);
-  if (dtype == DT_F16)
-    pool_gemm_kernel<F16><<<g, 512, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
-  else
-    pool_gemm_kernel<BF16><<<g, 512, 0, s>>>((const __bf16*)x, (const __bf16*)wt, bias, pooled, HW, K, Kp, N);
+  if (dtype == DT_F16) {
+    if (Kp == 320)
+      pool_gemm_kernel<F16, 10><<<g, 512, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
+    else
+      pool_gemm_kernel<F16, 0><<<g, 512, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
+  } else {
+    pool_gemm_kernel<BF16, 0><<<g, 512, 0, s>>>((const __bf16*)x, (const __bf16*)wt, bias, pooled, HW, K, Kp, N);
+  }
   return hipGetLastError();
 }
 

@@ -32,8 +32,8 @@ def main():
     b = sys.argv[2] if len(sys.argv) > 2 and not sys.argv[2].isdigit() else ''
     rounds = int(sys.argv[-1]) if sys.argv[-1].isdigit() else 2
     acc = {'A': defaultdict(list), 'B': defaultdict(list)}
-    for _ in range(rounds):
-        for tag, lib in (('A', a), ('B', b)):
+    for r in range(rounds):   # alternate the order (A B, B A, ...): the second run of a pair is systematically slower
+        for tag, lib in ((('A', a), ('B', b)) if r % 2 == 0 else (('B', b), ('A', a))):
             for k, v in run(lib).items():
                 acc[tag][k].append(v)
     keys = sorted(acc['A'], key=lambda k: -sum(acc['A'][k]) / len(acc['A'][k]))
