@@ -384,8 +384,8 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   X(1, 32, 192, 32, 1, 8, 16, true, 2, 4, 1)                                \
   X(0, 64, 384, 64, 1, 16, 16, true, 4, 8, 1)      /* blocks 8-10  */       \
   X(1, 64, 384, 64, 1, 16, 16, true, 4, 4, 1)                               \
-  X(0, 64, 384, 96, 1, 16, 16, false, 4, 8, 1)     /* block 11     */       \
-  X(1, 64, 384, 96, 1, 16, 16, false, 4, 4, 1)                              \
+  X(0, 64, 384, 96, 1, 16, 16, false, 4, 4, 1)     /* block 11     */       \
+  X(1, 64, 384, 96, 1, 16, 16, false, 4, 8, 1)                              \
   X(0, 96, 576, 96, 1, 16, 16, true, 4, 8, 1)      /* blocks 12-13 */       \
   X(1, 96, 576, 96, 1, 16, 16, true, 4, 4, 1)                               \
   X(0, 96, 576, 160, 2, 8, 8, false, 4, 4, 2)      /* block 14     */       \
