@@ -257,6 +257,29 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     for (int qi = 0; qi < G::QPW; ++qi) acc[qi][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
   }
 
+  // expand weight fragments (no STW) are prefetched one chunk ahead into registers (they were loaded at the top of
+  // their own chunk and waited for right away by the expand). Branch-free: a missing second half of a partial chunk
+  // (rows past the blob's HID rounded to 16) reloads the first half and is zeroed at use.
+  constexpr int WKP = (CIN + 31) / 32 * 32;
+  constexpr int NP16 = (HID + 15) / 16 * 16;
+  x8 ca0[G::KS], ca1[G::KS];
+  x4 cq0 = {}, cq1 = {};
+  auto ew_load = [&](int cc, x4& q0_, x4& q1_, x8* a0_, x8* a1_) {
+    cc = cc < G::NCH ? cc : G::NCH - 1;
+    const int h1 = 32 * cc + 16 < NP16 ? 32 * cc + 16 : 32 * cc;
+    if constexpr (G::K16) {
+      q0_ = *reinterpret_cast<const x4*>(We + (size_t)(32 * cc + r16) * WKP + 4 * kg);
+      q1_ = *reinterpret_cast<const x4*>(We + (size_t)(h1 + r16) * WKP + 4 * kg);
+    } else {
+#pragma unroll
+      for (int ks = 0; ks < G::KS; ++ks) {
+        a0_[ks] = load8<DT>(We + (size_t)(32 * cc + r16) * WKP + 32 * ks + 8 * kg);
+        a1_[ks] = load8<DT>(We + (size_t)(h1 + r16) * WKP + 32 * ks + 8 * kg);
+      }
+    }
+  };
+  if constexpr (EXPAND && !STW) ew_load(0, cq0, cq1, ca0, ca1);
+
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
     const uint4 slab_next = slab_load(c + 1);      // issued now, stored after this chunk's depthwise
@@ -277,7 +300,6 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       const int vh = HID - 32 * c < 32 ? HID - 32 * c : 32;   // valid hidden channels in this chunk
       // ---- 2. expand: E[p][h] = relu(sum_k X[p][k] We[32c+h][k] + be) for all tile pixels
       // expand weights are stored [Np][Kp] with Kp = CIN rounded up to 32 (blob layout)
-      constexpr int WKP = (CIN + 31) / 32 * 32;
       x8 a0[G::KS], a1[G::KS];
       x4 q0 = {}, q1 = {};
       if constexpr (STW) {
@@ -292,16 +314,23 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
             a1[ks] = *reinterpret_cast<const x8*>(w0 + 16 * G::WES + 32 * ks + 8 * kg);
           }
         }
-      } else if constexpr (G::K16) {
-        const T* w0 = We + (size_t)(32 * c + r16) * WKP + 4 * kg;
-        q0 = *reinterpret_cast<const x4*>(w0);
-        if (vh > 16) q1 = *reinterpret_cast<const x4*>(w0 + 16 * WKP);
       } else {
-        const T* w0 = We + (size_t)(32 * c + r16) * WKP + 8 * kg;
+        x8 na0[G::KS], na1[G::KS];
+        x4 nq0 = {}, nq1 = {};
+        ew_load(c + 1, nq0, nq1, na0, na1);   // next chunk's fragments, in flight across this chunk
+        if constexpr (G::K16) {
+          q0 = cq0;
+          q1 = vh > 16 ? cq1 : x4{};
+          cq0 = nq0;
+          cq1 = nq1;
+        } else {
 #pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-          a0[ks] = load8<DT>(w0 + 32 * ks);
-          a1[ks] = vh > 16 ? load8<DT>(w0 + 16 * WKP + 32 * ks) : zero8<DT>();
+          for (int ks = 0; ks < G::KS; ++ks) {
+            a0[ks] = ca0[ks];
+            a1[ks] = vh > 16 ? ca1[ks] : zero8<DT>();
+            ca0[ks] = na0[ks];
+            ca1[ks] = na1[ks];
+          }
         }
       }
       const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
