@@ -86,19 +86,23 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
 
-  // per-chunk tables -> LDS buffer (cc & 1): 16-B pieces, RQ16 expand (32), RQ16 depthwise (32), weights (36)
-  auto stage_tables = [&](int cc) {
-    uint4* dst = reinterpret_cast<uint4*>(Tb + (cc & 1) * G::TAB);
-    for (int u = tid; u < 32 + 32 + 36; u += NW * 64) {
-      uint4 v;
-      if (u < 32) v = *reinterpret_cast<const uint4*>(gRqE + 32 * cc + u);
-      else if (u < 64) v = *reinterpret_cast<const uint4*>(gRqD + 32 * cc + (u - 32));
-      else {
-        const int f = (u - 64) * 8, tap = f >> 5, ch = f & 31;   // 8 fp16 weights of one tap
-        v = *reinterpret_cast<const uint4*>(gWd + tap * G::H32 + 32 * cc + ch);
-      }
-      dst[u] = v;
+  // per-chunk tables -> LDS buffer (cc & 1): 16-B pieces, RQ16 expand (32), RQ16 depthwise (32), weights (36); one
+  // piece per thread. Loads are branch-free and issued a chunk ahead of their store: a load under a condition, or
+  // one stored right away, is waited for at once (a full memory round trip per chunk).
+  static_assert(NW * 64 >= 100, "one table piece per thread");
+  auto tab_load = [&](int cc) -> uint4 {
+    const int u = tid;
+    const void* src = gRqE;
+    if (u < 32) src = gRqE + 32 * cc + u;
+    else if (u < 64) src = gRqD + 32 * cc + (u - 32);
+    else if (u < 100) {
+      const int f = (u - 64) * 8, tap = f >> 5, ch = f & 31;   // 8 fp16 weights of one tap
+      src = gWd + tap * G::H32 + 32 * cc + ch;
     }
+    return *reinterpret_cast<const uint4*>(src);
+  };
+  auto tab_store = [&](int cc, uint4 v) {
+    if (tid < 100) reinterpret_cast<uint4*>(Tb + (cc & 1) * G::TAB)[tid] = v;
   };
 
   // ---- 1. input tile (+halo) -> LDS (int8; zero outside the image and in the K padding), tables of chunk 0
@@ -106,29 +110,41 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
     constexpr int GPR = G::CINP / 8, CG = CIN / 8;
     constexpr int NU = G::PINP * GPR, NIT = (NU + NW * 64 - 1) / (NW * 64);
     const int8_t* Xb = X + (size_t)b * H * W * CIN;
+    // every prologue load issued branch-free before the first LDS store (see tab_load)
     long xin[NIT];
+    uint32_t okm = 0;
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int u = tid + NW * 64 * i;
       const int p = u / GPR, g = u - p * GPR;
-      xin[i] = 0;
-      if (u < NU && p < G::PIN && g < CG) {
-        const int py = p / G::IW, px = p - py * G::IW;
-        const int iy = iy0 + py, ix = ix0 + px;
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W)
-          xin[i] = *reinterpret_cast<const long*>(Xb + ((size_t)iy * W + ix) * CIN + g * 8);
-      }
+      const int py = p / G::IW, px = p - py * G::IW;
+      const int iy = iy0 + py, ix = ix0 + px;
+      const bool ok = u < NU && p < G::PIN && g < CG && iy >= 0 && iy < H && ix >= 0 && ix < W;
+      xin[i] = *reinterpret_cast<const long*>(Xb + (ok ? ((size_t)iy * W + ix) * CIN + g * 8 : 0));
+      okm |= (uint32_t)ok << i;
     }
+    constexpr int NRQ = (G::NPO + NW * 64 - 1) / (NW * 64);
+    RQ16 rqp[NRQ];
+#pragma unroll
+    for (int j = 0; j < NRQ; ++j) {
+      const int u = tid + NW * 64 * j;
+      rqp[j] = gRqP[u < G::NPO ? u : 0];
+    }
+    const uint4 tab0 = tab_load(0);
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int u = tid + NW * 64 * i;
       if (u < NU) {
         const int p = u / GPR, g = u - p * GPR;
-        *reinterpret_cast<long*>(Xs + p * G::XSB + g * 8) = xin[i];
+        *reinterpret_cast<long*>(Xs + p * G::XSB + g * 8) = ((okm >> i) & 1u) ? xin[i] : 0;
       }
     }
-    for (int u = tid; u < G::NPO; u += NW * 64) RqP[u] = gRqP[u];
-    stage_tables(0);
+#pragma unroll
+    for (int j = 0; j < NRQ; ++j) {
+      const int u = tid + NW * 64 * j;
+      if (u < G::NPO) RqP[u] = rqp[j];
+    }
+    tab_store(0, tab0);
   }
 
   uint32_t pvmask = 0;   // validity of this lane's expand pixels (inside the image): the depthwise zero padding
@@ -157,8 +173,23 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
   }
   __syncthreads();
 
+  // expand weight fragments prefetched one chunk ahead (branch-free: rows past HID reload a valid row and are zeroed
+  // at use)
+  long ca0[G::KSE], ca1[G::KSE];
+  auto ew_load = [&](int cc, long* a0_, long* a1_) {
+    cc = cc < G::NCH ? cc : G::NCH - 1;
+    const int h0 = 32 * cc + r16 < HID ? 32 * cc + r16 : r16, h1 = 32 * cc + 16 + r16 < HID ? 32 * cc + 16 + r16 : r16;
+#pragma unroll
+    for (int ks = 0; ks < G::KSE; ++ks) {
+      a0_[ks] = *reinterpret_cast<const long*>(We + (size_t)h0 * G::KPE + 32 * ks + 8 * kg);
+      a1_[ks] = *reinterpret_cast<const long*>(We + (size_t)h1 * G::KPE + 32 * ks + 8 * kg);
+    }
+  };
+  if constexpr (EXPAND) ew_load(0, ca0, ca1);
+
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
+    const uint4 tab_next = tab_load(c + 1 < G::NCH ? c + 1 : c);   // stored after this chunk's depthwise
     const uint8_t* tb = Tb + (c & 1) * G::TAB;
     const RQ16* rqE = reinterpret_cast<const RQ16*>(tb);
     const RQ16* rqD = rqE + 32;
@@ -183,12 +214,15 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
         *reinterpret_cast<f16x8*>(Es + p * G::ES + 8 * g) = o;
       }
     } else {
-      long a0[G::KSE], a1[G::KSE];
+      long a0[G::KSE], a1[G::KSE], na0[G::KSE], na1[G::KSE];
       const int h0 = 32 * c + r16, h1 = 32 * c + 16 + r16;
+      ew_load(c + 1, na0, na1);   // next chunk's fragments, in flight across this chunk
 #pragma unroll
       for (int ks = 0; ks < G::KSE; ++ks) {
-        a0[ks] = h0 < HID ? *reinterpret_cast<const long*>(We + (size_t)h0 * G::KPE + 32 * ks + 8 * kg) : 0;
-        a1[ks] = h1 < HID ? *reinterpret_cast<const long*>(We + (size_t)h1 * G::KPE + 32 * ks + 8 * kg) : 0;
+        a0[ks] = h0 < HID ? ca0[ks] : 0;
+        a1[ks] = h1 < HID ? ca1[ks] : 0;
+        ca0[ks] = na0[ks];
+        ca1[ks] = na1[ks];
       }
       RQ16 r0[4], r1[4];
 #pragma unroll
@@ -252,7 +286,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
         for (int t = 0; t < G::NCT; ++t) acc[qi][t] = mfma_i8(pa[t], bf, acc[qi][t]);
       }
     }
-    if (c + 1 < G::NCH) stage_tables(c + 1);   // buffer (c+1)&1 was last read in chunk c-1
+    if (c + 1 < G::NCH) tab_store(c + 1, tab_next);   // buffer (c+1)&1 was last read in chunk c-1
   }
 
   // ---- 5. epilogue: requant to the block's output scale (+ residual join + rescale) -> int8 NHWC
