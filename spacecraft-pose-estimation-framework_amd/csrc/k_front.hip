@@ -178,6 +178,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
 #pragma unroll
     for (int qi = 0; qi < QPW; qi += 2) {
       const int oy = wave * QPW + qi, ox = r16;
+      const T* xb = Xs + (oy * SW + ox) * XS + 8 * kg;   // tap (r, kx) at a constant offset: ds_read immediates
       float a0[8], a1[8];
 #pragma unroll
       for (int e = 0; e < 8; ++e) a0[e] = a1[e] = Sb[8 * kg + e];
@@ -188,7 +189,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
         for (int ky = 0; ky < 3; ++ky) w[ky].load(Sl + (ky * 3 + kx) * 32 + 8 * kg);
         x8 v[4];
 #pragma unroll
-        for (int r = 0; r < 4; ++r) v[r] = *reinterpret_cast<const x8*>(Xs + ((oy + r) * SW + (ox + kx)) * XS + 8 * kg);
+        for (int r = 0; r < 4; ++r) v[r] = *reinterpret_cast<const x8*>(xb + (r * SW + kx) * XS);
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -197,12 +198,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
             a1[e] = fmaf((float)v[ky + 1][e], w[ky][e], a1[e]);
           }
       }
-      x8 bf0, bf1;
-#pragma unroll
-      for (int e = 0; e < 8; ++e) {
-        bf0[e] = (T)fmaxf(a0[e], 0.f);
-        bf1[e] = (T)fmaxf(a1[e], 0.f);
-      }
+      const x8 bf0 = relu_cvt8<DT>(a0), bf1 = relu_cvt8<DT>(a1);
       f32x4 acc0 = {pb.x, pb.y, pb.z, pb.w}, acc1 = acc0;   // bias as MFMA C (same order as the block kernels)
       acc0 = DT::mfma(pa, bf0, acc0);
       acc1 = DT::mfma(pa, bf1, acc1);
@@ -228,9 +224,7 @@ __global__ __launch_bounds__(NW * 64) void front_kernel(
 #pragma unroll
         for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wt[e], a8[e]);
       }
-    x8 bf;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
+    const x8 bf = relu_cvt8<DT>(a8);
     f32x4 acc = {pb.x, pb.y, pb.z, pb.w};      // bias as MFMA C (same order as the block kernels)
     acc = DT::mfma(pa, bf, acc);
     store(oy, ox, acc);

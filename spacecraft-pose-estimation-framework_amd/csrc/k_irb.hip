@@ -440,11 +440,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
                 a1[e] = fmaf((float)v[ky + 1][e], w[ky][e], a1[e]);
               }
           }
-#pragma unroll
-          for (int e = 0; e < 8; ++e) {
-            bf0[e] = (T)fmaxf(a0[e], 0.f);
-            bf1[e] = (T)fmaxf(a1[e], 0.f);
-          }
+          bf0 = relu_cvt8<DT>(a0);
+          bf1 = relu_cvt8<DT>(a1);
         }
 #pragma unroll
         for (int t = 0; t < G::NCTW; ++t) {
@@ -476,8 +473,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wt[e], a8[e]);
           }
-#pragma unroll
-        for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
+        bf = relu_cvt8<DT>(a8);
       }
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) {

@@ -306,11 +306,8 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
                   a1[e] = fmaf((float)v[ky + 1][e], w[ky][e], a1[e]);
                 }
             }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              bf0[e] = (T)fmaxf(a0[e], 0.f);
-              bf1[e] = (T)fmaxf(a1[e], 0.f);
-            }
+            bf0 = relu_cvt8<DT>(a0);
+            bf1 = relu_cvt8<DT>(a1);
           }
 #pragma unroll
           for (int t = 0; t < G::NCTW; ++t) {
@@ -337,8 +334,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 #pragma unroll
                 for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wt[e], a8[e]);
               }
-#pragma unroll
-            for (int e = 0; e < 8; ++e) bf[e] = (T)fmaxf(a8[e], 0.f);
+            bf = relu_cvt8<DT>(a8);
           }
 #pragma unroll
           for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);

@@ -67,6 +67,35 @@ __device__ __forceinline__ typename DT::x4 relu_cvt4(f32x4 v) {
   return o;
 }
 
+// ReLU + round of 8 fp32 values (a depthwise output B fragment): 4 v_cvt_pk + 4 v_pk_max instead of 8 v_max_f32 +
+// 4 v_cvt_pk on fp16 (VALU issue is the limit of the depthwise-heavy kernels)
+// (pairs are built from the scalars: an f32x4 temporary lets the SLP vectorizer turn the producing v_fma_mix chain
+// into v_cvt + v_pk_fma_f32, which issues more instructions)
+template <typename DT>
+__device__ __forceinline__ typename DT::x8 relu_cvt8(const float a[8]) {
+  typename DT::x8 o;
+  if constexpr (__is_same(typename DT::T, _Float16)) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const h2 z = {(_Float16)0.0f, (_Float16)0.0f};
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      // the empty asm keeps the fp32 values: otherwise the producing FMA and the convert fuse into one
+      // v_fma_mixlo/hi_f16 (a single rounding to fp16), which differs from the unfused kernels' fp32 -> fp16
+      // double rounding in rare ties (1 ulp; test_fused_blocks_bit_identical_to_unfused)
+      float x0 = a[e], x1 = a[e + 1];
+      asm("" : "+v"(x0), "+v"(x1));
+      h2 p = {(_Float16)x0, (_Float16)x1};
+      p = __builtin_elementwise_max(p, z);
+      o[e] = p[0];
+      o[e + 1] = p[1];
+    }
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (typename DT::T)fmaxf(a[e], 0.f);
+  }
+  return o;
+}
+
 // 8 consecutive depthwise weights kept in their storage type (fp16: 4 VGPRs, read by v_fma_mix directly)
 template <typename DT, bool H = (sizeof(typename DT::DW) == 2)>
 struct DW8 {
