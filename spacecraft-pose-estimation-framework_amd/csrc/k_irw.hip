@@ -376,8 +376,6 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 // (variant, cin, hidden, cout, stride, TH x TW tile, residual, expand waves, depthwise waves, cout groups).
 // Variant 0 is the default; others are alternatives for tuning sweeps (SPEF_OPT_IRB_VARIANT).
 #define SPEF_IRW_TABLE(X)                                                   \
-  X(0, 32, 192, 32, 1, 8, 16, true, 4, 4, 1)       /* blocks 5-6   */       \
-  X(1, 32, 192, 32, 1, 8, 16, true, 2, 4, 1)                                \
   X(0, 64, 384, 64, 1, 16, 16, true, 4, 8, 1)      /* blocks 8-10  */       \
   X(1, 64, 384, 64, 1, 16, 16, true, 4, 4, 1)                               \
   X(0, 64, 384, 96, 1, 16, 16, false, 4, 4, 1)     /* block 11     */       \
@@ -390,6 +388,8 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   X(1, 160, 960, 160, 1, 8, 8, true, 4, 8, 2)
 // Blocks 2-4 stay on the slab kernel (measured: the wave-specialised form is 0-70 % slower there -- the stride-2
 // input tiles make the double-buffered slab too large for more than one or two workgroups per CU).
+// Blocks 5-6 (32 -> 192 -> 32, 64x64 maps) moved back to the slab kernel (8x16 tiles, 4 waves) once its prologue
+// loads were branch-free and its expand weights prefetched: 76 us vs 85 us here.
 // Block 17 (160 -> 960 -> 320) stays on the slab kernel: with 20 output-channel tiles the depthwise waves carry
 // too many accumulators (measured 72-80 us here vs 61 us slab).
 

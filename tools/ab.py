@@ -36,12 +36,12 @@ def main():
         for tag, lib in ((('A', a), ('B', b)) if r % 2 == 0 else (('B', b), ('A', a))):
             for k, v in run(lib).items():
                 acc[tag][k].append(v)
-    keys = sorted(acc['A'], key=lambda k: -sum(acc['A'][k]) / len(acc['A'][k]))
+    mean = lambda v: sum(v) / len(v) if v else float('nan')  # noqa: E731
+    keys = sorted(set(acc['A']) | set(acc['B']), key=lambda k: -max(mean(acc['A'].get(k)), mean(acc['B'].get(k)),
+                                                                 key=lambda x: x if x == x else -1))
     print(f'{"A us":>9} {"B us":>9} {"B-A":>8}  kernel   (A={a}, B={b or "in-tree"}, {rounds} rounds)')
     for k in keys:
-        ma = sum(acc['A'][k]) / len(acc['A'][k])
-        vb = acc['B'].get(k)
-        mb = sum(vb) / len(vb) if vb else float('nan')
+        ma, mb = mean(acc['A'].get(k)), mean(acc['B'].get(k))
         print(f'{ma:9.1f} {mb:9.1f} {mb - ma:+8.1f}  {k}')
 
 
