@@ -338,17 +338,17 @@ hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
 // (cin, hidden, cout, stride, TH, TW, residual, waves) for MobileNet-V2 blocks 2-17
 #define SPEF_QIRB_TABLE(X)                                                              \
   X(32, 32, 16, 1, 16, 16, false, 8, false)     /* block 1 (t = 1) */                  \
-  X(16, 96, 24, 2, 8, 16, false, 8, true)       /* block 2      */                     \
+  X(16, 96, 24, 2, 4, 16, false, 4, true)       /* block 2      */                     \
   X(24, 144, 24, 1, 8, 16, true, 4, true)       /* block 3      */                     \
   X(24, 144, 32, 2, 8, 8, false, 4, true)       /* block 4      */                     \
-  X(32, 192, 32, 1, 16, 16, true, 8, true)      /* blocks 5-6   */                     \
+  X(32, 192, 32, 1, 8, 16, true, 4, true)       /* blocks 5-6   */                     \
   X(32, 192, 64, 2, 8, 8, false, 4, true)       /* block 7      */                     \
-  X(64, 384, 64, 1, 16, 16, true, 8, true)      /* blocks 8-10  */                     \
-  X(64, 384, 96, 1, 16, 16, false, 8, true)     /* block 11     */                     \
-  X(96, 576, 96, 1, 16, 16, true, 8, true)      /* blocks 12-13 */                     \
-  X(96, 576, 160, 2, 8, 8, false, 4, true)      /* block 14     */                     \
-  X(160, 960, 160, 1, 8, 8, true, 4, true)      /* blocks 15-16 */                     \
-  X(160, 960, 320, 1, 8, 8, false, 4, true)     /* block 17     */
+  X(64, 384, 64, 1, 8, 16, true, 4, true)       /* blocks 8-10  */                     \
+  X(64, 384, 96, 1, 8, 16, false, 4, true)      /* block 11     */                     \
+  X(96, 576, 96, 1, 8, 16, true, 4, true)       /* blocks 12-13 */                     \
+  X(96, 576, 160, 2, 4, 8, false, 2, true)      /* block 14     */                     \
+  X(160, 960, 160, 1, 4, 8, true, 2, true)      /* blocks 15-16 */                     \
+  X(160, 960, 320, 1, 4, 8, false, 2, true)     /* block 17     */
 
 }  // namespace
 
