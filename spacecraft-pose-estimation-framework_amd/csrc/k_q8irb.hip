@@ -1,9 +1,10 @@
 // Fused INT8 inverted-residual block (QInvertedResidual, src/modeling/common/brevitas_layers.py:57-136) with
 // the integer semantics of oracle/int8_ref.py, bit-exact like the unfused k_q8.hip kernels:
 //
-//   expand   acc = sum q_x q_we (v_mfma_i32_16x16x32_i8) -> requant + ReLU -> u8, kept in LDS as fp16
-//   depthwise acc = sum u8 * q_wd over 9 taps by v_fma_mix_f32 on fp16 operands: every product and partial
-//            sum is an integer below 2^19, so the fp32 accumulation is exact -> requant + ReLU -> u8
+//   expand   acc = sum q_x q_we (v_mfma_i32_16x16x32_i8) -> requant + ReLU -> u8 n, kept in LDS as fp16 1024 + n
+//   depthwise acc = sum (1024 + n) * q_wd over 9 taps by v_fma_mix_f32 on fp16 operands: every product and
+//            partial sum is an integer below 2^21, so the fp32 accumulation is exact -> requant (offset carries
+//            -1024 * M * sum q_wd, blob_q8.py) + ReLU -> u8
 //   project  acc = 128 * sum q_wp + sum (u8 - 128) q_wp (int8 MFMA, unsigned operand offset by -128)
 //            -> requant to the shared signed quantizer (+ residual join + rescale) -> int8
 //
@@ -31,6 +32,29 @@ __device__ __forceinline__ int rq_apply(int acc, const RQ16& r, int lo, int hi) 
   const int64_t t = (int64_t)acc * r.M + r.B;
   const int v = (int)(t >> 32) >> (r.S - 32);
   return min(max(v, lo), hi);   // v_med3_i32
+}
+
+// A requant record held in registers for a whole chunk, with the shift already reduced to S - 32.
+struct RQR {
+  int M, sh;
+  int64_t B;
+  __device__ __forceinline__ void set(const RQ16& r) {
+    M = r.M;
+    sh = r.S - 32;
+    B = r.B;
+  }
+  __device__ __forceinline__ int u8(int acc) const {   // clip(., 0, 255): v_mad_i64_i32, v_ashrrev_i32, v_med3_i32
+    const int v = (int)(((int64_t)acc * M + B) >> 32) >> sh;
+    return min(max(v, 0), 255);
+  }
+};
+
+// Hidden u8 values live in the LDS slab as the fp16 number 1024 + n, i.e. the bit pattern 0x6400 | n (exact: fp16
+// has an 11-bit significand): two values pack into one dword with a shift-or, no int -> float conversion. The
+// depthwise sum then carries + 1024 * sum_taps w, which the packer folded into the depthwise requant offset.
+constexpr uint32_t kF16Bias2 = 0x64006400u;   // two fp16 1024.0
+__device__ __forceinline__ uint32_t pack_biased(int lo, int hi) {
+  return ((uint32_t)hi << 16) | (uint32_t)lo | kF16Bias2;
 }
 
 __device__ __forceinline__ i32x4_t mfma_i8(long a, long b, i32x4_t c) {
@@ -147,9 +171,13 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
     tab_store(0, tab0);
   }
 
-  uint32_t pvmask = 0;   // validity of this lane's expand pixels (inside the image): the depthwise zero padding
+  // validity of this lane's expand pixels (inside the image): the depthwise zero padding. Interior tiles (whole
+  // input tile inside the image) need no mask (workgroup-uniform branch).
+  const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + G::IH <= H && ix0 + G::IW <= W;
+  uint32_t pvmask = 0;
 #pragma unroll
   for (int j = 0; j < G::EPT; ++j) {
+    if (interior) break;
     const int p = (wave + NW * j) * 16 + r16;
     if (p < G::PIN) {
       const int py = p / G::IW, px = p - py * G::IW;
@@ -208,10 +236,12 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
       for (int u = tid; u < G::PIN * 4; u += NW * 64) {
         const int p = u >> 2, g = u & 3;
         const uint2 v = *reinterpret_cast<const uint2*>(Xs + p * G::XSB + 8 * g);
-        f16x8 o;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) o[e] = (_Float16)(int)(((e < 4 ? v.x : v.y) >> (8 * (e & 3))) & 0xffu);
-        *reinterpret_cast<f16x8*>(Es + p * G::ES + 8 * g) = o;
+        uint4 o;   // byte n -> fp16 1024 + n (0x6400 | n), two per dword
+        o.x = (v.x & 0xffu) | ((v.x & 0xff00u) << 8) | kF16Bias2;
+        o.y = ((v.x >> 16) & 0xffu) | ((v.x >> 8) & 0xff0000u) | kF16Bias2;
+        o.z = (v.y & 0xffu) | ((v.y & 0xff00u) << 8) | kF16Bias2;
+        o.w = ((v.y >> 16) & 0xffu) | ((v.y >> 8) & 0xff0000u) | kF16Bias2;
+        *reinterpret_cast<uint4*>(Es + p * G::ES + 8 * g) = o;
       }
     } else {
       long a0[G::KSE], a1[G::KSE], na0[G::KSE], na1[G::KSE];
@@ -224,11 +254,11 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
         ca0[ks] = na0[ks];
         ca1[ks] = na1[ks];
       }
-      RQ16 r0[4], r1[4];
+      RQR r0[4], r1[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        r0[r] = rqE[4 * kg + r];
-        r1[r] = rqE[16 + 4 * kg + r];
+        r0[r].set(rqE[4 * kg + r]);
+        r1[r].set(rqE[16 + 4 * kg + r]);
       }
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
@@ -241,26 +271,24 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
           e0 = mfma_i8(a0[ks], bx, e0);
           e1 = mfma_i8(a1[ks], bx, e1);
         }
-        const bool pv = (pvmask >> j) & 1u;
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        h4 o0, o1;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          o0[r] = (_Float16)(pv ? rq_apply(e0[r], r0[r], 0, 255) : 0);
-          o1[r] = (_Float16)(pv ? rq_apply(e1[r], r1[r], 0, 255) : 0);
+        uint2 u0 = {pack_biased(r0[0].u8(e0[0]), r0[1].u8(e0[1])), pack_biased(r0[2].u8(e0[2]), r0[3].u8(e0[3]))};
+        uint2 u1 = {pack_biased(r1[0].u8(e1[0]), r1[1].u8(e1[1])), pack_biased(r1[2].u8(e1[2]), r1[3].u8(e1[3]))};
+        if (!interior && !((pvmask >> j) & 1u)) {   // pixel outside the image: the depthwise zero padding (n = 0)
+          u0 = make_uint2(kF16Bias2, kF16Bias2);
+          u1 = u0;
         }
         _Float16* er = Es + (pt * 16 + r16) * G::ES + 4 * kg;
-        *reinterpret_cast<h4*>(er) = o0;
-        *reinterpret_cast<h4*>(er + 16) = o1;
+        *reinterpret_cast<uint2*>(er) = u0;
+        *reinterpret_cast<uint2*>(er + 16) = u1;
       }
     }
     __syncthreads();   // slab and this chunk's tables visible
 
     // ---- 3. depthwise (exact fp32 sums of integer products) -> requant -> offset int8 B fragment; 4. project
     {
-      RQ16 rd[8];
+      RQR rd[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) rd[e] = rqD[8 * kg + e];
+      for (int e = 0; e < 8; ++e) rd[e].set(rqD[8 * kg + e]);
 #pragma unroll
       for (int qi = 0; qi < G::QPW; ++qi) {
         float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
@@ -274,13 +302,16 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
 #pragma unroll
             for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], (float)w[e], a8[e]);
           }
+        // a8 = exact sum of (1024 + n) * w: the biased depthwise offset in rd[] removes the 1024 * sum w
         uint32_t lo = 0, hi = 0;
 #pragma unroll
         for (int e = 0; e < 8; ++e) {
-          const uint32_t q = (uint32_t)(rq_apply((int)a8[e], rd[e], 0, 255) ^ 0x80) & 0xffu;
+          const uint32_t q = (uint32_t)rd[e].u8((int)a8[e]);
           if (e < 4) lo |= q << (8 * e);
           else hi |= q << (8 * (e - 4));
         }
+        lo ^= 0x80808080u;   // u8 -> the project MFMA's offset int8 (u8 - 128)
+        hi ^= 0x80808080u;
         const long bf = (long)(((uint64_t)hi << 32) | lo);
 #pragma unroll
         for (int t = 0; t < G::NCT; ++t) acc[qi][t] = mfma_i8(pa[t], bf, acc[qi][t]);

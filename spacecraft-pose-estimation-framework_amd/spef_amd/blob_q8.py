@@ -99,12 +99,19 @@ def _rq16(M, B, S, n_pad: int) -> bytes:
 
 
 def _fused_tables(e_rq, d_rq, p_rq, qdw, hidden: int, cout: int) -> bytes:
-    """x2 of an expand block: the fused int8 kernel's per-channel tables (spef_blob.hpp)."""
+    """x2 of an expand block: the fused int8 kernel's per-channel tables (spef_blob.hpp).
+
+    The fused kernel keeps each hidden u8 value n in LDS as the fp16 number 1024 + n (bit pattern 0x6400 | n: no
+    int -> float conversion in the expand epilogue), so its depthwise sum is acc + 1024 * sum_taps q_wd. The
+    depthwise requant offset absorbs that exactly: B' = B - 1024 * M * sum_taps q_wd (same q for every acc)."""
     h32 = (hidden + 31) // 32 * 32
     np_ = (cout + 15) // 16 * 16
+    w9 = qdw[:, 0].reshape(hidden, 9).astype(np.int64)
     wd = np.zeros((9, h32), np.float16)
-    wd[:, :hidden] = qdw[:, 0].reshape(hidden, 9).T          # int8 values, exact in fp16
-    return _rq16(*e_rq, h32) + _rq16(*d_rq, h32) + _rq16(*p_rq, np_) + wd.tobytes()
+    wd[:, :hidden] = w9.T                                     # int8 values, exact in fp16
+    M, B, S = d_rq
+    B = np.asarray(B, np.int64) - 1024 * np.asarray(M, np.int64) * w9.sum(axis=1)
+    return _rq16(*e_rq, h32) + _rq16(M, B, S, h32) + _rq16(*p_rq, np_) + wd.tobytes()
 
 
 def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None) -> bytes:

@@ -25,6 +25,17 @@ __global__ __launch_bounds__(256) void k(float* out, int n, float s) {
         if constexpr (OP == 5) asm volatile("v_max_f32 %0, %1, %0" : "+v"(a[i]) : "v"(b));
         if constexpr (OP == 6) asm volatile("v_cvt_pk_f16_f32 %0, %1, %2" : "=v"(a[i]) : "v"(a[(i + 1) & 7]), "v"(b));
         if constexpr (OP == 7) asm volatile("v_add_u32 %0, %1, %0" : "+v"(a[i]) : "v"(h));
+        // integer / fp64 ops of the int8 requant epilogue
+        if constexpr (OP == 8)
+          asm volatile("v_mad_i64_i32 %0, vcc, %1, %2, %0" : "+v"(*reinterpret_cast<long*>(&a[i & 6])) : "v"(h), "v"(b) : "vcc");
+        if constexpr (OP == 9)
+          asm volatile("v_fma_f64 %0, %1, %2, %0" : "+v"(*reinterpret_cast<double*>(&a[i & 6])) : "v"(*reinterpret_cast<double*>(&a[(i + 2) & 6])), "v"(*reinterpret_cast<double*>(&a[(i + 4) & 6])));
+        if constexpr (OP == 10) asm volatile("v_mul_hi_i32 %0, %1, %0" : "+v"(a[i]) : "v"(h));
+        if constexpr (OP == 11) asm volatile("v_med3_i32 %0, %1, %0, %2" : "+v"(a[i]) : "v"(h), "v"(b));
+        if constexpr (OP == 12) asm volatile("v_cvt_f32_i32 %0, %1" : "=v"(a[i]) : "v"(h));
+        if constexpr (OP == 13) asm volatile("v_cvt_f64_i32 %0, %1" : "=v"(*reinterpret_cast<double*>(&a[i & 6])) : "v"(h));
+        if constexpr (OP == 14) asm volatile("v_mul_i32_i24 %0, %1, %0" : "+v"(a[i]) : "v"(h));
+        if constexpr (OP == 15) asm volatile("v_mul_lo_u32 %0, %1, %0" : "+v"(a[i]) : "v"(h));
       }
     }
   }
@@ -39,13 +50,14 @@ int main() {
   int ncu = 256, wgs_per_cu = 8;   // 256-thread WGs: 8 per CU = 32 waves/CU = 8 waves/SIMD
   const int n = 2000;
   const char* names[] = {"v_fma_f32", "v_fma_mix_f32", "v_cvt_f32_f16", "v_pk_fma_f32", "v_dot2_f32_f16", "v_max_f32",
-                         "v_cvt_pk_f16_f32", "v_add_u32"};
+                         "v_cvt_pk_f16_f32", "v_add_u32", "v_mad_i64_i32", "v_fma_f64", "v_mul_hi_i32",
+                         "v_med3_i32", "v_cvt_f32_i32", "v_cvt_f64_i32", "v_mul_i32_i24", "v_mul_lo_u32"};
   hipEvent_t e0, e1;
   hipEventCreate(&e0);
   hipEventCreate(&e1);
-  for (int waves_per_simd : {8, 2, 1}) {
+  for (int waves_per_simd : {8, 2}) {
     int wgs = ncu * waves_per_simd;   // 4 waves per WG -> waves_per_simd WGs per CU
-    for (int op = 0; op < 8; ++op) {
+    for (int op = 0; op < 16; ++op) {
       for (int rep = 0; rep < 2; ++rep) {
         hipEventRecord(e0);
         switch (op) {
@@ -57,6 +69,14 @@ int main() {
           case 5: k<5><<<wgs, 256>>>(out, n, 1.f); break;
           case 6: k<6><<<wgs, 256>>>(out, n, 1.f); break;
           case 7: k<7><<<wgs, 256>>>(out, n, 1.f); break;
+          case 8: k<8><<<wgs, 256>>>(out, n, 1.f); break;
+          case 9: k<9><<<wgs, 256>>>(out, n, 1.f); break;
+          case 10: k<10><<<wgs, 256>>>(out, n, 1.f); break;
+          case 11: k<11><<<wgs, 256>>>(out, n, 1.f); break;
+          case 12: k<12><<<wgs, 256>>>(out, n, 1.f); break;
+          case 13: k<13><<<wgs, 256>>>(out, n, 1.f); break;
+          case 14: k<14><<<wgs, 256>>>(out, n, 1.f); break;
+          case 15: k<15><<<wgs, 256>>>(out, n, 1.f); break;
         }
         hipEventRecord(e1);
         hipEventSynchronize(e1);
