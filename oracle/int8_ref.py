@@ -80,9 +80,9 @@ def bn(sd, prefix):
 
 def fixed(m, b):
     """Per-channel fixed-point form of ``x * m + b``: -> (M int64, B int64 incl. the rounding half, sh int64)
-    with q = (x * M + B) >> sh. |m| * 2**sh in [2**29, 2**30), raised to sh = 32 when |m| < 0.5 (so sh >= 32 and
-    |M| < 2**31 for every realistic conv scale: the fused kernel's 3-instruction requant); sh capped so
-    |b| * 2**sh < 2**61."""
+    with q = (x * M + B) >> sh. sh = 32 exactly when 2**-12 <= |m| < 0.5 (every realistic conv scale: the fused
+    kernel's requant is the high word of one 64-bit multiply-add), otherwise |m| * 2**sh in [2**29, 2**30); sh
+    capped so |b| * 2**sh < 2**61."""
     m = np.atleast_1d(np.asarray(m, np.float64))
     b = np.broadcast_to(np.atleast_1d(np.asarray(b, np.float64)), m.shape)
     M = np.zeros(m.shape, np.int64)
@@ -92,8 +92,10 @@ def fixed(m, b):
         em = math.frexp(abs(m[i]))[1] if m[i] != 0 else -30
         eb = math.frexp(abs(b[i]))[1] if b[i] != 0 else -200
         sh0 = 30 - em
-        if sh0 < 32 and abs(m[i]) < 0.5:
-            sh0 = 32           # |M| < 2**31 still: the kernels take the high word of acc * M + B and shift by sh - 32
+        if 2.0 ** -12 <= abs(m[i]) < 0.5:
+            # sh = 32 exactly: M = rint(m 2**32) in [2**20, 2**31) keeps the requant error below 2**-13 LSB for
+            # outputs in the 8-bit range, and the fused kernels take the high word of acc * M + B with no shift
+            sh0 = 32
         sh = int(min(sh0, 61 - eb, 62))
         assert sh >= 1, (m[i], b[i])
         M[i] = int(np.rint(math.ldexp(m[i], sh)))

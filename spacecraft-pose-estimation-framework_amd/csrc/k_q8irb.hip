@@ -34,18 +34,21 @@ __device__ __forceinline__ int rq_apply(int acc, const RQ16& r, int lo, int hi) 
   return min(max(v, lo), hi);   // v_med3_i32
 }
 
-// A requant record held in registers for a whole chunk, with the shift already reduced to S - 32.
+// A requant record held in registers for a whole chunk, with the shift already reduced to S - 32. SH32 (blob flag 4:
+// every shift of the block is exactly 32): no shift at all, and a constant added to the offset moves the clamped
+// result straight into the encoding the consumer wants (B + (c << 32) adds c to the high word exactly).
+template <bool SH32>
 struct RQR {
   int M, sh;
   int64_t B;
-  __device__ __forceinline__ void set(const RQ16& r) {
+  __device__ __forceinline__ void set(const RQ16& r, int64_t add) {
     M = r.M;
     sh = r.S - 32;
-    B = r.B;
+    B = SH32 ? r.B + add * 4294967296LL : r.B;
   }
-  __device__ __forceinline__ int u8(int acc) const {   // clip(., 0, 255): v_mad_i64_i32, v_ashrrev_i32, v_med3_i32
-    const int v = (int)(((int64_t)acc * M + B) >> 32) >> sh;
-    return min(max(v, 0), 255);
+  __device__ __forceinline__ int hi(int acc) const {   // v_mad_i64_i32 (+ v_ashrrev_i32 unless SH32)
+    const int v = (int)(((int64_t)acc * M + B) >> 32);
+    return SH32 ? v : v >> sh;
   }
 };
 
@@ -53,8 +56,16 @@ struct RQR {
 // has an 11-bit significand): two values pack into one dword with a shift-or, no int -> float conversion. The
 // depthwise sum then carries + 1024 * sum_taps w, which the packer folded into the depthwise requant offset.
 constexpr uint32_t kF16Bias2 = 0x64006400u;   // two fp16 1024.0
-__device__ __forceinline__ uint32_t pack_biased(int lo, int hi) {
-  return ((uint32_t)hi << 16) | (uint32_t)lo | kF16Bias2;
+// expand output: u8 n of two channels -> one dword of fp16 (1024 + n)
+template <bool SH32>
+__device__ __forceinline__ uint32_t expand_pair(const RQR<SH32>& r0, int a0, const RQR<SH32>& r1, int a1) {
+  if constexpr (SH32) {   // the offset carries + 0x6400: clamp to [0x6400, 0x64ff], two low halves -> one v_perm_b32
+    const int v0 = min(max(r0.hi(a0), 0x6400), 0x64ff), v1 = min(max(r1.hi(a1), 0x6400), 0x64ff);
+    return __builtin_amdgcn_perm((uint32_t)v1, (uint32_t)v0, 0x05040100u);
+  } else {
+    const int v0 = min(max(r0.hi(a0), 0), 255), v1 = min(max(r1.hi(a1), 0), 255);
+    return ((uint32_t)v1 << 16) | (uint32_t)v0 | kF16Bias2;
+  }
 }
 
 __device__ __forceinline__ i32x4_t mfma_i8(long a, long b, i32x4_t c) {
@@ -74,6 +85,8 @@ struct QGeom {
   static constexpr int NPO = (COUT + 15) / 16 * 16, NCT = NPO / 16;
   static constexpr int EPT = (PIN16 + NW - 1) / NW;
   static constexpr int POUT16 = TH * TW / 16, QPW = POUT16 / NW;
+  // depthwise row pairs: a wave's consecutive pixel tiles are vertically adjacent rows (16-wide, stride 1)
+  static constexpr bool PAIR = S == 1 && TW == 16 && QPW % 2 == 0;
   static constexpr int TAB = 32 * 16 * 2 + 9 * 32 * 2;   // bytes per chunk: RQ16 expand + depthwise, fp16 weights
   static constexpr int LDS_BYTES = PINP * XSB + PINP * ES * 2 + 2 * TAB + NPO * 16;
   static_assert(POUT16 % NW == 0, "tile split");
@@ -82,7 +95,7 @@ struct QGeom {
   static_assert(!RES || (S == 1 && CIN == COUT), "residual geometry");
 };
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, bool EXPAND>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, bool EXPAND, bool SH32>
 __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
     const int8_t* __restrict__ X, const int8_t* __restrict__ We, const int8_t* __restrict__ Wp,
     const int32_t* __restrict__ pinit, const uint8_t* __restrict__ tabs, int64_t RM, int64_t RB, int RSH,
@@ -254,11 +267,11 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
         ca0[ks] = na0[ks];
         ca1[ks] = na1[ks];
       }
-      RQR r0[4], r1[4];
+      RQR<SH32> r0[4], r1[4];
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        r0[r].set(rqE[4 * kg + r]);
-        r1[r].set(rqE[16 + 4 * kg + r]);
+        r0[r].set(rqE[4 * kg + r], 0x6400);
+        r1[r].set(rqE[16 + 4 * kg + r], 0x6400);
       }
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
@@ -271,8 +284,8 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
           e0 = mfma_i8(a0[ks], bx, e0);
           e1 = mfma_i8(a1[ks], bx, e1);
         }
-        uint2 u0 = {pack_biased(r0[0].u8(e0[0]), r0[1].u8(e0[1])), pack_biased(r0[2].u8(e0[2]), r0[3].u8(e0[3]))};
-        uint2 u1 = {pack_biased(r1[0].u8(e1[0]), r1[1].u8(e1[1])), pack_biased(r1[2].u8(e1[2]), r1[3].u8(e1[3]))};
+        uint2 u0 = {expand_pair(r0[0], e0[0], r0[1], e0[1]), expand_pair(r0[2], e0[2], r0[3], e0[3])};
+        uint2 u1 = {expand_pair(r1[0], e1[0], r1[1], e1[1]), expand_pair(r1[2], e1[2], r1[3], e1[3])};
         if (!interior && !((pvmask >> j) & 1u)) {   // pixel outside the image: the depthwise zero padding (n = 0)
           u0 = make_uint2(kF16Bias2, kF16Bias2);
           u1 = u0;
@@ -286,35 +299,85 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
 
     // ---- 3. depthwise (exact fp32 sums of integer products) -> requant -> offset int8 B fragment; 4. project
     {
-      RQR rd[8];
+      RQR<SH32> rd[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) rd[e].set(rqD[8 * kg + e]);
+      for (int e = 0; e < 8; ++e) rd[e].set(rqD[8 * kg + e], -128);
+      // a8 = exact sum of (1024 + n) * w: the biased depthwise offset in rd[] removes the 1024 * sum w. Output: the
+      // project MFMA's offset int8 u8 - 128 (SH32: the offset already carries the -128)
+      auto bfrag = [&](const float* a8) -> long {
+        uint32_t lo, hi;
+        if constexpr (SH32) {
+          int q[8];
 #pragma unroll
-      for (int qi = 0; qi < G::QPW; ++qi) {
-        float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+          for (int e = 0; e < 8; ++e) q[e] = min(max(rd[e].hi((int)a8[e]), -128), 127);
+          const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)q[1], (uint32_t)q[0], 0x0c0c0400u);
+          const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)q[3], (uint32_t)q[2], 0x0c0c0400u);
+          const uint32_t p45 = __builtin_amdgcn_perm((uint32_t)q[5], (uint32_t)q[4], 0x0c0c0400u);
+          const uint32_t p67 = __builtin_amdgcn_perm((uint32_t)q[7], (uint32_t)q[6], 0x0c0c0400u);
+          lo = __builtin_amdgcn_perm(p23, p01, 0x05040100u);
+          hi = __builtin_amdgcn_perm(p67, p45, 0x05040100u);
+        } else {
+          lo = 0;
+          hi = 0;
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-          for (int ky = 0; ky < 3; ++ky) {
-            const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
-            const f16x8 v = *reinterpret_cast<const f16x8*>(Es + p * G::ES + 8 * kg);
-            const f16x8 w = *reinterpret_cast<const f16x8*>(wd + (ky * 3 + kx) * 32 + 8 * kg);
-#pragma unroll
-            for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], (float)w[e], a8[e]);
+          for (int e = 0; e < 8; ++e) {
+            const uint32_t q = (uint32_t)min(max(rd[e].hi((int)a8[e]), 0), 255);
+            if (e < 4) lo |= q << (8 * e);
+            else hi |= q << (8 * (e - 4));
           }
-        // a8 = exact sum of (1024 + n) * w: the biased depthwise offset in rd[] removes the 1024 * sum w
-        uint32_t lo = 0, hi = 0;
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          const uint32_t q = (uint32_t)rd[e].u8((int)a8[e]);
-          if (e < 4) lo |= q << (8 * e);
-          else hi |= q << (8 * (e - 4));
+          lo ^= 0x80808080u;
+          hi ^= 0x80808080u;
         }
-        lo ^= 0x80808080u;   // u8 -> the project MFMA's offset int8 (u8 - 128)
-        hi ^= 0x80808080u;
-        const long bf = (long)(((uint64_t)hi << 32) | lo);
+        return (long)(((uint64_t)hi << 32) | lo);
+      };
+      if constexpr (G::PAIR) {
+        // Two vertically adjacent output rows per step (tiles qi, qi+1 = rows oy, oy+1 of the same 16 columns): per
+        // tap column the 3 weights and the 4 input rows are read once and feed both rows (21 instead of 36
+        // ds_read_b128 per 2 x 16 pixels x 8 channels), as in the fp16 kernel
 #pragma unroll
-        for (int t = 0; t < G::NCT; ++t) acc[qi][t] = mfma_i8(pa[t], bf, acc[qi][t]);
+        for (int qi = 0; qi < G::QPW; qi += 2) {
+          float a0[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f}, a1[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) {
+            f16x8 w[3], v[4];
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) w[ky] = *reinterpret_cast<const f16x8*>(wd + (ky * 3 + kx) * 32 + 8 * kg);
+#pragma unroll
+            for (int r = 0; r < 4; ++r)
+              v[r] = *reinterpret_cast<const f16x8*>(Es + ((oyq[qi] + r) * G::IW + oxq[qi] + kx) * G::ES + 8 * kg);
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                a0[e] = fmaf((float)v[ky][e], (float)w[ky][e], a0[e]);
+                a1[e] = fmaf((float)v[ky + 1][e], (float)w[ky][e], a1[e]);
+              }
+          }
+          const long bf0 = bfrag(a0), bf1 = bfrag(a1);
+#pragma unroll
+          for (int t = 0; t < G::NCT; ++t) {
+            acc[qi][t] = mfma_i8(pa[t], bf0, acc[qi][t]);
+            acc[qi + 1][t] = mfma_i8(pa[t], bf1, acc[qi + 1][t]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int qi = 0; qi < G::QPW; ++qi) {
+          float a8[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+            for (int ky = 0; ky < 3; ++ky) {
+              const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
+              const f16x8 v = *reinterpret_cast<const f16x8*>(Es + p * G::ES + 8 * kg);
+              const f16x8 w = *reinterpret_cast<const f16x8*>(wd + (ky * 3 + kx) * 32 + 8 * kg);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], (float)w[e], a8[e]);
+            }
+          const long bf = bfrag(a8);
+#pragma unroll
+          for (int t = 0; t < G::NCT; ++t) acc[qi][t] = mfma_i8(pa[t], bf, acc[qi][t]);
+        }
       }
     }
     if (c + 1 < G::NCH) tab_store(c + 1, tab_next);   // buffer (c+1)&1 was last read in chunk c-1
@@ -347,7 +410,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
   }
 }
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, bool EXPAND>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, bool EXPAND, bool SH32>
 hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const int32_t* pinit, const uint8_t* tabs,
                     int64_t rm, int64_t rb, int rs, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
   using G = QGeom<CIN, HID, COUT, S, TH, TW, RES, NW>;
@@ -355,7 +418,7 @@ hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  auto k = q_irb_kernel<CIN, HID, COUT, S, TH, TW, RES, NW, EXPAND>;
+  auto k = q_irb_kernel<CIN, HID, COUT, S, TH, TW, RES, NW, EXPAND, SH32>;
   static bool attr_set = false;
   if (!attr_set && G::LDS_BYTES > 65536) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
@@ -391,12 +454,15 @@ bool q_irb_supported(int cin, int hid, int cout, int stride, bool res, bool expa
   return false;
 }
 
-hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, const int8_t* x, const int8_t* we,
-                        const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm, int64_t rb, int rs,
-                        int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
-#define SPEF_QIRB_CASE(CI, HI, CO, ST, TH_, TW_, RS, NW_, EX)                                          \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS && expand == EX)                 \
-    return q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, OH, OW, s);
+hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, bool sh32, const int8_t* x,
+                        const int8_t* we, const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm,
+                        int64_t rb, int rs, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
+#define SPEF_QIRB_CASE(CI, HI, CO, ST, TH_, TW_, RS, NW_, EX)                                                         \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS && expand == EX)                                \
+    return sh32 ? q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX, true>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, \
+                                                                        OH, OW, s)                                      \
+                : q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX, false>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, \
+                                                                         OH, OW, s);
   SPEF_QIRB_TABLE(SPEF_QIRB_CASE)
 #undef SPEF_QIRB_CASE
   return hipErrorNotSupported;

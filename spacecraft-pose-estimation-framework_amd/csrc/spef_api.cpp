@@ -420,7 +420,7 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
         HIP_TRY(prof_launch(c, s, key, (double)M * op.cin + (double)M2 * op.cout + (double)op.hidden * (op.cin + op.cout + 9),
                             2.0 * M * op.cin * op.hidden + 18.0 * M2 * op.hidden + 2.0 * M2 * op.hidden * op.cout, [&] {
           return launch_q_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, op.expand != 1,
-                              (const int8_t*)x,
+                              (op.flags & 4u) != 0, (const int8_t*)x,
                               ptr<int8_t>(c, op.w0), ptr<int8_t>(c, op.w2), ptr<int32_t>(c, op.x0),
                               ptr<uint8_t>(c, op.x2), r3[0], r3[1], (int)r3[2], (int8_t*)y, B, h, w, OH, OW, s);
         }));

@@ -18,6 +18,7 @@
 //   OP_QIRB  w0/b0 expand int8 [Np][Kp64] + RQ (absent if t==1); w1/b1 dw int8 [9][hidden] + RQ;
 //            w2/b2 project int8 [Np][Kp64] + RQ; x0 int32 [Np] project accumulator init (128 * sum_k q_w);
 //            x1 int64 [3] residual-join rescale (R, RB, RS) when flags & 1; flags & 2: unsigned block input;
+//            flags & 4: every x2 requant shift is exactly 32;
 //            x2 fused-kernel tables (expand ops): RQ16 expand [H32] | RQ16 depthwise [H32] | RQ16 project [Np] |
 //            depthwise weights fp16 [9][H32] (H32 = hidden rounded up to 32; RQ16 = {int32 M, int32 S, int64 B})
 //   OP_QLAST w0 int8 [Np][Kp64], b0 RQ

@@ -122,7 +122,7 @@ hipError_t launch_q_gemm(const QGemmArgs& a, hipStream_t s);
 hipError_t launch_q_pool(const uint8_t* x, int8_t* p, int B, int HW, int C, int tb, hipStream_t s);
 // Fused int8 inverted-residual block (expand blocks 2-17; k_q8irb.hip). tabs = blob OP_QIRB x2.
 bool q_irb_supported(int cin, int hid, int cout, int stride, bool res, bool expand);
-hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, const int8_t* x, const int8_t* we,
+hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, bool sh32, const int8_t* x, const int8_t* we,
                         const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm, int64_t rb, int rs,
                         int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 // int8 (is_unsigned 0) or u8 codes -> fp32 code * scale.

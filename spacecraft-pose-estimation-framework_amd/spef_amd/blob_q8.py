@@ -39,8 +39,8 @@ def _bn(sd, prefix):
 
 
 def fixed(m, b):
-    """x * m + b in fixed point: (M, B incl. rounding half, sh), |m| 2**sh in [2**29, 2**30) raised to sh = 32 when
-    |m| < 0.5, |b| 2**sh < 2**61 (oracle/int8_ref.fixed states the same rule)."""
+    """x * m + b in fixed point: (M, B incl. rounding half, sh): sh = 32 when 2**-12 <= |m| < 0.5, otherwise
+    |m| 2**sh in [2**29, 2**30); |b| 2**sh < 2**61 (oracle/int8_ref.fixed states the same rule)."""
     m = np.atleast_1d(np.asarray(m, np.float64))
     b = np.broadcast_to(np.atleast_1d(np.asarray(b, np.float64)), m.shape)
     M = np.zeros(m.shape, np.int64)
@@ -50,8 +50,10 @@ def fixed(m, b):
         em = math.frexp(abs(m[i]))[1] if m[i] != 0 else -30
         eb = math.frexp(abs(b[i]))[1] if b[i] != 0 else -200
         sh0 = 30 - em
-        if sh0 < 32 and abs(m[i]) < 0.5:
-            sh0 = 32           # |M| < 2**31 still: the kernels take the high word of acc * M + B and shift by sh - 32
+        if 2.0 ** -12 <= abs(m[i]) < 0.5:
+            # sh = 32 exactly: M = rint(m 2**32) in [2**20, 2**31) keeps the requant error below 2**-13 LSB for
+            # outputs in the 8-bit range, and the fused kernels take the high word of acc * M + B with no shift
+            sh0 = 32
         sh = int(min(sh0, 61 - eb, 62))
         if sh < 1:
             raise ValueError(f'requant scale out of range (m={m[i]}, b={b[i]})')
@@ -114,8 +116,11 @@ def _fused_tables(e_rq, d_rq, p_rq, qdw, hidden: int, cout: int) -> bytes:
     return _rq16(*e_rq, h32) + _rq16(M, B, S, h32) + _rq16(*p_rq, np_) + wd.tobytes()
 
 
-def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None) -> bytes:
-    """Pack a reference-layout FP32 state_dict + activation scales into an int8 blob (URSONet head)."""
+def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None, shift32: bool = True) -> bytes:
+    """Pack a reference-layout FP32 state_dict + activation scales into an int8 blob (URSONet head).
+
+    ``shift32=False`` never sets the "every shift is 32" flag, so the fused blocks run their general-shift kernel
+    variant (same results; kept for the tests)."""
     arch = arch or arch_from_state_dict(sd)
     if arch.head != 'ursonet':
         raise NotImplementedError('the int8 path mirrors QURSONetHead (ursonet.py:36-93) only')
@@ -169,6 +174,8 @@ def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None) -> bytes:
             R, RB, RS = fixed(s_q / s_next, 0.0)
             x1 = data.add(np.array([R[0], RB[0], RS[0]], np.int64).tobytes())
         flags = (1 if blk.residual else 0) | (2 if s_q is None else 0)
+        if shift32 and fusable and all(np.all(r[2] == 32) for r in (e_rq, d_rq, p_rq)):
+            flags |= 4       # every fused requant shift is exactly 32: the kernel's shift-free variant
         ops.append((OP_QIRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, flags,
                     e_w, e_b, d_w, d_b, p_w, p_b, data.add(init.tobytes()), x1, x2))
 

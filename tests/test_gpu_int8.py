@@ -73,3 +73,18 @@ def test_int8_batch_64_512(q8):
     ro, rp = Q.int8_forward(fr[idx], sd, qp)
     np.testing.assert_array_equal(o.cpu().numpy()[idx], ro)
     np.testing.assert_array_equal(p.cpu().numpy()[idx], rp)
+
+
+def test_int8_general_shift_kernels_bit_exact(q8):
+    """The fused blocks' general-shift variant (blob flag 4 cleared) gives the same bits as the shift-free one."""
+    from spef_amd.engine import Engine
+    _, sd, qp = q8
+    fr = synth_frames(2, 96, 64, 13)
+    e = Engine(pack_int8(sd, qp, shift32=False), 'cuda:0')
+    try:
+        o, p = e.forward(torch.from_numpy(fr).cuda())
+        ro, rp = Q.int8_forward(fr, sd, qp)
+        np.testing.assert_array_equal(o.cpu().numpy(), ro)
+        np.testing.assert_array_equal(p.cpu().numpy(), rp)
+    finally:
+        e.close()

@@ -72,3 +72,10 @@ def test_bit_width_config():
     check_bit_width({'image': '8', 'first_conv': '(8, 8)', 'inverted_residual': ['[(8, 8), (8, 8), (8,)]']})
     with pytest.raises(NotImplementedError):
         check_bit_width({'image': '8', 'first_conv': '(4, 4)'})
+
+
+def test_fixed_point_shift_rule():
+    """sh = 32 exactly for 2**-12 <= |m| < 0.5 (the fused kernels' shift-free requant), finer shifts below."""
+    M_, B_, S_ = Q.fixed(np.array([0.3, 1e-2, 2.0 ** -12, 1e-5, 0.7]), np.zeros(5))
+    assert list(S_[:3]) == [32, 32, 32] and S_[3] > 32 and S_[4] < 32
+    assert np.all(np.abs(M_) < 2 ** 31)
