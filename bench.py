@@ -113,9 +113,13 @@ def main():
     ap.add_argument('--cpu-threads', type=int, default=16)
     ap.add_argument('--cpu-batch', type=int, default=64)
     ap.add_argument('--cpu-batches', type=int, default=3)
-    ap.add_argument('--traffic', default=os.path.join(ROOT, 'profiles', 'r01_pmc_traffic.json'),
-                    help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic')
+    ap.add_argument('--traffic', default=None,
+                    help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic (default: '
+                         'profiles/r01_pmc_traffic.json, r01_int8_pmc_traffic.json for --dtype int8)')
     args = ap.parse_args()
+    if args.traffic is None:
+        args.traffic = os.path.join(ROOT, 'profiles', 'r01_int8_pmc_traffic.json' if args.dtype == 'int8'
+                                    else 'r01_pmc_traffic.json')
 
     import numpy as np
     import torch

@@ -22,12 +22,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def short_name(full: str) -> str:
     """'void spef::pw_kernel<spef::F16, 6, 2, 1>(...)' -> 'pw_kernel<F16,6,2,1>' (bench.py key form)."""
-    n = full.split('(')[0].replace('void ', '').replace('spef::', '').strip()
+    n = full.replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '').replace('spef::', '').strip()
     n = re.sub(r'\s+', '', n)
     n = n.replace('stem_kernel<F16,0>', 'stem_kernel<u8>').replace('stem_kernel<F16,1>', 'stem_kernel<f32>')
     n = n.replace('stem_kernel<BF16,0>', 'stem_kernel<u8>').replace('stem_kernel<BF16,1>', 'stem_kernel<f32>')
     n = re.sub(r'dw_kernel<B?F16,(\d)>', r'dw_kernel<\1>', n)
     n = re.sub(r'pw_pool_kernel<B?F16,(\d)>', r'pw_pool_kernel<\1>', n)
+    n = re.sub(r'^q_irb_kernel<(\d+),(\d+),(\d+),(\d+),.*>$', r'q_irb_kernel<\1,\2,\3,s\4>', n)   # int8 path
+    n = n.replace('q_stem_kernel<false>', 'q_stem_kernel<u8>').replace('q_stem_kernel<true>', 'q_stem_kernel<f32>')
     return n
 
 
