@@ -1,6 +1,6 @@
-// VALU issue-rate microbenchmark (GPU box): 8 waves/SIMD, 8 independent accumulators per lane, N iterations.
-// Prints cycles per wave64 instruction per SIMD for v_fma_f32, v_fma_mix_f32, v_cvt_f32_f16, v_pk_fma_f32,
-// v_dot2_f32_f16. Build: hipcc -O3 --offload-arch=gfx950 valu_rate.hip -o valu_rate
+// VALU issue-rate microbenchmark (GPU box): 8 and 2 waves/SIMD, 8 independent accumulators per lane, N iterations.
+// Prints cycles per wave64 instruction per SIMD for fp32/fp16 ops and the int8 requant ops (v_mad_i64_i32, v_med3_i32, ...):
+// Build: hipcc -O3 --offload-arch=gfx950 valu_rate.hip -o valu_rate
 #include <hip/hip_runtime.h>
 #include <cstdio>
 
