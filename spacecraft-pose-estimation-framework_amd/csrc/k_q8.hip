@@ -31,73 +31,101 @@ __device__ __forceinline__ int requant(int acc, int64_t M, int64_t B, int S, int
 }
 
 // ------------------------------------------------------------------------------------------------ stem
-// Input QuantIdentity + QConvBnAct 3->32 3x3/s2 (mobilenet_v2.py:177-182). One thread per output pixel,
-// 27 taps packed into 7 dwords (sdot4), 32 channel accumulators; weights [32][28] int8 broadcast from LDS.
+// Input QuantIdentity + QConvBnAct 3->32 3x3/s2 (mobilenet_v2.py:177-182), 32 channel accumulators on v_dot4_i32_i8.
+// A workgroup owns a 4 x 64 output tile. Its 9 x 129 input
+// pixels are staged in LDS once, quantised (LUT / rint), one dword per pixel [q_r, q_g, q_b, 0]: every tap of an
+// output pixel is then one ds_read_b32 and one v_dot4_i32_i8 per channel against weights rearranged to
+// [32][9] dwords (w28's k = ky*9 + kx*3 + ci order, so the sums are the same integers). 15 byte gathers per thread
+// instead of 27 per pixel. Requant: the high word of one v_mad_i64_i32 shifted by S - 32 when every channel's
+// S >= 32 and |M| < 2^31 (workgroup-uniform check), the 64-bit form otherwise.
+constexpr int kStemTH = 4, kStemTW = 64, kStemIH = 2 * kStemTH + 1, kStemIW = 2 * kStemTW + 1;
 template <bool F32IN>
-__global__ __launch_bounds__(256) void q_stem_kernel(const void* __restrict__ in, const int8_t* __restrict__ lut,
-                                                     float s_img, const int8_t* __restrict__ w28,
-                                                     Rq rq, uint8_t* __restrict__ Y, int B, int H, int W,
-                                                     int OH, int OW) {
-  __shared__ int Wl[32 * 7];
+__global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict__ in, const int8_t* __restrict__ lut,
+                                                          float s_img, const int8_t* __restrict__ w28, Rq rq,
+                                                          uint8_t* __restrict__ Y, int H, int W, int OH, int OW,
+                                                          int tiles_x, int tiles_y) {
+  __shared__ int Xs[kStemIH * kStemIW];
+  __shared__ int Wl[32 * 9];
   __shared__ int8_t Ll[256];
   __shared__ int64_t Ml[32], Bl[32];
-  __shared__ int Sl[32], M32[32];
+  __shared__ int Sl[32];
   const int tid = threadIdx.x;
-  if (tid < 32 * 7) Wl[tid] = reinterpret_cast<const int*>(w28)[tid];
-  if (!F32IN) Ll[tid] = lut[tid];
+  int L = blockIdx.x;
+  const int tx = L % tiles_x;
+  L /= tiles_x;
+  const int ty = L % tiles_y, b = L / tiles_y;
+  const int oy0 = ty * kStemTH, ox0 = tx * kStemTW;
+  const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
+  // staging: every load issued (clamped address) before any is used
+  constexpr int NS = kStemIH * kStemIW, NIT = (NS + 255) / 256;
+  float fv[F32IN ? NIT * 3 : 1];
+  uint8_t uv[F32IN ? 1 : NIT * 3];
+  uint32_t okm = 0;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = tid + 256 * it;
+    const int r = i / kStemIW, cc = i - r * kStemIW;
+    const int iy = iy0 + r, ix = ix0 + cc;
+    const bool ok = i < NS && (unsigned)iy < (unsigned)H && (unsigned)ix < (unsigned)W;
+    okm |= (uint32_t)ok << it;
+#pragma unroll
+    for (int ci = 0; ci < 3; ++ci) {
+      if (F32IN) {
+        const size_t off = ok ? (((size_t)b * 3 + ci) * H + iy) * W + ix : 0;
+        fv[it * 3 + ci] = reinterpret_cast<const float*>(in)[off];
+      } else {
+        const size_t off = ok ? (((size_t)b * H + iy) * W + ix) * 3 + ci : 0;
+        uv[it * 3 + ci] = reinterpret_cast<const uint8_t*>(in)[off];
+      }
+    }
+  }
   bool fast_ok = true;
   if (tid < 32) {
     Ml[tid] = rq.M[tid];
     Bl[tid] = rq.B[tid];
     Sl[tid] = rq.S[tid];
-    M32[tid] = (int)rq.M[tid];
     fast_ok = rq.S[tid] >= 32 && rq.M[tid] > -(1LL << 31) && rq.M[tid] < (1LL << 31);
   }
-  // every channel's shift >= 32 and |M| < 2^31 (what blob_q8.fixed produces for realistic scales): the requant is
-  // the high word of one v_mad_i64_i32 shifted by S - 32, then a clamp -- bit-identical to the 64-bit form
+  for (int i = tid; i < 32 * 9; i += 256) {   // [c][tap] dwords {w(ci 0), w(ci 1), w(ci 2), 0}
+    const int c = i / 9, t = i - 9 * c;
+    const uint8_t* w = reinterpret_cast<const uint8_t*>(w28) + c * 28 + 3 * t;
+    Wl[i] = (int)((uint32_t)w[0] | ((uint32_t)w[1] << 8) | ((uint32_t)w[2] << 16));
+  }
+  if (!F32IN) Ll[tid] = lut[tid];
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    const int i = tid + 256 * it;
+    if (i < NS) {
+      uint32_t v = 0;
+      if ((okm >> it) & 1u) {
+#pragma unroll
+        for (int ci = 0; ci < 3; ++ci) {
+          int q;
+          if (F32IN) q = (int)fminf(fmaxf(rintf(fv[it * 3 + ci] / s_img), -128.f), 127.f);
+          else q = Ll[uv[it * 3 + ci]];
+          v |= ((uint32_t)q & 0xffu) << (8 * ci);
+        }
+      }
+      Xs[i] = (int)v;
+    }
+  }
   const bool fast = __syncthreads_and(fast_ok);
-  const int64_t p = (int64_t)blockIdx.x * 256 + tid;
-  if (p >= (int64_t)B * OH * OW) return;
-  const int ox = (int)(p % OW);
-  const int oy = (int)((p / OW) % OH);
-  const int b = (int)(p / ((int64_t)OW * OH));
-  int8_t t[28];
+  const int oy = tid / kStemTW, ox = tid - oy * kStemTW;
+  int x[9];
 #pragma unroll
   for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      const int iy = 2 * oy - 1 + ky, ix = 2 * ox - 1 + kx;
-      const bool v = iy >= 0 && iy < H && ix >= 0 && ix < W;
-#pragma unroll
-      for (int ci = 0; ci < 3; ++ci) {
-        int8_t q = 0;
-        if (v) {
-          if (F32IN) {
-            const float x = reinterpret_cast<const float*>(in)[(((size_t)b * 3 + ci) * H + iy) * W + ix];
-            const float r = rintf(x / s_img);
-            q = (int8_t)fminf(fmaxf(r, -128.f), 127.f);
-          } else {
-            q = Ll[reinterpret_cast<const uint8_t*>(in)[(((size_t)b * H + iy) * W + ix) * 3 + ci]];
-          }
-        }
-        t[ky * 9 + kx * 3 + ci] = q;
-      }
-    }
-  t[27] = 0;
-  int xp[7];
-#pragma unroll
-  for (int d = 0; d < 7; ++d)
-    xp[d] = (int)(uint8_t)t[4 * d] | ((int)(uint8_t)t[4 * d + 1] << 8) | ((int)(uint8_t)t[4 * d + 2] << 16) |
-            ((int)(uint8_t)t[4 * d + 3] << 24);
+    for (int kx = 0; kx < 3; ++kx) x[ky * 3 + kx] = Xs[(2 * oy + ky) * kStemIW + 2 * ox + kx];
   uint32_t o[8];
 #pragma unroll
   for (int c = 0; c < 32; ++c) {
     int acc = 0;
 #pragma unroll
-    for (int d = 0; d < 7; ++d) acc = __builtin_amdgcn_sdot4(xp[d], Wl[c * 7 + d], acc, false);
+    for (int t = 0; t < 9; ++t) acc = __builtin_amdgcn_sdot4(x[t], Wl[c * 9 + t], acc, false);
     uint32_t q;
     if (fast) {
-      const int v = (int)(((int64_t)acc * M32[c] + Bl[c]) >> 32) >> (Sl[c] - 32);
+      const int v = (int)(((int64_t)acc * (int)Ml[c] + Bl[c]) >> 32) >> (Sl[c] - 32);
       q = (uint32_t)min(max(v, 0), 255);
     } else {
       q = (uint32_t)requant(acc, Ml[c], Bl[c], Sl[c], 0, 255);
@@ -105,9 +133,12 @@ __global__ __launch_bounds__(256) void q_stem_kernel(const void* __restrict__ in
     if ((c & 3) == 0) o[c >> 2] = 0;
     o[c >> 2] |= q << (8 * (c & 3));
   }
-  uint4* dst = reinterpret_cast<uint4*>(Y + (size_t)p * 32);
-  dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-  dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  const int gy = oy0 + oy, gx = ox0 + ox;
+  if (gy < OH && gx < OW) {
+    uint4* dst = reinterpret_cast<uint4*>(Y + (((size_t)b * OH + gy) * OW + gx) * 32);
+    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
+    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------ depthwise
@@ -359,14 +390,15 @@ hipError_t launch_q_to_f32(const void* x, float* y, int64_t n, int is_unsigned, 
 hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_img, const int8_t* w28,
                          const int64_t* M, const int64_t* Bq, const int32_t* S, uint8_t* y, int B, int H, int W,
                          int OH, int OW, hipStream_t s) {
-  const int64_t n = (int64_t)B * OH * OW;
-  const int64_t nb = (n + 255) / 256;
+  const int tiles_x = (OW + kStemTW - 1) / kStemTW, tiles_y = (OH + kStemTH - 1) / kStemTH;
+  const int64_t nb = (int64_t)tiles_x * tiles_y * B;
   if (nb > 0x7fffffff) return hipErrorInvalidValue;
+  if (nb == 0) return hipSuccess;
   Rq rq{M, Bq, S};
   if (f32in)
-    q_stem_kernel<true><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, B, H, W, OH, OW);
+    q_stem_rows_kernel<true><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y);
   else
-    q_stem_kernel<false><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, B, H, W, OH, OW);
+    q_stem_rows_kernel<false><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y);
   return hipGetLastError();
 }
 
