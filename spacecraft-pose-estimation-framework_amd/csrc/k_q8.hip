@@ -31,20 +31,22 @@ __device__ __forceinline__ int requant(int acc, int64_t M, int64_t B, int S, int
 }
 
 // ------------------------------------------------------------------------------------------------ stem
-// Input QuantIdentity + QConvBnAct 3->32 3x3/s2 (mobilenet_v2.py:177-182), 32 channel accumulators on v_dot4_i32_i8.
+// Input QuantIdentity + QConvBnAct 3->32 3x3/s2 (mobilenet_v2.py:177-182).
 // A workgroup owns a 4 x 64 output tile. Its 9 x 129 input
-// pixels are staged in LDS once, quantised (LUT / rint), one dword per pixel [q_r, q_g, q_b, 0]: every tap of an
-// output pixel is then one ds_read_b32 and one v_dot4_i32_i8 per channel against weights rearranged to
-// [32][9] dwords (w28's k = ky*9 + kx*3 + ci order, so the sums are the same integers). 15 byte gathers per thread
-// instead of 27 per pixel. Requant: the high word of one v_mad_i64_i32 shifted by S - 32 when every channel's
+// pixels are staged in LDS once, quantised (LUT / rint), one dword per pixel [q_r, q_g, q_b, 0], and the weights
+// rearranged to [32][9] dwords of the same form (w28's k = ky*9 + kx*3 + ci order: the sums are the same integers).
+// The conv is then a K = 64 MFMA (9 tap dwords + zero padding): one ds_read_b32 per tap per lane. 15 byte gathers
+// per thread instead of 27 per pixel. Requant: the high word of one v_mad_i64_i32 shifted by S - 32 when every channel's
 // S >= 32 and |M| < 2^31 (workgroup-uniform check), the 64-bit form otherwise.
 constexpr int kStemTH = 4, kStemTW = 64, kStemIH = 2 * kStemTH + 1, kStemIW = 2 * kStemTW + 1;
 template <bool F32IN>
 __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict__ in, const int8_t* __restrict__ lut,
                                                           float s_img, const int8_t* __restrict__ w28, Rq rq,
                                                           uint8_t* __restrict__ Y, int H, int W, int OH, int OW,
-                                                          int tiles_x, int tiles_y) {
+                                                          int tiles_x, int tiles_y, size_t nbytes) {
   __shared__ int Xs[kStemIH * kStemIW];
+  constexpr int RAWDW = (3 * kStemIW + 6) / 4 + 1;   // dwords of one window row's aligned byte span
+  __shared__ uint32_t Raw[F32IN ? 1 : kStemIH * RAWDW];
   __shared__ int Wl[32 * 9];
   __shared__ int8_t Ll[256];
   __shared__ int64_t Ml[32], Bl[32];
@@ -56,10 +58,33 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
   const int ty = L % tiles_y, b = L / tiles_y;
   const int oy0 = ty * kStemTH, ox0 = tx * kStemTW;
   const int iy0 = 2 * oy0 - 1, ix0 = 2 * ox0 - 1;
-  // staging: every load issued (clamped address) before any is used
+  // staging: every load issued (clamped address) before any is used. u8 frames: each window row is one contiguous
+  // byte span (clipped to the image row), moved as aligned dwords into Raw and unpacked from LDS below.
+  const int cx0 = ix0 > 0 ? ix0 : 0, cx1 = ix0 + kStemIW < W ? ix0 + kStemIW : W;   // valid columns [cx0, cx1)
+  constexpr int NRAW = kStemIH * RAWDW, NITR = (NRAW + 255) / 256;
+  uint32_t rw[F32IN ? 1 : NITR];
+  if constexpr (!F32IN) {
+    const uint8_t* inb = reinterpret_cast<const uint8_t*>(in);
+#pragma unroll
+    for (int it = 0; it < NITR; ++it) {
+      const int i = tid + 256 * it;
+      const int r = i / RAWDW, d = i - r * RAWDW;
+      const int iy = iy0 + r;
+      const size_t rs = (((size_t)b * H + (iy >= 0 ? iy : 0)) * W + cx0) * 3, re = rs + (size_t)(cx1 - cx0) * 3;
+      const size_t dw = (rs >> 2) + d;
+      const bool ok = i < NRAW && (unsigned)iy < (unsigned)H && cx1 > cx0 && 4 * dw < re;
+      if (ok && 4 * dw + 4 > nbytes) {   // the buffer's partial last dword: bytes one by one
+        uint32_t v = 0;
+        for (int k = 0; k < 4; ++k)
+          if (4 * dw + k < nbytes) v |= (uint32_t)inb[4 * dw + k] << (8 * k);
+        rw[it] = v;
+      } else {
+        rw[it] = reinterpret_cast<const uint32_t*>(inb)[ok ? dw : 0];
+      }
+    }
+  }
   constexpr int NS = kStemIH * kStemIW, NIT = (NS + 255) / 256;
   float fv[F32IN ? NIT * 3 : 1];
-  uint8_t uv[F32IN ? 1 : NIT * 3];
   uint32_t okm = 0;
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -73,9 +98,6 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
       if (F32IN) {
         const size_t off = ok ? (((size_t)b * 3 + ci) * H + iy) * W + ix : 0;
         fv[it * 3 + ci] = reinterpret_cast<const float*>(in)[off];
-      } else {
-        const size_t off = ok ? (((size_t)b * H + iy) * W + ix) * 3 + ci : 0;
-        uv[it * 3 + ci] = reinterpret_cast<const uint8_t*>(in)[off];
       }
     }
   }
@@ -91,7 +113,14 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
     const uint8_t* w = reinterpret_cast<const uint8_t*>(w28) + c * 28 + 3 * t;
     Wl[i] = (int)((uint32_t)w[0] | ((uint32_t)w[1] << 8) | ((uint32_t)w[2] << 16));
   }
-  if (!F32IN) Ll[tid] = lut[tid];
+  if constexpr (!F32IN) {
+    Ll[tid] = lut[tid];
+#pragma unroll
+    for (int it = 0; it < NITR; ++it) {
+      const int i = tid + 256 * it;
+      if (i < NRAW) Raw[i] = rw[it];
+    }
+  }
   __syncthreads();
 #pragma unroll
   for (int it = 0; it < NIT; ++it) {
@@ -102,8 +131,15 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
 #pragma unroll
         for (int ci = 0; ci < 3; ++ci) {
           int q;
-          if (F32IN) q = (int)fminf(fmaxf(rintf(fv[it * 3 + ci] / s_img), -128.f), 127.f);
-          else q = Ll[uv[it * 3 + ci]];
+          if (F32IN) {
+            q = (int)fminf(fmaxf(rintf(fv[it * 3 + ci] / s_img), -128.f), 127.f);
+          } else {   // byte (ix - cx0) * 3 + ci of window row r's span, which starts (rs & 3) bytes into Raw
+            const int r = i / kStemIW, ix = ix0 + (i - r * kStemIW);
+            const int iy = iy0 + r;
+            const size_t rs = (((size_t)b * H + iy) * W + cx0) * 3;
+            const int pos = (int)(rs & 3) + (ix - cx0) * 3 + ci;
+            q = Ll[reinterpret_cast<const uint8_t*>(Raw + r * RAWDW)[pos]];
+          }
           v |= ((uint32_t)q & 0xffu) << (8 * ci);
         }
       }
@@ -111,33 +147,75 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
     }
   }
   const bool fast = __syncthreads_and(fast_ok);
-  const int oy = tid / kStemTW, ox = tid - oy * kStemTW;
-  int x[9];
+  // ---- the 3x3/s2 conv on v_mfma_i32_16x16x64_i8: k = 4 * tap + byte (tap = ky*3 + kx, taps >= 9 zero), a wave
+  // computes 16 pixels x 16 channels per MFMA; lane (r16, kg) holds taps 4 kg .. 4 kg + 3 of pixel / channel r16
+  const int lane = tid & 63, wave = tid >> 6, r16 = lane & 15, kg = lane >> 4;
+  int toff[4];
+  uint32_t tv = 0;
 #pragma unroll
-  for (int ky = 0; ky < 3; ++ky)
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) x[ky * 3 + kx] = Xs[(2 * oy + ky) * kStemIW + 2 * ox + kx];
-  uint32_t o[8];
-#pragma unroll
-  for (int c = 0; c < 32; ++c) {
-    int acc = 0;
-#pragma unroll
-    for (int t = 0; t < 9; ++t) acc = __builtin_amdgcn_sdot4(x[t], Wl[c * 9 + t], acc, false);
-    uint32_t q;
-    if (fast) {
-      const int v = (int)(((int64_t)acc * (int)Ml[c] + Bl[c]) >> 32) >> (Sl[c] - 32);
-      q = (uint32_t)min(max(v, 0), 255);
-    } else {
-      q = (uint32_t)requant(acc, Ml[c], Bl[c], Sl[c], 0, 255);
-    }
-    if ((c & 3) == 0) o[c >> 2] = 0;
-    o[c >> 2] |= q << (8 * (c & 3));
+  for (int j = 0; j < 4; ++j) {
+    const int t = 4 * kg + j, tc = t < 9 ? t : 0;
+    toff[j] = (tc / 3) * kStemIW + tc % 3;
+    tv |= (uint32_t)(t < 9) << j;
   }
-  const int gy = oy0 + oy, gx = ox0 + ox;
-  if (gy < OH && gx < OW) {
-    uint4* dst = reinterpret_cast<uint4*>(Y + (((size_t)b * OH + gy) * OW + gx) * 32);
-    dst[0] = make_uint4(o[0], o[1], o[2], o[3]);
-    dst[1] = make_uint4(o[4], o[5], o[6], o[7]);
+  i32x4 a[2];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int t = 4 * kg + j;
+      const int v = Wl[(16 * h + r16) * 9 + (t < 9 ? t : 0)];
+      a[h][j] = ((tv >> j) & 1u) ? v : 0;
+    }
+  int64_t Mr[8], Br[8];
+  int Sr[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int c = (i < 4 ? 0 : 12) + 4 * kg + i;
+    Mr[i] = Ml[c];
+    Br[i] = Bl[c];
+    Sr[i] = Sl[c];
+  }
+  constexpr int GPW = kStemTH * kStemTW / 16 / 4;   // 16-pixel groups per wave
+#pragma unroll
+  for (int gi = 0; gi < GPW; ++gi) {
+    const int g = wave * GPW + gi;
+    const int oy = g / (kStemTW / 16), ox = (g % (kStemTW / 16)) * 16 + r16;
+    const int base = 2 * oy * kStemIW + 2 * ox;
+    i32x4 bx;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int v = Xs[base + toff[j]];
+      bx[j] = ((tv >> j) & 1u) ? v : 0;
+    }
+    const i32x4 z = {0, 0, 0, 0};
+    const i32x4 acc0 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[0], bx, z, 0, 0, 0);
+    const i32x4 acc1 = __builtin_amdgcn_mfma_i32_16x16x64_i8(a[1], bx, z, 0, 0, 0);
+    uint32_t o[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      uint32_t w = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int acc = h ? acc1[i] : acc0[i];
+        const int e = 4 * h + i;
+        int v;
+        if (fast) {
+          v = (int)(((int64_t)acc * (int)Mr[e] + Br[e]) >> 32) >> (Sr[e] - 32);
+          v = min(max(v, 0), 255);
+        } else {
+          v = requant(acc, Mr[e], Br[e], Sr[e], 0, 255);
+        }
+        w |= (uint32_t)v << (8 * i);
+      }
+      o[h] = w;
+    }
+    const int gy = oy0 + oy, gx = ox0 + ox;
+    if (gy < OH && gx < OW) {
+      uint8_t* y = Y + (((size_t)b * OH + gy) * OW + gx) * 32 + 4 * kg;
+      *reinterpret_cast<uint32_t*>(y) = o[0];
+      *reinterpret_cast<uint32_t*>(y + 16) = o[1];
+    }
   }
 }
 
@@ -391,14 +469,17 @@ hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_i
                          const int64_t* M, const int64_t* Bq, const int32_t* S, uint8_t* y, int B, int H, int W,
                          int OH, int OW, hipStream_t s) {
   const int tiles_x = (OW + kStemTW - 1) / kStemTW, tiles_y = (OH + kStemTH - 1) / kStemTH;
+  const size_t nbytes = (size_t)B * H * W * 3;   // u8 NHWC frame buffer (the f32 form does not use it)
   const int64_t nb = (int64_t)tiles_x * tiles_y * B;
   if (nb > 0x7fffffff) return hipErrorInvalidValue;
   if (nb == 0) return hipSuccess;
   Rq rq{M, Bq, S};
   if (f32in)
-    q_stem_rows_kernel<true><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y);
+    q_stem_rows_kernel<true><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y,
+                                                           nbytes);
   else
-    q_stem_rows_kernel<false><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y);
+    q_stem_rows_kernel<false><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y,
+                                                            nbytes);
   return hipGetLastError();
 }
 
