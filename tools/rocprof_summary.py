@@ -29,7 +29,8 @@ def short_name(full: str) -> str:
     n = re.sub(r'dw_kernel<B?F16,(\d)>', r'dw_kernel<\1>', n)
     n = re.sub(r'pw_pool_kernel<B?F16,(\d)>', r'pw_pool_kernel<\1>', n)
     n = re.sub(r'^q_irb_kernel<(\d+),(\d+),(\d+),(\d+),.*>$', r'q_irb_kernel<\1,\2,\3,s\4>', n)   # int8 path
-    n = n.replace('q_stem_kernel<false>', 'q_stem_kernel<u8>').replace('q_stem_kernel<true>', 'q_stem_kernel<f32>')
+    n = re.sub(r'^q_stem(_rows)?_kernel<false>$', 'q_stem_kernel<u8>', n)
+    n = re.sub(r'^q_stem(_rows)?_kernel<true>$', 'q_stem_kernel<f32>', n)
     return n
 
 
