@@ -173,7 +173,18 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
       const int u = tid + NW * 64 * i;
       if (u < NU) {
         const int p = u / GPR, g = u - p * GPR;
-        *reinterpret_cast<long*>(Xs + p * G::XSB + g * 8) = ((okm >> i) & 1u) ? xin[i] : 0;
+        const long v = ((okm >> i) & 1u) ? xin[i] : 0;
+        if constexpr (EXPAND) {
+          *reinterpret_cast<long*>(Xs + p * G::XSB + g * 8) = v;
+        } else {   // t == 1 (block 1): the hidden tensor is the u8 input itself, straight into the slab as fp16 1024 + n
+          const uint32_t lo = (uint32_t)v, hi = (uint32_t)((uint64_t)v >> 32);
+          uint4 o;
+          o.x = (lo & 0xffu) | ((lo & 0xff00u) << 8) | kF16Bias2;
+          o.y = ((lo >> 16) & 0xffu) | ((lo >> 8) & 0xff0000u) | kF16Bias2;
+          o.z = (hi & 0xffu) | ((hi & 0xff00u) << 8) | kF16Bias2;
+          o.w = ((hi >> 16) & 0xffu) | ((hi >> 8) & 0xff0000u) | kF16Bias2;
+          *reinterpret_cast<uint4*>(Es + p * G::ES + 8 * g) = o;
+        }
       }
     }
 #pragma unroll
@@ -245,17 +256,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
     // ---- 2. expand (32 hidden channels) -> requant -> u8 as fp16 in the slab. t == 1 (block 1): the hidden
     // tensor is the unsigned stem output itself, converted to fp16 (zero outside the image from the staging).
     if constexpr (!EXPAND) {
-      static_assert(HID == 32 && CIN == 32, "t == 1 is MobileNet-V2 block 1");
-      for (int u = tid; u < G::PIN * 4; u += NW * 64) {
-        const int p = u >> 2, g = u & 3;
-        const uint2 v = *reinterpret_cast<const uint2*>(Xs + p * G::XSB + 8 * g);
-        uint4 o;   // byte n -> fp16 1024 + n (0x6400 | n), two per dword
-        o.x = (v.x & 0xffu) | ((v.x & 0xff00u) << 8) | kF16Bias2;
-        o.y = ((v.x >> 16) & 0xffu) | ((v.x >> 8) & 0xff0000u) | kF16Bias2;
-        o.z = (v.y & 0xffu) | ((v.y & 0xff00u) << 8) | kF16Bias2;
-        o.w = ((v.y >> 16) & 0xffu) | ((v.y >> 8) & 0xff0000u) | kF16Bias2;
-        *reinterpret_cast<uint4*>(Es + p * G::ES + 8 * g) = o;
-      }
+      static_assert(HID == 32 && CIN == 32, "t == 1 is MobileNet-V2 block 1");   // slab filled by the prologue
     } else {
       long a0[G::KSE], a1[G::KSE], na0[G::KSE], na1[G::KSE];
       const int h0 = 32 * c + r16, h1 = 32 * c + 16 + r16;
