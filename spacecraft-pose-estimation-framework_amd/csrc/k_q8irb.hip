@@ -102,8 +102,10 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
     int8_t* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y, uint32_t nwg) {
   using G = QGeom<CIN, HID, COUT, S, TH, TW, RES, NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // t == 1 without residual (block 1) never reads an int8 input copy: no Xs region, more workgroups per CU
+  constexpr int XREG = (EXPAND || RES) ? G::PINP * G::XSB : 0;
   int8_t* Xs = reinterpret_cast<int8_t*>(smem);
-  _Float16* Es = reinterpret_cast<_Float16*>(smem + G::PINP * G::XSB);
+  _Float16* Es = reinterpret_cast<_Float16*>(smem + XREG);
   uint8_t* Tb = reinterpret_cast<uint8_t*>(Es + G::PINP * G::ES);          // [2][TAB]
   RQ16* RqP = reinterpret_cast<RQ16*>(Tb + 2 * G::TAB);                      // [NPO]
 
@@ -420,13 +422,14 @@ hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   auto k = q_irb_kernel<CIN, HID, COUT, S, TH, TW, RES, NW, EXPAND, SH32>;
+  constexpr int lds = G::LDS_BYTES - ((EXPAND || RES) ? 0 : G::PINP * G::XSB);   // see XREG in the kernel
   static bool attr_set = false;
-  if (!attr_set && G::LDS_BYTES > 65536) {
-    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
+  if (!attr_set && lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  k<<<nwg, NW * 64, G::LDS_BYTES, s>>>(x, we, wp, pinit, tabs, rm, rb, rs, y, H, W, OH, OW, tiles_x, tiles_y, nwg);
+  k<<<nwg, NW * 64, lds, s>>>(x, we, wp, pinit, tabs, rm, rb, rs, y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   return hipGetLastError();
 }
 
