@@ -22,7 +22,8 @@
 extern "C" {
 #endif
 
-#define SPEF_ABI_VERSION 1
+#define SPEF_ABI_VERSION 2
+#define SPEF_COMM_ID_BYTES 128   /* size of the RCCL unique id (ncclUniqueId) */
 
 enum spef_status {
   SPEF_OK = 0,
@@ -53,8 +54,9 @@ int spef_init(int device, spef_ctx** out);
 int spef_destroy(spef_ctx* ctx);
 
 /* Load a packed weight blob (built by build_mi355x.py from parameters.pt, model.py:261-266 layout).
- * _host: blob in host memory; _device: blob already in this device's memory (e.g. after an RCCL
- * broadcast from rank 0) -- copied device-to-device. */
+ * _host: blob in host memory; _device: blob already in this device's memory -- copied device-to-device.
+ * The blob is validated in full first (spef_validate_blob); on any failure the context keeps the model it had
+ * (or stays empty), so a failed reload never leaves a half-loaded context. */
 int spef_load_weights(spef_ctx* ctx, const void* host_blob, size_t bytes);
 int spef_load_weights_device(spef_ctx* ctx, const void* dev_blob, size_t bytes);
 /* Query the loaded model: head (0 URSONet, 1 keypoints), output widths, storage dtype (1 fp16, 2 bf16). */
@@ -86,14 +88,17 @@ int spef_set_decode_tables(spef_ctx* ctx, const double* ori_bins, int n_ori_bins
                            int n_pos_bins);
 
 /* SPEUtils.last_activ + SPEUtils.decode (spe_utils.py:56-101) for the URSONet head.
- * ori_mode: SPEF_CLASSIFICATION (softmax -> ori_soft [B x n_ori_bins], Markley average -> quat [B x 4]) or
- *           SPEF_REGRESSION (L2 normalise ori_raw [B x 4] -> quat).
- * pos_mode: SPEF_CLASSIFICATION (softmax -> pos_soft [B x n_pos_bins], soft-argmax -> pos [B x 3]) or
+ * ori_mode: SPEF_CLASSIFICATION (softmax -> ori_soft [B x n_ori], Markley average -> quat [B x 4]) or
+ *           SPEF_REGRESSION (L2 normalise ori_raw [B x 4] -> quat, spe_utils.py:72).
+ * pos_mode: SPEF_CLASSIFICATION (softmax -> pos_soft [B x n_pos], soft-argmax -> pos [B x 3]) or
  *           SPEF_REGRESSION (pos = pos_raw copied).
+ * n_ori / n_pos: the row widths of ori_raw / pos_raw (the shapes NumPy carries in the reference). They must equal
+ *           the decode tables' bin counts in classification mode (spef_set_decode_tables) and 4 / 3 in regression
+ *           mode, else SPEF_ERR_ARG -- the kernels never read rows of a width the tables do not describe.
  * status: device int[B], zeroed by this call; bit 1 NaN orientation, 2 position zero sum, 4 NaN position.
  * ori_soft / pos_soft may be NULL. */
-int spef_decode(spef_ctx* ctx, int ori_mode, int pos_mode, const float* ori_raw, const float* pos_raw, int B,
-                float* ori_soft, float* quat, float* pos_soft, float* pos, int* status, void* stream);
+int spef_decode(spef_ctx* ctx, int ori_mode, int pos_mode, const float* ori_raw, int n_ori, const float* pos_raw,
+                int n_pos, int B, float* ori_soft, float* quat, float* pos_soft, float* pos, int* status, void* stream);
 
 /* Keypoint mode (ORI == POS == 'keypoints', config.py:53-58): the 3-D model points (host float32 n x 3,
  * e.g. tangoPoints.mat's 11 Tango keypoints, keypoints_utils.py:31-45), the camera matrix (host float64
@@ -113,25 +118,34 @@ int spef_decode_keypoints(spef_ctx* ctx, const float* raw, int B, int apply_sigm
 int spef_preprocess(spef_ctx* ctx, const uint8_t* frames, int B, int Hin, int Win, uint8_t* out, int H, int W,
                     void* stream);
 
-/* Options. SPEF_OPT_FUSE_BLOCKS (default 1): run each inverted-residual block as one fused kernel
- * (expand + depthwise + project on-chip) where its geometry is in the fused table; 0 = one kernel per conv. */
-/* SPEF_OPT_FUSE_MIN_HW: fuse only blocks whose input has at least this many pixels per image (late,
- * low-resolution blocks then run as GEMM + depthwise + GEMM with the hidden tensor L2/MALL-resident).
- * SPEF_OPT_PW_GEMM (default 1): LDS-tiled MFMA GEMM for unfused 1x1 convs; 0 = register-direct kernel. */
-/* SPEF_OPT_IRB_VARIANT: fused-block tile variant (0 = tuned default; others for tuning sweeps).
- * SPEF_OPT_STRIP (default 0, experimental): register-streaming fused blocks for the high-resolution geometries; 0 = LDS-slab
- * fused blocks everywhere.
- * SPEF_OPT_WAVESPEC (default 1): wave-specialised fused blocks for the low-resolution geometries (expand waves
- * and depthwise/project waves pipelined over hidden chunks); 0 = LDS-slab fused blocks. */
+/* Schedule options (both choices of each are bit-identical; the parity tests switch them):
+ * SPEF_OPT_FUSE_BLOCKS (default 1): each inverted-residual block as one fused kernel (expand + depthwise + project
+ *   on-chip); 0 = one kernel per conv (the reference's module-by-module schedule).
+ * SPEF_OPT_WAVESPEC (default 1): wave-specialised fused kernels for the low-resolution blocks (expand waves and
+ *   depthwise/project waves pipelined over hidden chunks); 0 = LDS-slab fused kernels everywhere.
+ * (Kernel-tuning knobs used by the sweep tools are internal: csrc/spef_tuning.hpp.) */
 enum spef_option {
   SPEF_OPT_FUSE_BLOCKS = 1,
-  SPEF_OPT_FUSE_MIN_HW = 2,
-  SPEF_OPT_PW_GEMM = 3,
-  SPEF_OPT_IRB_VARIANT = 4,
-  SPEF_OPT_STRIP = 5,
   SPEF_OPT_WAVESPEC = 6
 };
 int spef_set_option(spef_ctx* ctx, int option, int value);
+
+/* Host-only validation of a weight blob (no device needed: build tools and CPU tests use it). Checks the header,
+ * the op table, every tensor's extent against the data section (from the op geometry) and the head widths;
+ * returns SPEF_ERR_BLOB with a message on the first problem. Outputs may be NULL. */
+int spef_validate_blob(const void* host_blob, size_t bytes, int* dtype, int* head, int* n_out0, int* n_out1);
+
+/* Weight broadcast over RCCL (xGMI) -- SURVEY.md §8b/§8e: rank `root` sends the blob its context holds, every
+ * other rank's context receives and loads it (header, op table and data section, device to device; no host
+ * round trip). Collective: every rank of `comm` calls it with the same root. Replaces each rank reading
+ * parameters.pt itself (modeling/model.py:261-266). `comm` is an RCCL communicator (ncclComm_t) -- the host's
+ * own, or one made with spef_comm_init from an id that rank 0 produced with spef_comm_unique_id and the host
+ * shipped to the other ranks (any side channel: torch.distributed, MPI, a file). On failure a receiving context
+ * keeps the model it had. */
+int spef_comm_unique_id(void* id_out, size_t cap);
+int spef_comm_init(int device, int nranks, int rank, const void* id, void** comm_out);
+int spef_comm_destroy(void* comm);
+int spef_bcast_weights(spef_ctx* ctx, void* comm, int root);
 
 /* Per-launch HIP-event profiling of every kernel the context enqueues between begin and end (bench.py's
  * roofline leg). spef_profile_end synchronises, then writes a JSON object

@@ -1,10 +1,14 @@
 // C ABI (include/spef.h) and the layer executor of the SPEF MI355X target.
 //
-// The executor walks the blob's op list (stem -> 17 inverted residuals -> last 1x1 -> head) over four
-// NHWC activation buffers sized at spef_reserve time, launching one kernel per conv (unfused v1 schedule).
+// The executor walks the blob's op list (stem -> 17 inverted residuals -> last 1x1 -> head) over four NHWC
+// activation buffers sized at spef_reserve time. Default schedule: the uint8 front kernel (stem + block 1), one
+// fused kernel per inverted residual (LDS-slab or wave-specialised), the last 1x1 conv fused with the global mean,
+// the FC head; SPEF_OPT_FUSE_BLOCKS=0 runs one kernel per conv instead (bit-identical). Also here: blob
+// validation and loading, the RCCL weight broadcast, decode dispatch and the per-launch profiler.
 #include "../../include/spef.h"
 
 #include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
 #include <math.h>
 #include <string.h>
 
@@ -16,6 +20,7 @@
 
 #include "spef_blob.hpp"
 #include "spef_kernels.hpp"
+#include "spef_tuning.hpp"
 
 using namespace spef;
 
@@ -62,7 +67,6 @@ struct spef_ctx {
   int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
   int irb_variant = 0;       // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps)
   int wavespec = 1;          // SPEF_OPT_WAVESPEC: wave-specialised fused blocks (k_irw.hip) where available
-  int strip = 0;             // SPEF_OPT_STRIP: register-streaming fused blocks (k_irs.hip) where available
   // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
   std::vector<double> q8_sw, q8_bias;
   std::vector<int32_t> q8_wsum;
@@ -276,19 +280,14 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const double bytes = (double)M * op.cin * 2 + (double)M2 * op.cout * 2 +
                              (expand ? pw_bytes(0, op.cin, op.hidden, false) : 0) + 40.0 * op.hidden +
                              pw_bytes(0, op.hidden, op.cout, false);
-        const bool strip = c->strip && irs_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res);
-        const bool wspec = !strip && c->wavespec &&
+        const bool wspec = c->wavespec &&
                            irw_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res);
         char key[96];
-        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", strip ? "irs_kernel" : wspec ? "irw_kernel" : "irb_kernel", op.cin,
+        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", wspec ? "irw_kernel" : "irb_kernel", op.cin,
                  op.hidden, op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
           if (wspec)
             return launch_irw(c->irb_variant, dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, x, ptr<void>(c, op.w0),
-                              ptr<float>(c, op.b0), ptr<void>(c, op.w1), ptr<float>(c, op.b1), ptr<void>(c, op.w2),
-                              ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
-          if (strip)
-            return launch_irs(dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, x, ptr<void>(c, op.w0),
                               ptr<float>(c, op.b0), ptr<void>(c, op.w1), ptr<float>(c, op.b1), ptr<void>(c, op.w2),
                               ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
           return launch_irb(c->irb_variant, dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
@@ -605,93 +604,276 @@ int spef_destroy(spef_ctx* c) {
   return SPEF_OK;
 }
 
-static int parse_blob(spef_ctx* c, const uint8_t* head_bytes, size_t bytes) {
-  if (bytes < sizeof(BlobHeader)) return fail(SPEF_ERR_BLOB, "blob too small");
+// Minimum byte extent of each tensor an op references (w0, b0, w1, b1, w2, b2, x0, x1, x2), from the op
+// geometry and the blob layout in spef_blob.hpp; 0 where the op has no such tensor.
+static void op_extents(const OpDesc& op, uint32_t dtype, uint64_t ext[9]) {
+  auto r16 = [](uint64_t n) { return (n + 15) & ~15ull; };
+  auto r32 = [](uint64_t n) { return (n + 31) & ~31ull; };
+  auto r64 = [](uint64_t n) { return (n + 63) & ~63ull; };
+  const uint64_t a = 2;                                   // fp16 / bf16 activation storage
+  const uint64_t rq = 20;                                 // int64 M + int64 B + int32 S per channel
+  for (int i = 0; i < 9; ++i) ext[i] = 0;
+  const uint64_t ci = op.cin, co = op.cout, h = op.hidden;
+  switch (op.kind) {
+    case OP_STEM: ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * co * 32 * a; break;
+    case OP_IRB:
+      if (op.expand != 1) { ext[0] = r16(h) * r32(ci) * a; ext[1] = r16(h) * 4; }
+      ext[2] = 9 * h * (dtype == DT_F16 ? 2 : 4); ext[3] = h * 4;
+      ext[4] = r16(co) * r32(h) * a; ext[5] = r16(co) * 4;
+      break;
+    case OP_LAST: ext[0] = r16(co) * r32(ci) * a; ext[1] = r16(co) * 4; break;
+    case OP_FC: case OP_FCKP: ext[0] = r16(co) * ci * 4; ext[1] = r16(co) * 4; break;
+    case OP_QSTEM: ext[0] = 32 * 28; ext[1] = 32 * rq; ext[2] = 256; ext[6] = 4; break;
+    case OP_QIRB: {
+      if (op.expand != 1) { ext[0] = r16(h) * r64(ci); ext[1] = r16(h) * rq; }
+      ext[2] = 9 * h; ext[3] = r16(h) * rq;
+      ext[4] = r16(co) * r64(h); ext[5] = r16(co) * rq;
+      ext[6] = r16(co) * 4;
+      if (op.flags & 1u) ext[7] = 24;
+      if (op.x2 != kAbsent) ext[8] = 16 * r32(h) * 2 + 16 * r16(co) + 2 * 9 * r32(h);
+      break;
+    }
+    case OP_QLAST: ext[0] = r16(co) * r64(ci); ext[1] = r16(co) * rq; break;
+    case OP_QFC: ext[0] = r16(co) * ci; ext[1] = r16(co) * 8; ext[2] = r16(co) * 8; ext[6] = r16(co) * 4; ext[7] = 8; break;
+    default: break;
+  }
+}
+
+// Parse and validate a blob's header + op table (host bytes: at least the first `meta_bytes` of the blob; `bytes`
+// is the whole blob's size). Pure host code -- writes nothing but *h / *ops, and only on success.
+static int parse_blob(const uint8_t* head_bytes, size_t meta_bytes, size_t bytes, BlobHeader* h_out,
+                      std::vector<OpDesc>* ops_out) {
+  if (meta_bytes < sizeof(BlobHeader) || bytes < sizeof(BlobHeader)) return fail(SPEF_ERR_BLOB, "blob too small");
   BlobHeader h;
   memcpy(&h, head_bytes, sizeof(h));
   if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_BLOB, "bad blob magic");
   if (h.version != kBlobVersion) return fail(SPEF_ERR_BLOB, "unsupported blob version");
   if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8) return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
-  if (h.ops_off + (uint64_t)h.n_ops * sizeof(OpDesc) > bytes || h.data_off + h.data_bytes > bytes)
+  if (h.n_ops == 0 || h.n_ops > 4096) return fail(SPEF_ERR_BLOB, "bad op count");
+  const uint64_t ops_end = h.ops_off + (uint64_t)h.n_ops * sizeof(OpDesc);
+  if (h.ops_off < sizeof(BlobHeader) || ops_end > h.data_off || h.data_off > bytes ||
+      h.data_bytes > bytes - h.data_off || ops_end > meta_bytes)
     return fail(SPEF_ERR_BLOB, "blob truncated");
+  if (h.feat_c != 1280) return fail(SPEF_ERR_BLOB, "feature width must be 1280 (mobilenet_v2.py:232)");
   std::vector<OpDesc> ops(h.n_ops);
   memcpy(ops.data(), head_bytes + h.ops_off, h.n_ops * sizeof(OpDesc));
+  int n_head = 0;
   for (const OpDesc& op : ops) {
-    for (uint64_t off : {op.w0, op.b0, op.w1, op.b1, op.w2, op.b2, op.x0, op.x1, op.x2})
-      if (off != kAbsent && (off >= h.data_bytes || (off & 15)))
-        return fail(SPEF_ERR_BLOB, "tensor offset out of range / misaligned");
+    uint64_t ext[9];
+    op_extents(op, h.dtype, ext);
+    const uint64_t offs[9] = {op.w0, op.b0, op.w1, op.b1, op.w2, op.b2, op.x0, op.x1, op.x2};
+    for (int i = 0; i < 9; ++i) {
+      if (offs[i] == kAbsent) {
+        if (ext[i] && !(op.kind == OP_QIRB && i == 8)) return fail(SPEF_ERR_BLOB, "op lacks a required tensor");
+        continue;
+      }
+      if ((offs[i] & 15) || offs[i] >= h.data_bytes || ext[i] > h.data_bytes - offs[i])
+        return fail(SPEF_ERR_BLOB, "tensor extent out of range / misaligned (op kind " + std::to_string(op.kind) + ")");
+    }
     if ((op.kind == OP_IRB || op.kind == OP_QIRB) &&
         (op.cin % 8 || op.cout % 8 || op.hidden % 8 || (op.stride != 1 && op.stride != 2)))
       return fail(SPEF_ERR_BLOB, "unsupported inverted-residual geometry");
     const bool qop = op.kind >= OP_QSTEM && op.kind <= OP_QFC;
     if (qop != (h.dtype == DT_I8)) return fail(SPEF_ERR_BLOB, "op kind does not match the blob dtype");
-    if (op.kind == OP_QSTEM && (op.cout != 32 || op.x0 == kAbsent || op.w1 == kAbsent))
-      return fail(SPEF_ERR_BLOB, "int8 stem needs 32 outputs, an input LUT and scale");
-    if (op.kind == OP_QIRB && (op.x0 == kAbsent || ((op.flags & 1u) && op.x1 == kAbsent)))
-      return fail(SPEF_ERR_BLOB, "int8 block lacks its projection init / residual rescale");
-    if (op.kind == OP_QFC && (op.x0 == kAbsent || op.x1 == kAbsent))
-      return fail(SPEF_ERR_BLOB, "int8 FC lacks its constants");
+    if (op.kind == OP_QSTEM && op.cout != 32) return fail(SPEF_ERR_BLOB, "int8 stem needs 32 outputs");
+    if (op.kind == OP_FC || op.kind == OP_QFC) {
+      ++n_head;
+      if (h.head != HEAD_URSONET || op.cin != h.feat_c || op.cout != h.n_out0 + h.n_out1)
+        return fail(SPEF_ERR_BLOB, "URSONet head widths do not match the header");
+    }
+    if (op.kind == OP_FCKP) {
+      ++n_head;
+      if (h.head != HEAD_KEYPOINTS || op.cout != h.n_out0 || op.cin != (uint64_t)h.kp_fh * h.kp_fw * h.feat_c)
+        return fail(SPEF_ERR_BLOB, "keypoint head widths do not match the header");
+    }
   }
-  c->hdr = h;
-  c->ops = std::move(ops);
+  if (n_head != 1) return fail(SPEF_ERR_BLOB, "blob must hold exactly one head op");
+  *h_out = h;
+  *ops_out = std::move(ops);
   return SPEF_OK;
 }
 
+// Load the blob at `blob` (host or device memory). Transactional: everything is parsed and copied into new
+// storage first; the context's model is replaced only when all of it succeeded.
 static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_device) {
   if (!c || !blob) return fail(SPEF_ERR_ARG, "null argument");
   Dev d(c->device);
   std::vector<uint8_t> head;
   const uint8_t* hb;
-  if (on_device) {
-    // header + op table live in the first bytes; fetch them to the host
-    BlobHeader h;
-    HIP_TRY(hipMemcpy(&h, blob, sizeof(h), hipMemcpyDeviceToHost));
-    const size_t meta = std::min<size_t>(bytes, (size_t)h.data_off);
-    head.resize(std::max<size_t>(meta, sizeof(h)));
-    HIP_TRY(hipMemcpy(head.data(), blob, head.size(), hipMemcpyDeviceToHost));
+  size_t meta;
+  if (on_device) {   // header + op table live in the first bytes; fetch them to the host
+    if (bytes < sizeof(BlobHeader)) return fail(SPEF_ERR_BLOB, "blob too small");
+    BlobHeader h0;
+    HIP_TRY(hipMemcpy(&h0, blob, sizeof(h0), hipMemcpyDeviceToHost));
+    meta = std::max<size_t>(sizeof(h0), std::min<size_t>(bytes, (size_t)h0.data_off));
+    head.resize(meta);
+    HIP_TRY(hipMemcpy(head.data(), blob, meta, hipMemcpyDeviceToHost));
     hb = head.data();
-    int rc = parse_blob(c, hb, bytes);
-    if (rc) return rc;
   } else {
     hb = (const uint8_t*)blob;
-    int rc = parse_blob(c, hb, bytes);
-    if (rc) return rc;
+    meta = bytes;
   }
-  if (c->d_data) hipFree(c->d_data);
-  c->d_data = nullptr;
-  HIP_TRY(hipMalloc(&c->d_data, c->hdr.data_bytes));
-  const uint8_t* src = (const uint8_t*)blob + c->hdr.data_off;
-  HIP_TRY(hipMemcpy(c->d_data, src, c->hdr.data_bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
-  c->data_bytes = c->hdr.data_bytes;
-  if (c->hdr.dtype == DT_I8) {   // small host-side constants of the int8 schedule, fetched once
-    c->q8_res.assign(c->ops.size(), {0, 0, 0});
-    c->q8_fc_hw = 0;
-    for (size_t i = 0; i < c->ops.size(); ++i) {
-      const OpDesc& op = c->ops[i];
-      if (op.kind == OP_QSTEM)
-        HIP_TRY(hipMemcpy(&c->q8_s_img, c->d_data + op.x0, sizeof(float), hipMemcpyDeviceToHost));
-      if (op.kind == OP_QIRB && (op.flags & 1u))
-        HIP_TRY(hipMemcpy(c->q8_res[i].data(), c->d_data + op.x1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost));
-      if (op.kind == OP_QFC) {
-        const size_t np_ = (op.cout + 15) & ~15u;
-        c->q8_sw.resize(np_);
-        c->q8_bias.resize(np_);
-        c->q8_wsum.resize(np_);
-        HIP_TRY(hipMemcpy(c->q8_sw.data(), c->d_data + op.b0, np_ * sizeof(double), hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(c->q8_bias.data(), c->d_data + op.w1, np_ * sizeof(double), hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(c->q8_wsum.data(), c->d_data + op.x0, np_ * sizeof(int32_t), hipMemcpyDeviceToHost));
-        HIP_TRY(hipMemcpy(&c->q8_sl, c->d_data + op.x1, sizeof(double), hipMemcpyDeviceToHost));
+  BlobHeader h;
+  std::vector<OpDesc> ops;
+  int rc = parse_blob(hb, meta, bytes, &h, &ops);
+  if (rc) return rc;
+
+  uint8_t* dd = nullptr;
+  std::vector<std::array<int64_t, 3>> q8_res;
+  std::vector<double> q8_sw, q8_bias;
+  std::vector<int32_t> q8_wsum;
+  double q8_sl = 0.0;
+  float q8_s_img = 0.f;
+  auto stage = [&]() -> int {
+    HIP_TRY(hipMalloc(&dd, std::max<uint64_t>(h.data_bytes, 256)));
+    const uint8_t* src = (const uint8_t*)blob + h.data_off;
+    HIP_TRY(hipMemcpy(dd, src, h.data_bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+    if (h.dtype == DT_I8) {   // small host-side constants of the int8 schedule, fetched once
+      q8_res.assign(ops.size(), {0, 0, 0});
+      for (size_t i = 0; i < ops.size(); ++i) {
+        const OpDesc& op = ops[i];
+        if (op.kind == OP_QSTEM) HIP_TRY(hipMemcpy(&q8_s_img, dd + op.x0, sizeof(float), hipMemcpyDeviceToHost));
+        if (op.kind == OP_QIRB && (op.flags & 1u))
+          HIP_TRY(hipMemcpy(q8_res[i].data(), dd + op.x1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost));
+        if (op.kind == OP_QFC) {
+          const size_t np_ = (op.cout + 15) & ~15u;
+          q8_sw.resize(np_);
+          q8_bias.resize(np_);
+          q8_wsum.resize(np_);
+          HIP_TRY(hipMemcpy(q8_sw.data(), dd + op.b0, np_ * sizeof(double), hipMemcpyDeviceToHost));
+          HIP_TRY(hipMemcpy(q8_bias.data(), dd + op.w1, np_ * sizeof(double), hipMemcpyDeviceToHost));
+          HIP_TRY(hipMemcpy(q8_wsum.data(), dd + op.x0, np_ * sizeof(int32_t), hipMemcpyDeviceToHost));
+          HIP_TRY(hipMemcpy(&q8_sl, dd + op.x1, sizeof(double), hipMemcpyDeviceToHost));
+        }
       }
     }
+    return SPEF_OK;
+  };
+  rc = stage();
+  if (rc) {
+    if (dd) hipFree(dd);
+    return rc;
   }
-  c->loaded = true;
+  // commit
   free_workspace(c);
+  if (c->d_data) hipFree(c->d_data);
+  c->d_data = dd;
+  c->data_bytes = h.data_bytes;
+  c->hdr = h;
+  c->ops = std::move(ops);
+  c->q8_res = std::move(q8_res);
+  c->q8_sw = std::move(q8_sw);
+  c->q8_bias = std::move(q8_bias);
+  c->q8_wsum = std::move(q8_wsum);
+  c->q8_sl = q8_sl;
+  c->q8_s_img = q8_s_img;
+  c->q8_fc_hw = 0;
+  c->loaded = true;
   return SPEF_OK;
 }
 
 int spef_load_weights(spef_ctx* c, const void* blob, size_t bytes) { return load_common(c, blob, bytes, false); }
 
 int spef_load_weights_device(spef_ctx* c, const void* blob, size_t bytes) { return load_common(c, blob, bytes, true); }
+
+int spef_validate_blob(const void* blob, size_t bytes, int* dtype, int* head, int* n_out0, int* n_out1) {
+  if (!blob) return fail(SPEF_ERR_ARG, "null blob");
+  BlobHeader h;
+  std::vector<OpDesc> ops;
+  const int rc = parse_blob((const uint8_t*)blob, bytes, bytes, &h, &ops);
+  if (rc) return rc;
+  if (dtype) *dtype = (int)h.dtype;
+  if (head) *head = (int)h.head;
+  if (n_out0) *n_out0 = (int)h.n_out0;
+  if (n_out1) *n_out1 = (int)h.n_out1;
+  return SPEF_OK;
+}
+
+#define NCCL_TRY(expr)                                                                                      \
+  do {                                                                                                      \
+    ncclResult_t r_ = (expr);                                                                               \
+    if (r_ != ncclSuccess) return fail(SPEF_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_));  \
+  } while (0)
+
+int spef_comm_unique_id(void* id_out, size_t cap) {
+  if (!id_out || cap < sizeof(ncclUniqueId)) return fail(SPEF_ERR_ARG, "id buffer smaller than SPEF_COMM_ID_BYTES");
+  static_assert(sizeof(ncclUniqueId) == SPEF_COMM_ID_BYTES, "SPEF_COMM_ID_BYTES != sizeof(ncclUniqueId)");
+  ncclUniqueId id;
+  NCCL_TRY(ncclGetUniqueId(&id));
+  memcpy(id_out, &id, sizeof(id));
+  return SPEF_OK;
+}
+
+int spef_comm_init(int device, int nranks, int rank, const void* id, void** comm_out) {
+  if (!id || !comm_out || nranks < 1 || rank < 0 || rank >= nranks) return fail(SPEF_ERR_ARG, "bad communicator arguments");
+  Dev d(device);
+  HIP_TRY(hipSetDevice(device));
+  ncclUniqueId uid;
+  memcpy(&uid, id, sizeof(uid));
+  ncclComm_t comm = nullptr;
+  NCCL_TRY(ncclCommInitRank(&comm, nranks, uid, rank));
+  *comm_out = comm;
+  return SPEF_OK;
+}
+
+int spef_comm_destroy(void* comm) {
+  if (!comm) return SPEF_OK;
+  NCCL_TRY(ncclCommDestroy((ncclComm_t)comm));
+  return SPEF_OK;
+}
+
+int spef_bcast_weights(spef_ctx* c, void* comm_, int root) {
+  if (!c || !comm_) return fail(SPEF_ERR_ARG, "null argument");
+  ncclComm_t comm = (ncclComm_t)comm_;
+  int rank = 0, n = 0;
+  NCCL_TRY(ncclCommUserRank(comm, &rank));
+  NCCL_TRY(ncclCommCount(comm, &n));
+  if (root < 0 || root >= n) return fail(SPEF_ERR_ARG, "root out of range");
+  Dev d(c->device);
+  struct Tmp {   // scratch freed on every exit path
+    hipStream_t s = nullptr;
+    uint8_t* buf = nullptr;
+    ~Tmp() {
+      if (s) hipStreamDestroy(s);
+      if (buf) hipFree(buf);
+    }
+  } t;
+  HIP_TRY(hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking));
+  // 1. header (a root without weights sends an all-zero header, so every rank fails the same way below)
+  BlobHeader h{};
+  if (rank == root && c->loaded) h = c->hdr;
+  const size_t meta = (rank == root && c->loaded) ? (size_t)h.data_off : 0;
+  uint8_t* dh = nullptr;
+  HIP_TRY(hipMalloc(&dh, sizeof(h)));
+  t.buf = dh;
+  HIP_TRY(hipMemcpy(dh, &h, sizeof(h), hipMemcpyHostToDevice));
+  NCCL_TRY(ncclBroadcast(dh, dh, sizeof(h), ncclUint8, root, comm, t.s));
+  HIP_TRY(hipStreamSynchronize(t.s));
+  HIP_TRY(hipMemcpy(&h, dh, sizeof(h), hipMemcpyDeviceToHost));
+  if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_STATE, "broadcast root has no weights loaded");
+  if (h.data_off > (1ull << 30) || h.data_bytes > (1ull << 36)) return fail(SPEF_ERR_BLOB, "broadcast header out of range");
+  // 2. op table + data section into a full blob image (the receivers load it like spef_load_weights_device)
+  const size_t total = (size_t)h.data_off + (size_t)h.data_bytes;
+  hipFree(t.buf);
+  t.buf = nullptr;
+  HIP_TRY(hipMalloc(&t.buf, std::max<size_t>(total, 256)));
+  uint8_t* img = t.buf;
+  HIP_TRY(hipMemcpy(img, &h, sizeof(h), hipMemcpyHostToDevice));
+  const size_t ops_bytes = (size_t)h.n_ops * sizeof(OpDesc);
+  if (h.ops_off + ops_bytes > h.data_off) return fail(SPEF_ERR_BLOB, "broadcast op table overlaps the data section");
+  if (rank == root) {
+    (void)meta;
+    HIP_TRY(hipMemcpy(img + h.ops_off, c->ops.data(), ops_bytes, hipMemcpyHostToDevice));
+    NCCL_TRY(ncclBroadcast(img + h.ops_off, img + h.ops_off, ops_bytes, ncclUint8, root, comm, t.s));
+    NCCL_TRY(ncclBroadcast(c->d_data, c->d_data, h.data_bytes, ncclUint8, root, comm, t.s));
+    HIP_TRY(hipStreamSynchronize(t.s));
+    return SPEF_OK;   // the root keeps its loaded model
+  }
+  NCCL_TRY(ncclBroadcast(img + h.ops_off, img + h.ops_off, ops_bytes, ncclUint8, root, comm, t.s));
+  NCCL_TRY(ncclBroadcast(img + h.data_off, img + h.data_off, h.data_bytes, ncclUint8, root, comm, t.s));
+  HIP_TRY(hipStreamSynchronize(t.s));
+  return load_common(c, img, total, true);
+}
 
 int spef_model_info(const spef_ctx* c, int* head, int* n_out0, int* n_out1, int* dtype, int* n_ops) {
   if (!c || !c->loaded) return fail(SPEF_ERR_STATE, "weights not loaded");
@@ -862,10 +1044,19 @@ int spef_set_decode_tables(spef_ctx* c, const double* ori_bins, int n_ori_bins, 
   return SPEF_OK;
 }
 
-int spef_decode(spef_ctx* c, int ori_mode, int pos_mode, const float* ori_raw, const float* pos_raw, int B,
-                float* ori_soft, float* quat, float* pos_soft, float* pos, int* status, void* stream) {
+int spef_decode(spef_ctx* c, int ori_mode, int pos_mode, const float* ori_raw, int n_ori, const float* pos_raw,
+                int n_pos, int B, float* ori_soft, float* quat, float* pos_soft, float* pos, int* status, void* stream) {
   if (!c) return fail(SPEF_ERR_ARG, "null context");
   if (B <= 0 || !ori_raw || !quat || !pos_raw || !pos || !status) return fail(SPEF_ERR_ARG, "null argument");
+  // row widths must be the ones the decode describes (the kernels stride rows by the table sizes)
+  if (ori_mode == SPEF_CLASSIFICATION && c->d_ori_bins && n_ori != c->n_ori_bins)
+    return fail(SPEF_ERR_ARG, "orientation logits are " + std::to_string(n_ori) + " wide, the histogram has " +
+                                  std::to_string(c->n_ori_bins) + " bins");
+  if (ori_mode == SPEF_REGRESSION && n_ori != 4) return fail(SPEF_ERR_ARG, "orientation regression needs 4 outputs");
+  if (pos_mode == SPEF_CLASSIFICATION && c->d_pos_grid && n_pos != c->n_pos_bins)
+    return fail(SPEF_ERR_ARG, "position logits are " + std::to_string(n_pos) + " wide, the grid has " +
+                                  std::to_string(c->n_pos_bins) + " bins");
+  if (pos_mode == SPEF_REGRESSION && n_pos != 3) return fail(SPEF_ERR_ARG, "position regression needs 3 outputs");
   Dev d(c->device);
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemsetAsync(status, 0, sizeof(int) * B, s));
@@ -1094,7 +1285,7 @@ int spef_set_option(spef_ctx* c, int option, int value) {
     c->fuse = value != 0;
     return SPEF_OK;
   }
-  if (option == SPEF_OPT_FUSE_MIN_HW) {
+  if (option == SPEF_OPT_FUSE_MIN_HW) {   // spef_tuning.hpp
     c->fuse_min_hw = value;
     return SPEF_OK;
   }
@@ -1108,10 +1299,6 @@ int spef_set_option(spef_ctx* c, int option, int value) {
   }
   if (option == SPEF_OPT_WAVESPEC) {
     c->wavespec = value != 0;
-    return SPEF_OK;
-  }
-  if (option == SPEF_OPT_STRIP) {
-    c->strip = value != 0;
     return SPEF_OK;
   }
   return fail(SPEF_ERR_ARG, "unknown option");

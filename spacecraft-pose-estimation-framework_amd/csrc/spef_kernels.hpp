@@ -48,12 +48,6 @@ hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int st
                       const void* we, const float* be, const void* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 
-// Register-streaming fused block for the high-resolution geometries in k_irs.hip's table (same contract).
-bool irs_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
-hipError_t launch_irs(int dtype, int cin, int hid, int cout, int stride, bool res, const void* x, const void* we,
-                      const float* be, const void* wd, const float* bd, const void* wp, const float* bp, void* y,
-                      int B, int H, int W, int OH, int OW, hipStream_t s);
-
 // Wave-specialised fused block (expand waves feed depthwise/project waves through a double-buffered LDS slab) for
 // the low-resolution geometries in k_irw.hip's table (same contract, bit-identical to the unfused kernels).
 bool irw_supported(int cin, int hid, int cout, int stride, bool expand, bool res);

@@ -1,0 +1,13 @@
+// Internal kernel-tuning options of spef_set_option (not part of the public ABI in include/spef.h).
+// Used by the sweep tools (tools/explore.py, tools/ab.py) to time alternative schedules on the GPU box.
+//   SPEF_OPT_FUSE_MIN_HW: fuse only blocks whose input has at least this many pixels per image (the rest run as
+//                         GEMM + depthwise + GEMM).
+//   SPEF_OPT_PW_GEMM    : LDS-tiled MFMA GEMM (1, default) or register-direct kernel (0) for unfused 1x1 convs.
+//   SPEF_OPT_IRB_VARIANT: fused-block tile variant (0 = tuned default).
+#pragma once
+
+enum spef_tuning_option {
+  SPEF_OPT_FUSE_MIN_HW = 2,
+  SPEF_OPT_PW_GEMM = 3,
+  SPEF_OPT_IRB_VARIANT = 4
+};

@@ -12,7 +12,10 @@ from . import _build
 OK, ERR_ARG, ERR_HIP, ERR_BLOB, ERR_STATE, ERR_NUMERIC = range(6)
 IN_U8_NHWC, IN_F32_NCHW = 0, 1
 REGRESSION, CLASSIFICATION, KEYPOINTS = 0, 1, 2
-OPT_FUSE_BLOCKS, OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT, OPT_STRIP, OPT_WAVESPEC = 1, 2, 3, 4, 5, 6
+ABI_VERSION = 2
+COMM_ID_BYTES = 128
+OPT_FUSE_BLOCKS, OPT_WAVESPEC = 1, 6                          # public schedule options (include/spef.h)
+OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT = 2, 3, 4       # internal tuning knobs (csrc/spef_tuning.hpp)
 
 # name -> (restype, argtypes); keep in sync with include/spef.h (tests/test_abi.py checks the header)
 _vp, _i, _sz = C.c_void_p, C.c_int, C.c_size_t
@@ -31,7 +34,12 @@ SIGNATURES = {
     'spef_backbone': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp]),
     'spef_probe': (_i, [_vp, _vp, _i, _i, _i, _i, _i, _vp, _ip, _ip, _ip, _vp]),
     'spef_set_decode_tables': (_i, [_vp, _vp, _i, _vp, _i]),
-    'spef_decode': (_i, [_vp, _i, _i, _vp, _vp, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'spef_decode': (_i, [_vp, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
+    'spef_validate_blob': (_i, [_vp, _sz, _ip, _ip, _ip, _ip]),
+    'spef_comm_unique_id': (_i, [_vp, _sz]),
+    'spef_comm_init': (_i, [_i, _i, _i, _vp, C.POINTER(_vp)]),
+    'spef_comm_destroy': (_i, [_vp]),
+    'spef_bcast_weights': (_i, [_vp, _vp, _i]),
     'spef_set_option': (_i, [_vp, _i, _i]),
     'spef_set_keypoints': (_i, [_vp, _vp, _i, _vp, C.c_float, C.c_float]),
     'spef_decode_keypoints': (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
@@ -54,16 +62,22 @@ def load(path: str | None = None) -> C.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
-    path = path or os.environ.get('SPEF_LIB') or _build.lib_path()   # SPEF_LIB: A/B timing of two builds
+    override = path or os.environ.get('SPEF_LIB')    # SPEF_LIB: A/B timing of two builds (tools/ab.py)
+    path = override or _build.lib_path()
     if not os.path.exists(path):
         raise ImportError(f'SPEF HIP library not built: {path} (run __graft_entry__.build() or '
                           f'python -m spef_amd._build)')
+    if not override:   # the in-tree library must have been linked from exactly the sources beside it
+        info = _build.read_info()
+        if info.get('source_digest') != _build.source_digest():
+            raise ImportError(f'SPEF HIP library {path} is stale or has no BUILD_INFO.json: it was not built from '
+                              f'the current csrc/ + include/ (run __graft_entry__.build())')
     lib = C.CDLL(path, mode=C.RTLD_GLOBAL)
     for name, (res, args) in SIGNATURES.items():
         f = getattr(lib, name)
         f.restype = res
         f.argtypes = args
-    if lib.spef_abi_version() != 1:
+    if lib.spef_abi_version() != ABI_VERSION:
         raise ImportError('SPEF ABI version mismatch')
     _LIB = lib
     return lib

@@ -29,7 +29,9 @@ class Engine:
     outputs; ``decode`` applies SPEUtils.last_activ + decode on the device.
     """
 
-    def __init__(self, blob: bytes | torch.Tensor, device: int | str | torch.device = 0):
+    def __init__(self, blob: bytes | torch.Tensor | None, device: int | str | torch.device = 0):
+        """``blob``: packed weights in host memory (bytes) or on this device (uint8 tensor), or None for an empty
+        context that receives its weights with ``bcast_weights``."""
         self.lib = L.load()
         self.device = torch.device(device if not isinstance(device, int) else f'cuda:{device}')
         if self.device.type != 'cuda':
@@ -38,9 +40,12 @@ class Engine:
         h = C.c_void_p()
         L.check(self.lib.spef_init(idx, C.byref(h)))
         self.ctx = h
-        self.load(blob)
         self._reserved = (0, 0, 0)
         self._decode_tables = None
+        self.head = self.n_out0 = self.n_out1 = self.n_ops = None
+        self.dtype = None
+        if blob is not None:
+            self.load(blob)
 
     # ------------------------------------------------------------------ weights
     def load(self, blob: bytes | torch.Tensor) -> None:
@@ -50,6 +55,15 @@ class Engine:
         else:
             buf = C.create_string_buffer(bytes(blob), len(blob))
             L.check(self.lib.spef_load_weights(self.ctx, buf, len(blob)))
+        self._model_info()
+
+    def bcast_weights(self, comm, root: int = 0) -> None:
+        """Collective over the RCCL communicator ``comm`` (spef_amd.shard.RcclComm): rank ``root``'s weights are
+        broadcast into every rank's context (spef_bcast_weights)."""
+        L.check(self.lib.spef_bcast_weights(self.ctx, C.c_void_p(int(comm)), root))
+        self._model_info()
+
+    def _model_info(self) -> None:
         head, n0, n1, dt, nops = (C.c_int(), C.c_int(), C.c_int(), C.c_int(), C.c_int())
         L.check(self.lib.spef_model_info(self.ctx, C.byref(head), C.byref(n0), C.byref(n1), C.byref(dt),
                                          C.byref(nops)))
@@ -134,8 +148,12 @@ class Engine:
         status = torch.empty((B,), dtype=torch.int32, device=dev)
         ori_soft = torch.empty_like(ori_raw) if (want_soft and ori_mode == L.CLASSIFICATION) else None
         pos_soft = torch.empty_like(pos_raw) if (want_soft and pos_mode == L.CLASSIFICATION) else None
-        L.check(self.lib.spef_decode(self.ctx, ori_mode, pos_mode, _ptr(ori_raw), _ptr(pos_raw), B, _ptr(ori_soft),
-                                     _ptr(quat), _ptr(pos_soft), _ptr(pos), _ptr(status), _stream(dev)))
+        assert ori_raw.dim() == 2 and pos_raw.dim() == 2 and pos_raw.shape[0] == B
+        assert ori_raw.is_contiguous() and pos_raw.is_contiguous()
+        assert ori_raw.dtype == torch.float32 and pos_raw.dtype == torch.float32
+        L.check(self.lib.spef_decode(self.ctx, ori_mode, pos_mode, _ptr(ori_raw), ori_raw.shape[1], _ptr(pos_raw),
+                                     pos_raw.shape[1], B, _ptr(ori_soft), _ptr(quat), _ptr(pos_soft), _ptr(pos),
+                                     _ptr(status), _stream(dev)))
         return {'ori': quat, 'pos': pos, 'ori_soft': ori_soft, 'pos_soft': pos_soft, 'status': status}
 
     def set_fused(self, on: bool) -> None:

@@ -2,7 +2,9 @@
 
 Frames are independent on this path, so N GPUs = N processes (``torch.distributed.run``), each owning a
 contiguous slice of the global frame range and its own engine. The only collectives are
-  * one broadcast of the packed weight blob from rank 0 (RCCL over xGMI on the GPU box; gloo in CPU tests),
+  * one broadcast of the packed weight blob from rank 0: ``RcclComm`` + ``Engine.bcast_weights`` on the GPU box
+    (the library's own RCCL communicator over xGMI, C ABI ``spef_bcast_weights``), or ``broadcast_blob`` through
+    any torch.distributed backend (gloo in the CPU tests),
   * the max-over-ranks of the timed region (bench contract),
   * optionally a gather of the B x 7 pose rows to rank 0 for metrics.
 There is nothing to all-reduce. Every function works with any process-group backend, so the CPU gloo tests
@@ -49,6 +51,39 @@ def broadcast_blob(blob: Optional[bytes], device: torch.device, src: int = 0) ->
     if ws > 1:
         dist.broadcast(out, src)
     return out
+
+
+class RcclComm:
+    """An RCCL communicator owned by the SPEF library (``spef_comm_init``), for ``spef_bcast_weights``.
+
+    Rank 0 draws the 128-byte unique id (``spef_comm_unique_id``); the id travels to the other ranks over the
+    already-initialised torch.distributed group (``broadcast_object_list``: any backend), the way a C host would ship
+    it over MPI or a file. ``int(comm)`` is the ncclComm_t handle."""
+
+    def __init__(self, device: torch.device):
+        import ctypes as C
+        from . import _lib as L
+        self.lib = L.load()
+        rank, ws = world()
+        idbuf = [None]
+        if rank == 0:
+            raw = C.create_string_buffer(L.COMM_ID_BYTES)
+            L.check(self.lib.spef_comm_unique_id(raw, L.COMM_ID_BYTES))
+            idbuf[0] = raw.raw
+        if ws > 1:
+            dist.broadcast_object_list(idbuf, src=0)
+        rid = C.create_string_buffer(bytes(idbuf[0]), L.COMM_ID_BYTES)
+        h = C.c_void_p()
+        L.check(self.lib.spef_comm_init(torch.device(device).index or 0, ws, rank, rid, C.byref(h)))
+        self.handle = h.value
+
+    def __int__(self) -> int:
+        return int(self.handle)
+
+    def close(self) -> None:
+        if self.handle:
+            self.lib.spef_comm_destroy(self.handle)
+            self.handle = None
 
 
 def max_over_ranks(seconds: float, device: torch.device) -> float:

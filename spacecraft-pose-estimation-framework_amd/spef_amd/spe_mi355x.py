@@ -66,8 +66,8 @@ class SPEMi355x:
             cam = kp.camera
             self.engine.set_keypoints(np.asarray(kp.keypoints3d, np.float32), np.asarray(cam.K, np.float64),
                                       float(cam.nu), float(cam.nv))
-            assert self.engine.n_out0 == 2 * (kp.keypoints3d.shape[0] + 1), \
-                f'keypoint head width {self.engine.n_out0} != 2 * (n_keypoints + 1)'   # model.py:236
+            if self.engine.n_out0 != 2 * (kp.keypoints3d.shape[0] + 1):   # model.py:236
+                raise AssertionError(f'keypoint head width {self.engine.n_out0} != 2 * (n_keypoints + 1)')
             return
         ori_bins = su.orientation.histogram if self.ori_mode == L.CLASSIFICATION else None
         pos_grid = su.position.histogram if self.pos_mode == L.CLASSIFICATION else None
@@ -75,8 +75,10 @@ class SPEMi355x:
         # the head widths in the blob must agree with the decode configuration (model.py:225-234)
         want0 = su.orientation.n_bins if self.ori_mode == L.CLASSIFICATION else 4
         want1 = su.position.n_bins if self.pos_mode == L.CLASSIFICATION else 3
-        assert (self.engine.n_out0, self.engine.n_out1) == (want0, want1), \
-            f'model head {(self.engine.n_out0, self.engine.n_out1)} != decode config {(want0, want1)}'
+        # (raised, not asserted: python -O must not drop it; spef_decode re-checks the widths in C as well)
+        if (self.engine.n_out0, self.engine.n_out1) != (want0, want1):
+            raise AssertionError(f'model head {(self.engine.n_out0, self.engine.n_out1)} != decode config '
+                                 f'{(want0, want1)}')
 
     def delete_model(self) -> None:
         if self.engine is not None:
@@ -111,7 +113,8 @@ class SPEMi355x:
 
     def predict(self, images: torch.Tensor, num_predict: int = 1) -> Tuple[Dict, float]:
         """images: NCHW float32 in [0,1] (the reference ``images['torch']``) or NHWC uint8 frames."""
-        assert self.engine is not None
+        if self.engine is None:
+            raise AssertionError('no model loaded')            # spe_torch.py:55 (assert hasattr(self, 'model'))
         x = images.to(self.device, non_blocking=True).contiguous()
         torch.cuda.synchronize(self.device)
         start, end = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)

@@ -55,8 +55,13 @@ def _conv_bn(sd: Dict[str, np.ndarray], c: ConvSpec, seed: int, m_in: float) -> 
 
 
 def synthetic_state_dict(arch: Arch | None = None, seed: int = 1001, head_std: float = 0.01,
-                         input_m2: float = 0.1) -> Dict[str, np.ndarray]:
-    """Return ``{reference key: float32 ndarray}`` (num_batches_tracked as int64 scalars)."""
+                         input_m2: float = 0.1, pos_std: float | None = None,
+                         pos_bias=None) -> Dict[str, np.ndarray]:
+    """Return ``{reference key: float32 ndarray}`` (num_batches_tracked as int64 scalars).
+
+    ``head_std`` is the orientation (or keypoint) Linear's weight std (the reference init is 0.01,
+    pytorch_layers.py:25-27); ``pos_std`` the position Linear's (default: ``head_std``); ``pos_bias`` an
+    optional position bias vector, e.g. a SPEED-range offset (0.3, -0.2, 12.0) m for regression heads."""
     arch = arch or mobilenet_v2()
     sd: Dict[str, np.ndarray] = {}
     m = _conv_bn(sd, arch.stem, seed, input_m2)
@@ -68,9 +73,12 @@ def synthetic_state_dict(arch: Arch | None = None, seed: int = 1001, head_std: f
             m = m + m_blk
     _conv_bn(sd, arch.last, seed, m)
     if arch.head == 'ursonet':
-        for name, n in (('head.pos.0', arch.n_pos), ('head.ori.1', arch.n_ori)):
-            sd[f'{name}.weight'] = _rng(seed, f'{name}.weight').normal(0.0, head_std, (n, LAST_CHANNELS))
+        for name, n, std in (('head.pos.0', arch.n_pos, head_std if pos_std is None else pos_std),
+                             ('head.ori.1', arch.n_ori, head_std)):
+            sd[f'{name}.weight'] = _rng(seed, f'{name}.weight').normal(0.0, std, (n, LAST_CHANNELS))
             sd[f'{name}.bias'] = np.zeros(n)
+        if pos_bias is not None:
+            sd['head.pos.0.bias'] = np.asarray(pos_bias, np.float64).reshape(arch.n_pos)
     else:
         sd['head.layer.1.weight'] = _rng(seed, 'head.layer.1.weight').normal(0.0, head_std,
                                                                              (arch.n_kp, 122880))

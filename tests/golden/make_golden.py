@@ -17,6 +17,15 @@ Fixtures (all small):
   encode.npz       reference OrientationSoftClassification.encode / PositionSoftClassification.encode.
   keypoints.npz    reference KeyPoints.create_keypoints2d for the 1,800 valid.json poses.
   score.npz        reference SPEUtils.get_score on perturbed poses.
+  predict_*.npz    reference SPETorch.predict (CPU) end to end -- forward + last_activ + decode -- for the
+                   three URSONet head modes the reference supports: 1232-bin orientation classification (the
+                   SPEUtils default, ORI_DELETE_UNUSED_BINS=True) + position regression at a SPEED-range
+                   bias; 1728-bin orientation + 1000-bin position classification; orientation regression
+                   (L2 normalise) + position regression.
+  kp_head_240x384_b2.npz  reference ModelWrapper(MobileNetV2, KeypointRegressionHead) raw outputs + the
+                   SPEUtils keypoint-mode sigmoid.
+
+Run with ``--only predict,kp_head`` to (re)write only the named groups.
 """
 from __future__ import annotations
 
@@ -79,7 +88,66 @@ def frames_u8(b, h, w, seed):
     return out
 
 
-def main(ref_root='/root/reference'):
+# predict fixture configs: name -> (SPEUtils args, arch (n_ori, n_pos), weight args, frames (b, h, w, seed))
+PREDICT_CASES = {
+    'predict_cls1232_posreg': (('classification', 12, 3, True, 'regression'), (1232, 3),
+                               dict(head_std=0.3, pos_std=0.01, pos_bias=(0.3, -0.2, 12.0)), (3, 160, 224, 21)),
+    'predict_cls1728_poscls': (('classification', 12, 3, False, 'classification'), (1728, 1000),
+                               dict(head_std=0.3, pos_std=0.05), (3, 128, 192, 22)),
+    'predict_orireg_posreg': (('regression', 12, 3, True, 'regression'), (4, 3),
+                              dict(head_std=0.01, pos_bias=(-1.1, 0.7, 25.0)), (3, 160, 224, 23)),
+}
+
+
+def predict_fixtures(ref_root):
+    """Reference SPETorch.predict on CPU (spe_torch.py:41-76) for each PREDICT_CASES entry."""
+    import torch
+    from src.modeling.backbone.mobilenet_v2 import MobileNetV2
+    from src.modeling.head.ursonet import URSONetHead
+    from src.modeling.common.pytorch_layers import ModelWrapper
+    from src.spe.spe_utils import SPEUtils
+    from src.spe.spe_torch import SPETorch
+    from src.data.datasets.speed import Camera
+    from spef_amd.weights import synthetic_state_dict, state_dict_digest
+    from spef_amd.arch import mobilenet_v2
+    for name, (su_args, (n_ori, n_pos), wargs, (b, h, w, fseed)) in PREDICT_CASES.items():
+        sd = synthetic_state_dict(mobilenet_v2('ursonet', n_ori, n_pos), seed=1001, **wargs)
+        model = ModelWrapper(MobileNetV2(3, 1280, True, True), URSONetHead(1280, n_ori, n_pos, True, 0.2))
+        model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+        su = SPEUtils(Camera(), *su_args)
+        spe = SPETorch(model, torch.device('cpu'), su)
+        fr = frames_u8(b, h, w, fseed)
+        x = torch.from_numpy(fr).permute(0, 3, 1, 2).float().div(255)     # ToTensor()
+        pose, _ = spe.predict(x)
+        out = {f'pose_{k}': np.asarray(v) for k, v in pose.items()}
+        np.savez_compressed(os.path.join(HERE, f'{name}.npz'), frames=fr, digest=state_dict_digest(sd),
+                            n_ori=n_ori, n_pos=n_pos, **out)
+        print(name, {k: v.shape for k, v in out.items()})
+
+
+def kp_head_fixture(ref_root):
+    """Reference ModelWrapper(MobileNetV2, KeypointRegressionHead) (head/keypoints.py:10-27) at 240x384."""
+    import torch
+    from src.modeling.backbone.mobilenet_v2 import MobileNetV2
+    from src.modeling.head.keypoints import KeypointRegressionHead
+    from src.modeling.common.pytorch_layers import ModelWrapper
+    from spef_amd.weights import synthetic_state_dict, state_dict_digest
+    from spef_amd.arch import mobilenet_v2
+    sd = synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=0.002)
+    model = ModelWrapper(MobileNetV2(3, 1280, True, True), KeypointRegressionHead(1280, 24, True, 0.2))
+    model.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
+    model.eval()
+    fr = frames_u8(2, 240, 384, 24)
+    x = torch.from_numpy(fr).permute(0, 3, 1, 2).float().div(255)
+    with torch.no_grad():
+        raw = model(x).numpy()
+    sig = 1 / (1 + np.exp(-raw))                                          # spe_utils.py:68
+    np.savez_compressed(os.path.join(HERE, 'kp_head_240x384_b2.npz'), frames=fr, raw=raw, sigmoid=sig,
+                        digest=state_dict_digest(sd))
+    print('kp head', raw.shape, float(np.abs(raw).max()))
+
+
+def main(ref_root='/root/reference', only=None):
     _install_stubs()
     sys.dont_write_bytecode = True
     sys.path.insert(0, ref_root)
@@ -95,6 +163,10 @@ def main(ref_root='/root/reference'):
 
     torch.set_num_threads(8)
     seed = 1001
+    if only:
+        for grp in only:
+            {'predict': predict_fixtures, 'kp_head': kp_head_fixture}[grp](ref_root)
+        return
 
     # ---------------------------------------------------------------- forward fixtures
     sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=seed)
@@ -174,7 +246,15 @@ def main(ref_root='/root/reference'):
     np.savez_compressed(os.path.join(HERE, 'score.npz'), q_true=q_true[:64], t_true=t_true[:64], q_pred=qp,
                         t_pred=tp, **{k: np.float64(v) for k, v in sc.items()})
     print('decode fixtures written')
+    predict_fixtures(ref_root)
+    kp_head_fixture(ref_root)
 
 
 if __name__ == '__main__':
-    main(*sys.argv[1:])
+    args = sys.argv[1:]
+    only = None
+    if '--only' in args:
+        i = args.index('--only')
+        only = args[i + 1].split(',')
+        del args[i:i + 2]
+    main(*args, only=only)

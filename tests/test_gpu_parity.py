@@ -225,19 +225,3 @@ def test_wave_specialised_blocks_bit_identical_to_slab(engine, b, h, w):
             assert np.array_equal(u, f), (op, np.abs(u.astype(np.float32) - f.astype(np.float32)).max())
     finally:
         engine.set_option(L.OPT_WAVESPEC, 1)
-
-
-@pytest.mark.parametrize('b,h,w', [(2, 512, 512), (3, 240, 384)])
-def test_strip_blocks_vs_oracle(engine, sd, b, h, w):
-    """Experimental register-streaming blocks (k_irs.hip, SPEF_OPT_STRIP=1) keep the expand output in fp32 and
-    permute the project's K order, so they are compared with the FP32 oracle at the logit tolerance."""
-    from spef_amd import _lib as L
-    fr = _frames(b, h, w, 5 + h)
-    try:
-        engine.set_option(L.OPT_STRIP, 1)
-        ori, pos = engine.forward(torch.from_numpy(fr).cuda())
-    finally:
-        engine.set_option(L.OPT_STRIP, 0)
-    ro, rp = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd)
-    assert float((ori.cpu() - ro).abs().max()) < 1e-3
-    assert float((pos.cpu() - rp).abs().max()) < 1e-3
