@@ -70,11 +70,12 @@ def _flags(src: str):
 
 def source_digest() -> str:
     """SHA-256 over every source and header (path + content) and the compile / link flags."""
+    top = os.path.dirname(ROOT)
     h = hashlib.sha256()
     for p in _sources() + _headers():
-        h.update(os.path.relpath(p, os.path.dirname(ROOT)).encode())
+        h.update(os.path.relpath(p, top).encode())
         h.update(_file_sha(p).encode())
-        h.update(' '.join(_flags(p)).encode())
+        h.update(' '.join(_flags(p)).replace(top, '<repo>').encode())   # -I paths: location-independent
     h.update(' '.join(LDFLAGS).encode())
     return h.hexdigest()
 

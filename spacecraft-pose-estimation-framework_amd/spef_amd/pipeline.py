@@ -22,11 +22,17 @@ from .engine import Engine
 
 class StreamPipeline:
     def __init__(self, blob, device, depth: int = 3, ori_bins: Optional[np.ndarray] = None,
-                 pos_grid: Optional[np.ndarray] = None):
+                 pos_grid: Optional[np.ndarray] = None, comm=None, root: int = 0):
+        """``blob``: the packed weights (host bytes or device tensor). With ``comm`` (a ``shard.RcclComm``), only
+        rank ``root`` passes a blob (the others None) and every context receives the root's weights over RCCL
+        (``spef_bcast_weights``, collective)."""
         assert depth >= 1
         self.device = torch.device(device)
         self.depth = depth
         self.engines: List[Engine] = [Engine(blob, self.device) for _ in range(depth)]
+        if comm is not None:
+            for e in self.engines:
+                e.bcast_weights(comm, root)
         for e in self.engines:
             e.set_decode_tables(ori_bins, pos_grid)
         self.streams = [torch.cuda.Stream(self.device) for _ in range(depth)]

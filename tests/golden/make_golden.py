@@ -41,6 +41,7 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 REPO = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, os.path.join(REPO, 'spacecraft-pose-estimation-framework_amd'))
+sys.path.insert(0, HERE)
 
 
 def _install_stubs():
@@ -88,15 +89,7 @@ def frames_u8(b, h, w, seed):
     return out
 
 
-# predict fixture configs: name -> (SPEUtils args, arch (n_ori, n_pos), weight args, frames (b, h, w, seed))
-PREDICT_CASES = {
-    'predict_cls1232_posreg': (('classification', 12, 3, True, 'regression'), (1232, 3),
-                               dict(head_std=0.3, pos_std=0.01, pos_bias=(0.3, -0.2, 12.0)), (3, 160, 224, 21)),
-    'predict_cls1728_poscls': (('classification', 12, 3, False, 'classification'), (1728, 1000),
-                               dict(head_std=0.3, pos_std=0.05), (3, 128, 192, 22)),
-    'predict_orireg_posreg': (('regression', 12, 3, True, 'regression'), (4, 3),
-                              dict(head_std=0.01, pos_bias=(-1.1, 0.7, 25.0)), (3, 160, 224, 23)),
-}
+from cases import PREDICT_CASES  # noqa: E402  (shared with tests/test_gpu_predict_modes.py)
 
 
 def predict_fixtures(ref_root):

@@ -150,12 +150,14 @@ def test_decode_nan_raises(engine):
 
 
 def test_predict_end_to_end():
-    """SPEMi355x.predict == oracle forward + reference decode on identical inputs (<0.1 deg, <1 mm).
-    A sharper head (std 0.3) gives peaked orientation histograms: with the reference init (std 0.01) the
-    softmax is near-uniform and the top eigenvector of `a` is ill-conditioned for ANY implementation."""
+    """SPEMi355x.predict == oracle forward + reference decode on identical inputs (<0.1 deg, <1 mm absolute).
+    A sharper orientation head (std 0.3) gives peaked orientation histograms: with the reference init (std 0.01)
+    the softmax is near-uniform and the top eigenvector of `a` is ill-conditioned for ANY implementation. The
+    position head keeps the reference init (pytorch_layers.py:25-27) with a SPEED-range bias (12 m range)."""
     from spef_amd.spe.spe_utils import SPEUtils
     from spef_amd.spe_mi355x import SPEMi355x
-    sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=1001, head_std=0.3)
+    sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=1001, head_std=0.3, pos_std=0.01,
+                              pos_bias=(0.4, -0.3, 12.0))
     su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
     tgt = SPEMi355x(Bl.pack(sd, dtype='fp16'), 'cuda:0', su)
     fr = _frames(4, 240, 384, 9)
@@ -166,9 +168,8 @@ def test_predict_end_to_end():
     h, _ = D.orientation_histogram(12, False)
     rq = D.decode_orientation_batch(D.softmax_f32(ro.numpy()), h)
     assert D.angle_deg_stable(pose['ori'], rq).max() < 0.1
-    # fp16 activation storage: position regression error is relative (~1.5e-3 of |pos|), see DESIGN.md
-    # "Precision"; the exact-fp32 blob variant meets the absolute 1 mm bound (test_fp32_variant_exact).
-    assert (np.abs(pose['pos'] - rp.numpy()) <= 1e-3 + 2e-3 * np.abs(rp.numpy())).all()
+    assert np.abs(pose['pos'] - rp.numpy()).max() < 1e-3           # < 1 mm, absolute
+    assert np.abs(rp.numpy()[:, 2] - 12.0).max() < 1.0              # the position is at SPEED range
     assert pose['ori_soft'].shape == (4, 1728)
     tgt.close()
 
