@@ -121,8 +121,9 @@ int spef_preprocess(spef_ctx* ctx, const uint8_t* frames, int B, int Hin, int Wi
 /* Schedule options (both choices of each are bit-identical; the parity tests switch them):
  * SPEF_OPT_FUSE_BLOCKS (default 1): each inverted-residual block as one fused kernel (expand + depthwise + project
  *   on-chip); 0 = one kernel per conv (the reference's module-by-module schedule).
- * SPEF_OPT_WAVESPEC (default 1): wave-specialised fused kernels for the low-resolution blocks (expand waves and
- *   depthwise/project waves pipelined over hidden chunks); 0 = LDS-slab fused kernels everywhere.
+ * SPEF_OPT_WAVESPEC (default 2): role-split fused kernels for the low-resolution blocks. 2 = three-stage pipeline
+ *   (MFMA waves expand + project, VALU waves depthwise); 1 = two-stage (expand waves, depthwise + project waves);
+ *   0 = LDS-slab fused kernels everywhere.
  * (Kernel-tuning knobs used by the sweep tools are internal: csrc/spef_tuning.hpp.) */
 enum spef_option {
   SPEF_OPT_FUSE_BLOCKS = 1,

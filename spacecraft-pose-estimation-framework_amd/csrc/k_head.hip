@@ -4,7 +4,7 @@
 //                      concatenated into one fp32 GEMM on the exact f32-input MFMA (v_mfma_f32_16x16x4_f32)
 //   decode_ori_kernel  SPEUtils.last_activ softmax (src/spe/spe_utils.py:75-76) fused with
 //                      OrientationSoftClassification.decode (src/spe/classification_utils.py:113-146):
-//                      a = sum_i p_i q_i q_i^T in fp64, top eigenvector by cyclic Jacobi, normalised
+//                      a = sum_i p_i q_i q_i^T in fp64, top eigenvector by repeated squaring, normalised
 //   decode_pos_kernel  softmax (spe_utils.py:78-79) + PositionSoftClassification.decode
 //                      (classification_utils.py:242-267): 3-D soft-argmax over the bin grid
 //   normalize_ori      orientation regression L2 normalisation (spe_utils.py:72)
@@ -22,13 +22,18 @@ namespace spef {
 // interleaved quarters of K (split-K inside the workgroup, reduced through LDS in a fixed order, so the
 // result is deterministic). Lane l loads float4 W[i0+(l&15)][t+4(l>>4)..] and X[j0+(l&15)][t+4(l>>4)..];
 // MFMA step e takes element e from both, so A and B see the same k.
+// 1-D grid, XCD-aware: the nJ image groups of one 16-row weight tile are consecutive logical ids, which
+// xcd_remap places on one XCD, so the fp32 weight (8.85 MB for 1728 bins) is fetched from HBM once per batch
+// and re-read from that XCD's L2 by the other image groups (round-robin placement fetched it once per group).
 __global__ __launch_bounds__(256) void fc_kernel(const float* __restrict__ X, const float* __restrict__ W,
                                                  const float* __restrict__ bias, float* __restrict__ out0, int n0,
                                                  float* __restrict__ out1, int n1, int B, int K, int Np) {
   __shared__ f32x4 part[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i0 = blockIdx.x * 16;
-  const int j0 = blockIdx.y * 16;
+  const uint32_t nJ = (uint32_t)(B + 15) / 16;
+  const uint32_t L = xcd_remap(blockIdx.x, gridDim.x);
+  const int i0 = (int)(L / nJ) * 16;
+  const int j0 = (int)(L % nJ) * 16;
   const int r16 = lane & 15, kg = lane >> 4;
   const float* wp = W + (size_t)(i0 + r16) * K + 4 * kg;
   const int j = j0 + r16;
@@ -65,7 +70,11 @@ __global__ __launch_bounds__(256) void fc_partial_kernel(const float* __restrict
                                                          float* __restrict__ part, int B, int K, int Np, int kslice) {
   __shared__ f32x4 red[4][64];
   const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int i0 = blockIdx.x * 16, j0 = blockIdx.y * 16, z = blockIdx.z;
+  const uint32_t nJ = (uint32_t)(B + 15) / 16, nI = (uint32_t)Np / 16;
+  uint32_t L = xcd_remap(blockIdx.x, gridDim.x);       // image groups of one (slice, row tile) on one XCD
+  const int j0 = (int)(L % nJ) * 16;
+  L /= nJ;
+  const int i0 = (int)(L % nI) * 16, z = (int)(L / nI);
   const int r16 = lane & 15, kg = lane >> 4;
   const int j = j0 + r16;
   const bool jv = j < B;
@@ -116,59 +125,56 @@ __device__ __forceinline__ float block_sum256(float v, float* sh) {
   return (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
-// Cyclic Jacobi on a symmetric 4x4 (fp64): returns the unit eigenvector of the largest eigenvalue.
-__device__ void sym4_top_eigvec(double a[4][4], double out[4]) {
-  double v[4][4] = {{1, 0, 0, 0}, {0, 1, 0, 0}, {0, 0, 1, 0}, {0, 0, 0, 1}};
-  for (int sweep = 0; sweep < 32; ++sweep) {
-    double off = 0.0, diag = 0.0;
+// Top eigenvector of the symmetric PSD 4x4 a (fp64) by repeated squaring: M <- M^2 / tr(M^2) from M = a / tr(a)
+// multiplies the eigenvalue ratios (l_i / l_1) by themselves each step, so after k steps M is l_1-dominated to
+// (l_2 / l_1)^(2^k); stop when M is rank one to fp64 precision (tr(M^2) = tr(M)^2 = 1), at most 40 steps. The
+// eigenvector is M's column of largest diagonal entry, polished by two power steps with a. Replaces np.linalg.eig
+// (classification_utils.py:137-141); ~7 squarings (<= 11 on every golden/random/near-uniform case, equal to
+// numpy's eigenvector in float32) -- a short dependent chain of independent FMAs where cyclic Jacobi spent ~20 us
+// of fp64 divides and square roots on one lane.
+__device__ void sym4_top_eigvec(const double t[10], double out[4]) {
+  // packed upper triangle: 0:00 1:01 2:02 3:03 4:11 5:12 6:13 7:22 8:23 9:33
+  const double tr0 = (t[0] + t[4]) + (t[7] + t[9]);
+  const double s0 = 1.0 / tr0;
+  double m[10];
 #pragma unroll
-    for (int p = 0; p < 4; ++p) {
-      diag += a[p][p] * a[p][p];
+  for (int k = 0; k < 10; ++k) m[k] = t[k] * s0;
+  for (int it = 0; it < 40; ++it) {
+    const double m00 = m[0], m01 = m[1], m02 = m[2], m03 = m[3], m11 = m[4], m12 = m[5], m13 = m[6], m22 = m[7],
+                 m23 = m[8], m33 = m[9];
+    double q[10];
+    q[0] = m00 * m00 + m01 * m01 + m02 * m02 + m03 * m03;
+    q[1] = m00 * m01 + m01 * m11 + m02 * m12 + m03 * m13;
+    q[2] = m00 * m02 + m01 * m12 + m02 * m22 + m03 * m23;
+    q[3] = m00 * m03 + m01 * m13 + m02 * m23 + m03 * m33;
+    q[4] = m01 * m01 + m11 * m11 + m12 * m12 + m13 * m13;
+    q[5] = m01 * m02 + m11 * m12 + m12 * m22 + m13 * m23;
+    q[6] = m01 * m03 + m11 * m13 + m12 * m23 + m13 * m33;
+    q[7] = m02 * m02 + m12 * m12 + m22 * m22 + m23 * m23;
+    q[8] = m02 * m03 + m12 * m13 + m22 * m23 + m23 * m33;
+    q[9] = m03 * m03 + m13 * m13 + m23 * m23 + m33 * m33;
+    const double tr = (q[0] + q[4]) + (q[7] + q[9]);
+    const double s = 1.0 / tr;
 #pragma unroll
-      for (int q = p + 1; q < 4; ++q) off += a[p][q] * a[p][q];
-    }
-    if (off <= 1e-34 * diag || off == 0.0) break;
-#pragma unroll
-    for (int p = 0; p < 3; ++p)
-#pragma unroll
-      for (int q = p + 1; q < 4; ++q) {
-        const double apq = a[p][q];
-        if (apq == 0.0) continue;
-        const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
-        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
-        for (int k = 0; k < 4; ++k) {  // A <- A J (columns p, q)
-          const double akp = a[k][p], akq = a[k][q];
-          a[k][p] = c * akp - s * akq;
-          a[k][q] = s * akp + c * akq;
-        }
-        for (int k = 0; k < 4; ++k) {  // A <- J^T A (rows p, q)
-          const double apk = a[p][k], aqk = a[q][k];
-          a[p][k] = c * apk - s * aqk;
-          a[q][k] = s * apk + c * aqk;
-        }
-        for (int k = 0; k < 4; ++k) {  // V <- V J
-          const double vkp = v[k][p], vkq = v[k][q];
-          v[k][p] = c * vkp - s * vkq;
-          v[k][q] = s * vkp + c * vkq;
-        }
-      }
+    for (int k = 0; k < 10; ++k) m[k] = q[k] * s;
+    if (tr >= 1.0 - 1e-15) break;
   }
-  // column of the largest diagonal entry, selected with static indices only (no scratch)
-  double bd = a[0][0], col[4] = {v[0][0], v[1][0], v[2][0], v[3][0]};
+  // column of the largest diagonal entry (static indices only: no scratch)
+  double v[4] = {m[0], m[1], m[2], m[3]}, bd = m[0];
+  if (m[4] > bd) { bd = m[4]; v[0] = m[1]; v[1] = m[4]; v[2] = m[5]; v[3] = m[6]; }
+  if (m[7] > bd) { bd = m[7]; v[0] = m[2]; v[1] = m[5]; v[2] = m[7]; v[3] = m[8]; }
+  if (m[9] > bd) { v[0] = m[3]; v[1] = m[6]; v[2] = m[8]; v[3] = m[9]; }
 #pragma unroll
-  for (int p = 1; p < 4; ++p)
-    if (a[p][p] > bd) {
-      bd = a[p][p];
+  for (int r = 0; r < 2; ++r) {
+    const double w0 = t[0] * v[0] + t[1] * v[1] + t[2] * v[2] + t[3] * v[3];
+    const double w1 = t[1] * v[0] + t[4] * v[1] + t[5] * v[2] + t[6] * v[3];
+    const double w2 = t[2] * v[0] + t[5] * v[1] + t[7] * v[2] + t[8] * v[3];
+    const double w3 = t[3] * v[0] + t[6] * v[1] + t[8] * v[2] + t[9] * v[3];
+    const double n = 1.0 / sqrt((w0 * w0 + w1 * w1) + (w2 * w2 + w3 * w3));
+    v[0] = w0 * n; v[1] = w1 * n; v[2] = w2 * n; v[3] = w3 * n;
+  }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) col[k] = v[k][p];
-    }
-  double n = 0.0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) n += col[k] * col[k];
-  n = sqrt(n);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) out[k] = col[k] / n;
+  for (int k = 0; k < 4; ++k) out[k] = v[k];
 }
 
 // ------------------------------------------------------------------------------------------ decode ori
@@ -215,9 +221,8 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
     for (int k = 0; k < 4; ++k) quat[4 * b + k] = NAN;
     return;
   }
-  double a[4][4] = {{t[0], t[1], t[2], t[3]}, {t[1], t[4], t[5], t[6]}, {t[2], t[5], t[7], t[8]}, {t[3], t[6], t[8], t[9]}};
   double q[4];
-  sym4_top_eigvec(a, q);
+  sym4_top_eigvec(t, q);
   for (int k = 0; k < 4; ++k) quat[4 * b + k] = (float)q[k];
 }
 
@@ -277,8 +282,9 @@ hipError_t launch_fc(const float* x, const float* w, const float* bias, float* o
                      int K, hipStream_t s) {
   if (K % 16) return hipErrorInvalidValue;
   const int Np = (n0 + n1 + 15) & ~15;
-  dim3 g(Np / 16, (B + 15) / 16);
-  fc_kernel<<<g, 256, 0, s>>>(x, w, bias, out0, n0, out1, n1, B, K, Np);
+  const int64_t nwg = (int64_t)(Np / 16) * ((B + 15) / 16);
+  if (nwg > 0x7fffffff) return hipErrorInvalidValue;
+  fc_kernel<<<(uint32_t)nwg, 256, 0, s>>>(x, w, bias, out0, n0, out1, n1, B, K, Np);
   return hipGetLastError();
 }
 
@@ -289,8 +295,9 @@ hipError_t launch_fc_splitk(const float* x, const float* w, const float* bias, f
   int kslice = (K + splits - 1) / splits;
   kslice = (kslice + 63) / 64 * 64;
   splits = (K + kslice - 1) / kslice;
-  dim3 g(Np / 16, (B + 15) / 16, splits);
-  fc_partial_kernel<<<g, 256, 0, s>>>(x, w, part, B, K, Np, kslice);
+  const int64_t nwg = (int64_t)(Np / 16) * ((B + 15) / 16) * splits;
+  if (nwg > 0x7fffffff) return hipErrorInvalidValue;
+  fc_partial_kernel<<<(uint32_t)nwg, 256, 0, s>>>(x, w, part, B, K, Np, kslice);
   fc_reduce_kernel<<<(B * n + 255) / 256, 256, 0, s>>>(part, bias, out, n, B, Np, splits);
   return hipGetLastError();
 }

@@ -49,6 +49,7 @@ struct IrwGeom {
   static_assert(CIN % 8 == 0 && HID % 16 == 0 && COUT % 8 == 0, "channel counts");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
   static_assert(EPT <= 32, "validity mask is 32 bits");
+  static_assert(2 * NCH + 8 <= SPEF_TRACE_SLOTS, "trace slots");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
@@ -73,6 +74,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
+  SPEF_TRACE(0);
   uint32_t L = xcd_remap(blockIdx.x, nwg);
   const int tx = (int)(L % (uint32_t)tiles_x);
   L /= (uint32_t)tiles_x;
@@ -130,6 +132,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       if (dst) *reinterpret_cast<uint4*>(dst) = v[i];
     }
   }
+  SPEF_TRACE(1);
 
   const bool is_expand = wave < NE;   // wave-uniform role
 
@@ -239,17 +242,23 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       }
     }
     load_ea(0);
+    SPEF_TRACE(2);
     __syncthreads();                                      // input tile, depthwise weights, biases visible
+    SPEF_TRACE(3);
     expand(0);
     load_ea(1);
+    SPEF_TRACE(4);
     __syncthreads();                                      // Es[0] visible
+    SPEF_TRACE(5);
 #pragma unroll 1
     for (int c = 0; c < G::NCH; ++c) {
       if (c + 1 < G::NCH) {
         expand(c + 1);          // into Es[(c+1) & 1]: last read by the depthwise of chunk c-1, before the barrier
         load_ea(c + 2);
       }
+      SPEF_TRACE(6 + 2 * c);
       __syncthreads();          // Es[(c+1) & 1] complete; Es[c & 1] free for chunk c+2
+      SPEF_TRACE(7 + 2 * c);
     }
   } else {
 #pragma unroll
@@ -259,8 +268,15 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       for (int qi = 0; qi < G::QPW; ++qi) acc[qi][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
     }
     load_pa(0);
+    SPEF_TRACE(2);
     __syncthreads();
+    SPEF_TRACE(3);
+    SPEF_TRACE(4);
     __syncthreads();
+    SPEF_TRACE(5);
+    // Retire load_pa(0) before the loop: otherwise the loop header merges "pa pending" from this edge, and the
+    // waitcnt pass makes every chunk's project MFMAs wait for the next chunk's fragment loads issued just before.
+    __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
 #pragma unroll 1
     for (int c = 0; c < G::NCH; ++c) {
       const T* Es = Es0 + (c & 1) * G::PINP * G::ES;
@@ -281,6 +297,12 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
         db[0] = u0.x; db[1] = u0.y; db[2] = u0.z; db[3] = u0.w;
         db[4] = u1.x; db[5] = u1.y; db[6] = u1.z; db[7] = u1.w;
       }
+      // the chunk's 9 depthwise weight vectors, read once for all of this wave's pixel tiles
+      DW8<DT> wt[9];
+      if (hv) {
+#pragma unroll
+        for (int tap = 0; tap < 9; ++tap) wt[tap].load(sl + tap * G::HIDP + 8 * kg);
+      }
       if constexpr (G::PAIR) {
 #pragma unroll
         for (int qi = 0; qi < G::QPW; qi += 2) {
@@ -291,10 +313,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
             for (int e = 0; e < 8; ++e) a0[e] = a1[e] = db[e];
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx) {
-              DW8<DT> w[3];
-#pragma unroll
-              for (int ky = 0; ky < 3; ++ky) w[ky].load(sl + (ky * 3 + kx) * G::HIDP + 8 * kg);
-              x8 v[4];
+              x8 v[4];                                     // the column's 4 window rows, read together
 #pragma unroll
               for (int r = 0; r < 4; ++r)
                 v[r] = *reinterpret_cast<const x8*>(Es + ((oyq[qi] + r) * G::IW + oxq[qi] + kx) * G::ES + 8 * kg);
@@ -302,8 +321,8 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
               for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
                 for (int e = 0; e < 8; ++e) {
-                  a0[e] = fmaf((float)v[ky][e], w[ky][e], a0[e]);
-                  a1[e] = fmaf((float)v[ky + 1][e], w[ky][e], a1[e]);
+                  a0[e] = fmaf((float)v[ky][e], wt[ky * 3 + kx][e], a0[e]);
+                  a1[e] = fmaf((float)v[ky + 1][e], wt[ky * 3 + kx][e], a1[e]);
                 }
             }
             bf0 = relu_cvt8<DT>(a0);
@@ -320,20 +339,22 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
         for (int qi = 0; qi < G::QPW; ++qi) {
           x8 bf = zero8<DT>();
           if (hv) {
+            x8 v[9];                                       // the 3x3 window, all reads before the first FMA
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+              for (int ky = 0; ky < 3; ++ky)
+                v[kx * 3 + ky] = *reinterpret_cast<const x8*>(
+                    Es + ((oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx)) * G::ES + 8 * kg);
             float a8[8];
 #pragma unroll
             for (int e = 0; e < 8; ++e) a8[e] = db[e];
 #pragma unroll
             for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
-              for (int ky = 0; ky < 3; ++ky) {
-                const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
-                const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + 8 * kg);
-                DW8<DT> wt;
-                wt.load(sl + (ky * 3 + kx) * G::HIDP + 8 * kg);
+              for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
-                for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[e], wt[e], a8[e]);
-              }
+                for (int e = 0; e < 8; ++e) a8[e] = fmaf((float)v[kx * 3 + ky][e], wt[ky * 3 + kx][e], a8[e]);
             bf = relu_cvt8<DT>(a8);
           }
 #pragma unroll
@@ -342,7 +363,9 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       }
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) pa[t] = pn[t];
+      SPEF_TRACE(6 + 2 * c);
       __syncthreads();
+      SPEF_TRACE(7 + 2 * c);
     }
   }
 
@@ -371,6 +394,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       }
     }
   }
+  SPEF_TRACE(SPEF_TRACE_SLOTS - 1);
 }
 
 // (variant, cin, hidden, cout, stride, TH x TW tile, residual, expand waves, depthwise waves, cout groups).

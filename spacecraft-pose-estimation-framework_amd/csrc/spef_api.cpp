@@ -66,7 +66,7 @@ struct spef_ctx {
   int64_t fuse_min_hw = 0;   // SPEF_OPT_FUSE_MIN_HW
   int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
   int irb_variant = 0;       // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps)
-  int wavespec = 1;          // SPEF_OPT_WAVESPEC: wave-specialised fused blocks (k_irw.hip) where available
+  int wavespec = 2;          // SPEF_OPT_WAVESPEC: 2 = pipelined (k_irp.hip), 1 = wave-specialised (k_irw.hip)
   // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
   std::vector<double> q8_sw, q8_bias;
   std::vector<int32_t> q8_wsum;
@@ -280,12 +280,18 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const double bytes = (double)M * op.cin * 2 + (double)M2 * op.cout * 2 +
                              (expand ? pw_bytes(0, op.cin, op.hidden, false) : 0) + 40.0 * op.hidden +
                              pw_bytes(0, op.hidden, op.cout, false);
-        const bool wspec = c->wavespec &&
+        const bool pipe3 = c->wavespec >= 2 &&
+                           irp_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res);
+        const bool wspec = !pipe3 && c->wavespec &&
                            irw_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res);
         char key[96];
-        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", wspec ? "irw_kernel" : "irb_kernel", op.cin,
-                 op.hidden, op.cout, op.stride);
+        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", pipe3 ? "irp_kernel" : wspec ? "irw_kernel" : "irb_kernel",
+                 op.cin, op.hidden, op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
+          if (pipe3)
+            return launch_irp(c->irb_variant, dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, x,
+                              ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<void>(c, op.w1), ptr<float>(c, op.b1),
+                              ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
           if (wspec)
             return launch_irw(c->irb_variant, dt, (int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, x, ptr<void>(c, op.w0),
                               ptr<float>(c, op.b0), ptr<void>(c, op.w1), ptr<float>(c, op.b1), ptr<void>(c, op.w2),
@@ -1298,7 +1304,8 @@ int spef_set_option(spef_ctx* c, int option, int value) {
     return SPEF_OK;
   }
   if (option == SPEF_OPT_WAVESPEC) {
-    c->wavespec = value != 0;
+    if (value < 0 || value > 2) return fail(SPEF_ERR_ARG, "SPEF_OPT_WAVESPEC: 0, 1 or 2");
+    c->wavespec = value;
     return SPEF_OK;
   }
   return fail(SPEF_ERR_ARG, "unknown option");

@@ -160,4 +160,21 @@ __device__ __forceinline__ double warp_sum_d(double v) {
   return v;
 }
 
+// Per-wave timeline probes for the kernel tracing harness (tools/kbench): compiled to nothing in the library.
+// With SPEF_KTRACE defined, SPEF_TRACE(slot) stores s_memtime of the calling wave into
+// spef_ktrace[(workgroup * 16 + wave) * SPEF_TRACE_SLOTS + slot] (lane 0 only, vector store). The counter is per
+// XCD: only deltas within one workgroup are meaningful.
+#define SPEF_TRACE_SLOTS 72
+#ifdef SPEF_KTRACE
+__device__ unsigned long long* spef_ktrace;
+#define SPEF_TRACE(slot)                                                                                        \
+  do {                                                                                                          \
+    const unsigned long long t_ = __builtin_amdgcn_s_memtime();                                                 \
+    if ((threadIdx.x & 63) == 0)                                                                                \
+      spef_ktrace[((size_t)blockIdx.x * 16 + (threadIdx.x >> 6)) * SPEF_TRACE_SLOTS + (slot)] = t_;              \
+  } while (0)
+#else
+#define SPEF_TRACE(slot) ((void)0)
+#endif
+
 }  // namespace spef

@@ -50,6 +50,11 @@ hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int st
 
 // Wave-specialised fused block (expand waves feed depthwise/project waves through a double-buffered LDS slab) for
 // the low-resolution geometries in k_irw.hip's table (same contract, bit-identical to the unfused kernels).
+// Three-stage pipelined fused block (k_irp.hip): MFMA waves expand + project, VALU waves depthwise; same contract.
+bool irp_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
+hipError_t launch_irp(int variant, int dtype, int cin, int hid, int cout, int stride, bool res, const void* x, const void* we,
+                      const float* be, const void* wd, const float* bd, const void* wp, const float* bp, void* y, int B,
+                      int H, int W, int OH, int OW, hipStream_t s);
 bool irw_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
 hipError_t launch_irw(int variant, int dtype, int cin, int hid, int cout, int stride, bool res, const void* x, const void* we,
                       const float* be, const void* wd, const float* bd, const void* wp, const float* bp, void* y,

@@ -211,18 +211,22 @@ def test_front_kernel_vs_stem_block1(engine, sd, b, h, w):
     assert np.abs(got - ref).max() / scale < 4e-3
 
 
-@pytest.mark.parametrize('b,h,w', [(2, 512, 512), (2, 100, 136)])
-def test_wave_specialised_blocks_bit_identical_to_slab(engine, b, h, w):
-    """k_irw.hip (expand waves pipelined against depthwise/project waves) keeps the slab kernel's rounding points
-    and accumulation order: every late-block output is bit-identical with SPEF_OPT_WAVESPEC on and off."""
+@pytest.mark.parametrize('b,h,w', [(2, 512, 512), (2, 100, 136), (1, 240, 384)])
+def test_role_split_blocks_bit_identical_to_slab(engine, b, h, w):
+    """k_irp.hip (three-stage pipeline: MFMA waves expand + project, VALU waves depthwise) and k_irw.hip (expand
+    waves pipelined against depthwise/project waves) keep the slab kernel's rounding points and accumulation order:
+    every late-block output is bit-identical under SPEF_OPT_WAVESPEC 0, 1 and 2 (ragged maps included: 100x136
+    frames give 7x9 and 4x5 maps, partial tiles everywhere)."""
     from spef_amd import _lib as L
     fr = torch.from_numpy(_frames(b, h, w, 31 + w)).cuda()
     try:
         for op in range(8, 18):
-            engine.set_option(L.OPT_WAVESPEC, 0)
-            u = engine.probe(fr, op).cpu().numpy()
-            engine.set_option(L.OPT_WAVESPEC, 1)
-            f = engine.probe(fr, op).cpu().numpy()
-            assert np.array_equal(u, f), (op, np.abs(u.astype(np.float32) - f.astype(np.float32)).max())
+            outs = []
+            for mode in (0, 1, 2):
+                engine.set_option(L.OPT_WAVESPEC, mode)
+                outs.append(engine.probe(fr, op).cpu().numpy())
+            for mode in (1, 2):
+                assert np.array_equal(outs[0], outs[mode]), (
+                    op, mode, np.abs(outs[0].astype(np.float32) - outs[mode].astype(np.float32)).max())
     finally:
-        engine.set_option(L.OPT_WAVESPEC, 1)
+        engine.set_option(L.OPT_WAVESPEC, 2)
