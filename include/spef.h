@@ -83,7 +83,8 @@ int spef_probe(spef_ctx* ctx, const void* input, int layout, int B, int H, int W
                int* c, int* h, int* w, void* stream);
 
 /* Decode constants (host, float64, as built by OrientationSoftClassification.build_histogram,
- * classification_utils.py:39-83, and PositionSoftClassification.build_histogram, :201-215). */
+ * classification_utils.py:39-83, and PositionSoftClassification.build_histogram, :201-215). At most 8192
+ * orientation bins (SPEF_ERR_ARG above; the default 12^3 grid has 1728, 1232 with unused bins deleted). */
 int spef_set_decode_tables(spef_ctx* ctx, const double* ori_bins, int n_ori_bins, const double* pos_grid,
                            int n_pos_bins);
 

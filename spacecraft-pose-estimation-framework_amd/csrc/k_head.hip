@@ -9,7 +9,7 @@
 //                      (classification_utils.py:242-267): 3-D soft-argmax over the bin grid
 //   normalize_ori      orientation regression L2 normalisation (spe_utils.py:72)
 // One 256-thread workgroup decodes one image (the reference loops over images in Python,
-// classification_utils.py:163-164).
+// classification_utils.py:163-164); the orientation decode supports up to 8192 bins.
 #include <math.h>
 
 #include "spef_common.hpp"
@@ -125,23 +125,26 @@ __device__ __forceinline__ float block_sum256(float v, float* sh) {
   return (sh[0] + sh[1]) + (sh[2] + sh[3]);
 }
 
-// Top eigenvector of the symmetric PSD 4x4 a (fp64) by repeated squaring: M <- M^2 / tr(M^2) from M = a / tr(a)
-// multiplies the eigenvalue ratios (l_i / l_1) by themselves each step, so after k steps M is l_1-dominated to
-// (l_2 / l_1)^(2^k); stop when M is rank one to fp64 precision (tr(M^2) = tr(M)^2 = 1), at most 40 steps. The
-// eigenvector is M's column of largest diagonal entry, polished by two power steps with a. Replaces np.linalg.eig
-// (classification_utils.py:137-141); ~7 squarings (<= 11 on every golden/random/near-uniform case, equal to
-// numpy's eigenvector in float32) -- a short dependent chain of independent FMAs where cyclic Jacobi spent ~20 us
-// of fp64 divides and square roots on one lane.
+// Top eigenvector of the symmetric PSD 4x4 a (fp64, packed upper triangle t) by repeated squaring: each step
+// M <- M^2 multiplies the eigenvalue ratios (l_i / l_1) by themselves, so after k steps M is l_1-dominated to
+// (l_2 / l_1)^(2^k); M is rescaled by a power of two each step (exact, no division) and the loop stops when M is
+// rank one to fp64 precision (tr(M^2) = tr(M)^2), at most 40 steps. The eigenvector is M's column of largest
+// diagonal entry, polished by two power steps with a. Replaces np.linalg.eig (classification_utils.py:137-141):
+// ~7 squarings (<= 11 on every golden/random/near-uniform case, equal to numpy's eigenvector in float32), a short
+// dependent chain of independent FMAs where cyclic Jacobi spent ~20 us of fp64 divides and square roots on one lane.
 __device__ void sym4_top_eigvec(const double t[10], double out[4]) {
   // packed upper triangle: 0:00 1:01 2:02 3:03 4:11 5:12 6:13 7:22 8:23 9:33
-  const double tr0 = (t[0] + t[4]) + (t[7] + t[9]);
-  const double s0 = 1.0 / tr0;
   double m[10];
+  {
+    int e;
+    frexp((t[0] + t[4]) + (t[7] + t[9]), &e);
 #pragma unroll
-  for (int k = 0; k < 10; ++k) m[k] = t[k] * s0;
+    for (int k = 0; k < 10; ++k) m[k] = ldexp(t[k], -e);
+  }
   for (int it = 0; it < 40; ++it) {
     const double m00 = m[0], m01 = m[1], m02 = m[2], m03 = m[3], m11 = m[4], m12 = m[5], m13 = m[6], m22 = m[7],
                  m23 = m[8], m33 = m[9];
+    const double trm = (m00 + m11) + (m22 + m33);
     double q[10];
     q[0] = m00 * m00 + m01 * m01 + m02 * m02 + m03 * m03;
     q[1] = m00 * m01 + m01 * m11 + m02 * m12 + m03 * m13;
@@ -154,10 +157,11 @@ __device__ void sym4_top_eigvec(const double t[10], double out[4]) {
     q[8] = m02 * m03 + m12 * m13 + m22 * m23 + m23 * m33;
     q[9] = m03 * m03 + m13 * m13 + m23 * m23 + m33 * m33;
     const double tr = (q[0] + q[4]) + (q[7] + q[9]);
-    const double s = 1.0 / tr;
+    int e;
+    frexp(tr, &e);
 #pragma unroll
-    for (int k = 0; k < 10; ++k) m[k] = q[k] * s;
-    if (tr >= 1.0 - 1e-15) break;
+    for (int k = 0; k < 10; ++k) m[k] = ldexp(q[k], -e);
+    if (tr >= (1.0 - 1e-15) * (trm * trm)) break;   // M was rank one: tr(M^2) = tr(M)^2
   }
   // column of the largest diagonal entry (static indices only: no scratch)
   double v[4] = {m[0], m[1], m[2], m[3]}, bd = m[0];
@@ -178,42 +182,78 @@ __device__ void sym4_top_eigvec(const double t[10], double out[4]) {
 }
 
 // ------------------------------------------------------------------------------------------ decode ori
+// One 256-thread workgroup per image; the image's logits stay in registers (PER per thread, n <= 256 PER) from one
+// global read. Softmax in float32 as SPEUtils.last_activ; the ten fp64 moments of a = sum_i p_i q_i q_i^T are
+// reduced through LDS (each of 160 threads sums 16 interleaved partials, ten threads sum those: a fixed order).
+template <int PER>
 __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict__ logits, int n,
                                                          const double* __restrict__ qb, float* __restrict__ soft,
                                                          float* __restrict__ quat, int* __restrict__ status) {
-  __shared__ float shf[4];
-  __shared__ double shd[4][10];
-  const int b = blockIdx.x;
+  __shared__ float shf[2][4];
+  __shared__ double shd[10][256];
+  __shared__ double shp[10][16];
+  const int tid = threadIdx.x, b = blockIdx.x;
   const float* x = logits + (size_t)b * n;
-  float m = -INFINITY;
-  for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, x[i]);
-  m = block_max256(m, shf);
+  float v[PER];
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + 256 * j;
+    v[j] = i < n ? x[i] : -INFINITY;
+  }
+  float m = v[0];
+#pragma unroll
+  for (int j = 1; j < PER; ++j) m = fmaxf(m, v[j]);
+  m = block_max256(m, shf[0]);
   float s = 0.0f;
-  for (int i = threadIdx.x; i < n; i += 256) s += expf(x[i] - m);
-  s = block_sum256(s, shf);
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    v[j] = tid + 256 * j < n ? expf(v[j] - m) : 0.0f;
+    s += v[j];
+  }
+  s = block_sum256(s, shf[1]);
   double mom[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) mom[k] = 0.0;
-  for (int i = threadIdx.x; i < n; i += 256) {
-    const float p = expf(x[i] - m) / s;
-    if (soft) soft[(size_t)b * n + i] = p;
-    const double pd = (double)p;
-    const double q0 = qb[4 * i], q1 = qb[4 * i + 1], q2 = qb[4 * i + 2], q3 = qb[4 * i + 3];
-    mom[0] += (q0 * q0) * pd; mom[1] += (q0 * q1) * pd; mom[2] += (q0 * q2) * pd; mom[3] += (q0 * q3) * pd;
-    mom[4] += (q1 * q1) * pd; mom[5] += (q1 * q2) * pd; mom[6] += (q1 * q3) * pd;
-    mom[7] += (q2 * q2) * pd; mom[8] += (q2 * q3) * pd; mom[9] += (q3 * q3) * pd;
+#pragma unroll
+  for (int j = 0; j < PER; ++j) {
+    const int i = tid + 256 * j;
+    if (i < n) {
+      const float p = v[j] / s;
+      if (soft) soft[(size_t)b * n + i] = p;
+      const double pd = (double)p;
+      const double4 q = *reinterpret_cast<const double4*>(qb + 4 * i);
+      mom[0] += (q.x * q.x) * pd; mom[1] += (q.x * q.y) * pd; mom[2] += (q.x * q.z) * pd; mom[3] += (q.x * q.w) * pd;
+      mom[4] += (q.y * q.y) * pd; mom[5] += (q.y * q.z) * pd; mom[6] += (q.y * q.w) * pd;
+      mom[7] += (q.z * q.z) * pd; mom[8] += (q.z * q.w) * pd; mom[9] += (q.w * q.w) * pd;
+    }
   }
 #pragma unroll
-  for (int k = 0; k < 10; ++k) {
-    const double w = warp_sum_d(mom[k]);
-    if ((threadIdx.x & 63) == 0) shd[threadIdx.x >> 6][k] = w;
+  for (int k = 0; k < 10; ++k) shd[k][tid] = mom[k];
+  __syncthreads();
+  if (tid < 160) {
+    const int k = tid >> 4, j = tid & 15;
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a += shd[k][j + 16 * r];
+    shp[k][j] = a;
   }
   __syncthreads();
-  if (threadIdx.x != 0) return;
+  if (tid >= 16) return;
   double t[10];
+  if (tid < 10) {
+    double a = 0.0;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) a += shp[tid][r];
+    shd[tid][0] = a;
+  }
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  if (tid != 0) return;
   bool nan = false;
+#pragma unroll
   for (int k = 0; k < 10; ++k) {
-    t[k] = (shd[0][k] + shd[1][k]) + (shd[2][k] + shd[3][k]);
+    t[k] = shd[k][0];
     nan |= isnan(t[k]);
   }
   if (nan) {  // classification_utils.py:134-135
@@ -304,7 +344,12 @@ hipError_t launch_fc_splitk(const float* x, const float* w, const float* bias, f
 
 hipError_t launch_decode_ori(const float* logits, int B, int n_bins, const double* q_bins, float* soft, float* quat,
                              int* status, hipStream_t s) {
-  decode_ori_kernel<<<B, 256, 0, s>>>(logits, n_bins, q_bins, soft, quat, status);
+  if (n_bins <= 256 * 8)
+    decode_ori_kernel<8><<<B, 256, 0, s>>>(logits, n_bins, q_bins, soft, quat, status);
+  else if (n_bins <= 256 * 32)
+    decode_ori_kernel<32><<<B, 256, 0, s>>>(logits, n_bins, q_bins, soft, quat, status);
+  else
+    return hipErrorInvalidValue;   // more than 8192 orientation bins (20^3 = 8000 is the largest cubic grid)
   return hipGetLastError();
 }
 

@@ -1031,6 +1031,7 @@ int spef_probe(spef_ctx* c, const void* input, int layout, int B, int H, int W, 
 int spef_set_decode_tables(spef_ctx* c, const double* ori_bins, int n_ori_bins, const double* pos_grid,
                            int n_pos_bins) {
   if (!c) return fail(SPEF_ERR_ARG, "null context");
+  if (n_ori_bins > 8192) return fail(SPEF_ERR_ARG, "at most 8192 orientation bins");
   Dev d(c->device);
   if (c->d_ori_bins) hipFree(c->d_ori_bins);
   if (c->d_pos_grid) hipFree(c->d_pos_grid);
