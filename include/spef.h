@@ -106,6 +106,11 @@ int spef_decode(spef_ctx* ctx, int ori_mode, int pos_mode, const float* ori_raw,
  * 3x3 row-major) and the image size the keypoints are normalised by (Camera nu, nv; speed.py:18-32). */
 int spef_set_keypoints(spef_ctx* ctx, const float* kp3d, int n, const double* K, float nu, float nv);
 
+/* Lens distortion of the keypoint camera, OpenCV order (k1, k2, p1, p2[, k3]); n = 0 removes it. The keypoint
+ * decode then undistorts the 2-D points as cv2.solvePnP does before EPnP (undistortPoints, 5 iterations) -- the
+ * reference passes camera.distCoeffs (keypoints_utils.py:136-142; SPEED+ camera, speed_plus.py:18-40). */
+int spef_set_keypoint_distortion(spef_ctx* ctx, const double* dist, int n);
+
 /* SPEUtils.last_activ (sigmoid, spe_utils.py:68) + KeyPoints.decode_batch (keypoints_utils.py:152-174):
  * raw [B x 2(n+1)] (origin + n keypoints) -> optional kp_out (sigmoid values, same shape), quat [B x 4],
  * pos [B x 3] by batched EPnP (cv2.SOLVEPNP_EPNP semantics) + dcm2quat. status bit 8 = EPnP failure. */

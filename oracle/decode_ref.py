@@ -165,21 +165,37 @@ SPEED_K = np.array([[0.0176 / 5.86e-6, 0, 960.0], [0, 0.0176 / 5.86e-6, 600.0], 
 SPEED_NU, SPEED_NV = 1920, 1200          # src/data/datasets/speed.py:18-32
 
 
-def project_keypoints(q, t, kp3d, K=SPEED_K):
-    """KeyPoints.project, keypoints_utils.py:47-92 (no distortion): origin + N keypoints -> 2 x (N+1) px."""
+def project_keypoints(q, t, kp3d, K=SPEED_K, dist=None):
+    """KeyPoints.project, keypoints_utils.py:47-92: origin + N keypoints -> 2 x (N+1) px; with ``dist`` =
+    (k1, k2, p1, p2, k3) the radial + tangential distortion of :74-80 (the SPEED+ camera, speed_plus.py:18-40)."""
     pts = np.concatenate((np.zeros((3, 1)), np.asarray(kp3d, np.float32).T.astype(np.float64)), axis=1)
     pts = np.vstack((pts, np.ones((1, pts.shape[1]))))
     xyz = np.hstack((quat2dcm(q), np.expand_dims(t, 1))) @ pts
     x0, y0 = xyz[0] / xyz[2], xyz[1] / xyz[2]
-    return np.vstack((K[0, 0] * x0 + K[0, 2], K[1, 1] * y0 + K[1, 2]))
+    if dist is not None:
+        d = dist
+        r2 = x0 * x0 + y0 * y0
+        cdist = 1 + d[0] * r2 + d[1] * r2 * r2 + d[4] * r2 * r2 * r2
+        x = x0 * cdist + d[2] * 2 * x0 * y0 + d[3] * (r2 + 2 * x0 * x0)
+        y = y0 * cdist + d[2] * (r2 + 2 * y0 * y0) + d[3] * 2 * x0 * y0
+    else:
+        x, y = x0, y0
+    return np.vstack((K[0, 0] * x + K[0, 2], K[1, 1] * y + K[1, 2]))
 
 
-def create_keypoints2d(q, t, kp3d, K=SPEED_K, nu=SPEED_NU, nv=SPEED_NV):
+def create_keypoints2d(q, t, kp3d, K=SPEED_K, nu=SPEED_NU, nv=SPEED_NV, dist=None):
     """KeyPoints.create_keypoints2d, keypoints_utils.py:94-110 -> 2(N+1) float32, normalised (x,y)."""
-    k2 = project_keypoints(q, t, kp3d, K)
+    k2 = project_keypoints(q, t, kp3d, K, dist)
     k2[0] /= nu
     k2[1] /= nv
     return np.reshape(k2.T, (-1,)).astype(np.float32)
+
+
+def create_bbox_from_keypoints(kp2d, nu=SPEED_NU, nv=SPEED_NV):
+    """KeyPoints.create_bbox_from_keypoints, keypoints_utils.py:176-198 -> [x_min, y_min, x_max, y_max]."""
+    x = kp2d[::2] * nu
+    y = kp2d[1::2] * nv
+    return np.array([np.min(x) / nu, np.min(y) / nv, np.max(x) / nu, np.max(y) / nv])
 
 
 # --------------------------------------------------------------------------- metrics

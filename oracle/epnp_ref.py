@@ -17,8 +17,11 @@ here and no reference test pins its output, so this module restates the publishe
                           det < 0 -> negate R's third row, t = pc0 - R pw0; reprojection error (mean pixel distance)
   pick                    N = argmin of rep_errors[1..3] with ties keeping the lower index
 
-Parity status: UNPINNED against OpenCV itself (absent); pinned by the noise-free known-answer test on the
-reference's own projections (tests/golden/keypoints.npz: 1,800 valid.json poses) -- see tests.
+  undistort_points        solvePnP's cv::undistortPoints (5 fixed-point iterations) + epnp::init_points re-projection
+
+Parity status: UNPINNED against OpenCV itself (absent); pinned by the noise-free known-answer tests on the
+reference's own projections (tests/golden/keypoints.npz: 1,800 valid.json poses, SPEED camera;
+tests/golden/keypoints_speedplus.npz: the same poses through the SPEED+ camera's lens distortion) -- see tests.
 """
 from __future__ import annotations
 
@@ -179,19 +182,52 @@ def epnp(pw, us, k=SPEED_K):
     return best[0], best[1]
 
 
-def pnp(kp2d_norm, kp3d, k=SPEED_K, nu=SPEED_NU, nv=SPEED_NV):
+def undistort_points(us32, k, dist=None, iters=5):
+    """cv::undistortPoints(src, dst, K, D) as solvePnP(SOLVEPNP_EPNP) calls it before EPnP (OpenCV 4.5.5
+    calib3d/src/solvepnp.cpp, undistort.dispatch.cpp cvUndistortPointsInternal; default criteria COUNT = 5):
+    x = (u - cx) / fx (as a product with 1/fx), then x <- (x0 - delta(x)) * icdist(x) five times (k4..k6 and the thin
+    prism / tilt terms are 0 for a 5-coefficient model; icdist < 0 falls back to the distorted point), output
+    rounded to the input's float32; epnp::init_points then re-projects with K (us = x * fu + uc, in double).
+    With ``dist`` None or all zeros only the float32 round trip of the normalised coordinate remains (the reference
+    passes zeros for SPEED, keypoints_utils.py:136)."""
+    fu, fv, uc, vc = k[0, 0], k[1, 1], k[0, 2], k[1, 2]
+    ifx, ify = 1.0 / fu, 1.0 / fv
+    d = np.zeros(5) if dist is None else np.asarray(dist, np.float64).reshape(-1)
+    k1, k2, p1, p2, k3 = d[:5]
+    out = np.zeros((us32.shape[0], 2))
+    for i in range(us32.shape[0]):
+        u, v = float(us32[i, 0]), float(us32[i, 1])
+        x = x0 = (u - uc) * ifx
+        y = y0 = (v - vc) * ify
+        for _ in range(iters):
+            r2 = x * x + y * y
+            icdist = 1.0 / (1 + ((k3 * r2 + k2) * r2 + k1) * r2)
+            if icdist < 0:
+                x, y = (u - uc) * ifx, (v - vc) * ify
+                break
+            dx = 2 * p1 * x * y + p2 * (r2 + 2 * x * x)
+            dy = p1 * (r2 + 2 * y * y) + 2 * p2 * x * y
+            x = (x0 - dx) * icdist
+            y = (y0 - dy) * icdist
+        out[i, 0] = float(np.float32(x)) * fu + uc
+        out[i, 1] = float(np.float32(y)) * fv + vc
+    return out
+
+
+def pnp(kp2d_norm, kp3d, k=SPEED_K, nu=SPEED_NU, nv=SPEED_NV, dist=None):
     """KeyPoints.pnp (keypoints_utils.py:112-150): normalised (x0,y0,x1,y1,...) incl. origin -> (q f32, t f32)."""
     x = kp2d_norm[0::2] * nu
     y = kp2d_norm[1::2] * nv
-    us = np.stack([x, y], axis=1)[1:].astype(np.float64)
+    us32 = np.stack([x, y], axis=1)[1:].astype(np.float32)         # float32 pixels (keypoints_utils.py:127-131)
+    us = undistort_points(us32, k, dist)
     r, t = epnp(np.asarray(kp3d, np.float32).astype(np.float64), us, k)
     return dcm2quat(r).astype(np.float32), np.asarray(t, np.float32)
 
 
-def decode_batch(kp2d_norm, kp3d, k=SPEED_K):
+def decode_batch(kp2d_norm, kp3d, k=SPEED_K, nu=SPEED_NU, nv=SPEED_NV, dist=None):
     """KeyPoints.decode_batch (keypoints_utils.py:152-174)."""
     q = np.zeros((kp2d_norm.shape[0], 4), np.float32)
     t = np.zeros((kp2d_norm.shape[0], 3), np.float32)
     for i in range(kp2d_norm.shape[0]):
-        q[i], t[i] = pnp(kp2d_norm[i], kp3d, k)
+        q[i], t[i] = pnp(kp2d_norm[i], kp3d, k, nu, nv, dist)
     return q, t

@@ -1,5 +1,6 @@
 // Batched keypoint decode: SPEUtils.last_activ sigmoid (src/spe/spe_utils.py:68) + KeyPoints.pnp
-// (src/spe/keypoints_utils.py:112-150) = cv2.solvePnP(SOLVEPNP_EPNP) -> Rodrigues -> dcm2quat (spe/utils.py:56-118).
+// (src/spe/keypoints_utils.py:112-150) = cv2.solvePnP(SOLVEPNP_EPNP) -> Rodrigues -> dcm2quat (spe/utils.py:56-118),
+// including solvePnP's undistortPoints for cameras with lens distortion (SPEED+, data/datasets/speed_plus.py:18-40).
 //
 // One fp64 thread per problem; the algorithm is OpenCV 4.5.5 epnp.cpp's (the reference's pinned OpenCV):
 // PCA control points, barycentric alphas, M (2n x 12), the 4 eigenvectors of M^T M with the smallest
@@ -184,10 +185,40 @@ __device__ double epnp_rt(const EpnpProblem& P, const double (&ut4)[4][12], cons
   return err / P.n;
 }
 
+// cv::undistortPoints as solvePnP(SOLVEPNP_EPNP) applies it before EPnP (OpenCV 4.5.5 solvepnp.cpp;
+// undistort.dispatch.cpp cvUndistortPointsInternal, default criteria COUNT = 5) followed by epnp::init_points'
+// re-projection with K: x = (u - cx) * (1/fx); five fixed-point steps x <- (x0 - delta(x)) * icdist(x) (5-coefficient
+// model: k1 k2 p1 p2 k3); the normalised point is stored as float32 (the reference's points are float32) and
+// re-projected in double, us = x fu + uc. Without distortion only that float32 round trip remains (the reference
+// always passes distCoeffs, zeros for SPEED: keypoints_utils.py:136-142).
+__device__ __forceinline__ void undistort_point(const EpnpDist& d, double fu, double fv, double uc, double vc,
+                                                float uf, float vf, double& u_out, double& v_out) {
+  const double ifx = 1.0 / fu, ify = 1.0 / fv;
+  const double x0 = ((double)uf - uc) * ifx, y0 = ((double)vf - vc) * ify;
+  double x = x0, y = y0;
+  if (d.on) {
+    for (int it = 0; it < 5; ++it) {
+      const double r2 = x * x + y * y;
+      const double icdist = 1.0 / (1.0 + ((d.k3 * r2 + d.k2) * r2 + d.k1) * r2);
+      if (icdist < 0) {
+        x = x0;
+        y = y0;
+        break;
+      }
+      const double dx = 2 * d.p1 * x * y + d.p2 * (r2 + 2 * x * x);
+      const double dy = d.p1 * (r2 + 2 * y * y) + 2 * d.p2 * x * y;
+      x = (x0 - dx) * icdist;
+      y = (y0 - dy) * icdist;
+    }
+  }
+  u_out = (double)(float)x * fu + uc;
+  v_out = (double)(float)y * fv + vc;
+}
+
 __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw, int B, int n,
                                                   const float* __restrict__ kp3d, const double* __restrict__ model,
                                                   double fu, double fv, double uc,
-                                                  double vc, float nu, float nv, int apply_sigmoid,
+                                                  double vc, float nu, float nv, EpnpDist dist, int apply_sigmoid,
                                                   float* __restrict__ kp_out, float* __restrict__ quat,
                                                   float* __restrict__ pos, int* __restrict__ status) {
   const int b = blockIdx.x * 64 + threadIdx.x;
@@ -206,10 +237,8 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
       kp_out[(size_t)b * nk + 2 * i] = x;
       kp_out[(size_t)b * nk + 2 * i + 1] = y;
     }
-    if (i > 0) {   // keypoints_utils.py:127-131: pixels (float32 products), origin dropped
-      P.us[i - 1][0] = (double)(x * nu);
-      P.us[i - 1][1] = (double)(y * nv);
-    }
+    if (i > 0)   // keypoints_utils.py:127-131: pixels (float32 products), origin dropped; then undistortPoints
+      undistort_point(dist, fu, fv, uc, vc, x * nu, y * nv, P.us[i - 1][0], P.us[i - 1][1]);
   }
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < 3; ++j) P.pw[i][j] = (double)kp3d[3 * i + j];
@@ -358,11 +387,11 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
 }
 
 hipError_t launch_epnp(const float* raw, int B, int n, const float* kp3d, const double* model, const double* K,
-                       float nu, float nv, int apply_sigmoid, float* kp_out, float* quat, float* pos, int* status,
-                       hipStream_t s) {
+                       float nu, float nv, const EpnpDist& dist, int apply_sigmoid, float* kp_out, float* quat,
+                       float* pos, int* status, hipStream_t s) {
   if (n < 4 || n > EPNP_MAXN) return hipErrorInvalidValue;
-  epnp_kernel<<<(B + 63) / 64, 64, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, apply_sigmoid,
-                                           kp_out, quat, pos, status);
+  epnp_kernel<<<(B + 63) / 64, 64, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, dist,
+                                           apply_sigmoid, kp_out, quat, pos, status);
   return hipGetLastError();
 }
 

@@ -57,6 +57,7 @@ struct spef_ctx {
   int kp_n = 0;
   double camK[9] = {0};
   float cam_nu = 0.f, cam_nv = 0.f;
+  EpnpDist kp_dist = {0, 0, 0, 0, 0, 0};   // spef_set_keypoint_distortion
   // decode tables
   double* d_ori_bins = nullptr;
   int n_ori_bins = 0;
@@ -1191,6 +1192,23 @@ int spef_set_keypoints(spef_ctx* c, const float* kp3d, int n, const double* K, f
   return SPEF_OK;
 }
 
+int spef_set_keypoint_distortion(spef_ctx* c, const double* dist, int n) {
+  if (!c) return fail(SPEF_ERR_ARG, "null context");
+  if (n != 0 && n != 4 && n != 5) return fail(SPEF_ERR_ARG, "distortion: 0, 4 (k1 k2 p1 p2) or 5 (+ k3) coefficients");
+  if (n && !dist) return fail(SPEF_ERR_ARG, "null distortion coefficients");
+  EpnpDist d = {0, 0, 0, 0, 0, 0};
+  if (n) {
+    d.k1 = dist[0];
+    d.k2 = dist[1];
+    d.p1 = dist[2];
+    d.p2 = dist[3];
+    d.k3 = n == 5 ? dist[4] : 0.0;
+    d.on = (d.k1 != 0 || d.k2 != 0 || d.p1 != 0 || d.p2 != 0 || d.k3 != 0) ? 1 : 0;
+  }
+  c->kp_dist = d;
+  return SPEF_OK;
+}
+
 int spef_decode_keypoints(spef_ctx* c, const float* raw, int B, int apply_sigmoid, float* kp_out, float* quat,
                           float* pos, int* status, void* stream) {
   if (!c || !raw || !quat || !pos || !status || B <= 0) return fail(SPEF_ERR_ARG, "null argument");
@@ -1199,7 +1217,7 @@ int spef_decode_keypoints(spef_ctx* c, const float* raw, int B, int apply_sigmoi
   hipStream_t s = (hipStream_t)stream;
   HIP_TRY(hipMemsetAsync(status, 0, sizeof(int) * B, s));
   HIP_TRY(prof_launch(c, s, "epnp_kernel", (double)B * (2 * (c->kp_n + 1) * 8 + 28), (double)B * 1.0e5, [&] {
-    return launch_epnp(raw, B, c->kp_n, c->kp3d, c->kp_model, c->camK, c->cam_nu, c->cam_nv, apply_sigmoid, kp_out,
+    return launch_epnp(raw, B, c->kp_n, c->kp3d, c->kp_model, c->camK, c->cam_nu, c->cam_nv, c->kp_dist, apply_sigmoid, kp_out,
                        quat, pos, status, s);
   }));
   return SPEF_OK;

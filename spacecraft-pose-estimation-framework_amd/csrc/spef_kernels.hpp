@@ -71,10 +71,15 @@ hipError_t launch_fc_splitk(const float* x, const float* w, const float* bias, f
 
 // Keypoint decode: sigmoid (optional) + EPnP + dcm2quat per problem (k_epnp.hip). raw: B x 2(n+1) (origin +
 // n keypoints, normalised x,y); kp3d: n x 3 fp32 (device); K: host 3x3 row-major. status |= 8 on failure.
+// Brown-Conrady lens distortion of the keypoint camera (OpenCV's 5-coefficient order); on = 0: none.
+struct EpnpDist {
+  double k1, k2, p1, p2, k3;
+  int on;
+};
 // model = control points [4][3] + alphas [n][4] (fp64, device), computed once by spef_set_keypoints.
 hipError_t launch_epnp(const float* raw, int B, int n, const float* kp3d, const double* model, const double* K,
-                       float nu, float nv, int apply_sigmoid, float* kp_out, float* quat, float* pos, int* status,
-                       hipStream_t s);
+                       float nu, float nv, const EpnpDist& dist, int apply_sigmoid, float* kp_out, float* quat,
+                       float* pos, int* status, hipStream_t s);
 
 // Activation dtype -> fp32 NHWC copy (debug probes / backbone feature export).
 hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStream_t s);

@@ -42,6 +42,7 @@ SIGNATURES = {
     'spef_bcast_weights': (_i, [_vp, _vp, _i]),
     'spef_set_option': (_i, [_vp, _i, _i]),
     'spef_set_keypoints': (_i, [_vp, _vp, _i, _vp, C.c_float, C.c_float]),
+    'spef_set_keypoint_distortion': (_i, [_vp, _vp, _i]),
     'spef_decode_keypoints': (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     'spef_profile_begin': (_i, [_vp]),
     'spef_profile_end': (_i, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),

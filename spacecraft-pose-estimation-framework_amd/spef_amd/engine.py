@@ -163,12 +163,17 @@ class Engine:
     def set_option(self, option: int, value: int) -> None:
         L.check(self.lib.spef_set_option(self.ctx, option, int(value)))
 
-    def set_keypoints(self, kp3d: np.ndarray, K: np.ndarray, nu: float, nv: float) -> None:
+    def set_keypoints(self, kp3d: np.ndarray, K: np.ndarray, nu: float, nv: float, dist=None) -> None:
+        """Keypoint-mode camera: 3-D model points, K, image size; ``dist`` = the camera's distCoeffs (k1, k2, p1,
+        p2[, k3]; SPEED+) or None (SPEED: cv2.solvePnP gets zeros, keypoints_utils.py:136)."""
         kp = np.ascontiguousarray(kp3d, np.float32)
         kk = np.ascontiguousarray(K, np.float64).reshape(9)
         L.check(self.lib.spef_set_keypoints(self.ctx, kp.ctypes.data_as(C.c_void_p), kp.shape[0],
                                             kk.ctypes.data_as(C.c_void_p), float(nu), float(nv)))
-        self._kp = (kp, kk)
+        dd = np.zeros(0) if dist is None else np.ascontiguousarray(np.asarray(dist, np.float64).reshape(-1))
+        L.check(self.lib.spef_set_keypoint_distortion(self.ctx, dd.ctypes.data_as(C.c_void_p) if dd.size else None,
+                                                      int(dd.size)))
+        self._kp = (kp, kk, dd)
 
     def decode_keypoints(self, raw: torch.Tensor, apply_sigmoid: bool = True):
         B = raw.shape[0]

@@ -1,7 +1,7 @@
 """Host mirror of the reference ``KeyPoints`` (src/spe/keypoints_utils.py:13-174).
 
-Holds the 3-D keypoints and the camera that the MI355X keypoint decode (sigmoid + batched EPnP,
-csrc/k_epnp.hip) is configured with through ``Engine.set_keypoints``. The solve itself is not here: ``pnp`` /
+Holds the 3-D keypoints and the camera (with its lens distortion, if any) that the MI355X keypoint decode (sigmoid +
+undistortPoints + batched EPnP, csrc/k_epnp.hip) is configured with through ``Engine.set_keypoints``. The solve itself is not here: ``pnp`` /
 ``decode_batch`` run on the GPU via ``SPEMi355x``; this class only loads the model points and builds the
 normalised 2-D keypoint vectors (``create_keypoints2d``) used to make targets and synthetic test inputs.
 """
@@ -22,10 +22,6 @@ class KeyPoints:
             self.keypoints3d = np.asarray(keypoints_dir, np.float32).reshape(-1, 3)
         else:
             self.keypoints3d = self.load_3d_keypoints(keypoints_dir)
-        d = getattr(camera, 'distCoeffs', None)
-        if d is not None and np.any(np.asarray(d, np.float64) != 0):
-            # cv2.solvePnP undistorts the image points first (keypoints_utils.py:139); the GPU EPnP does not
-            raise NotImplementedError('keypoint decode with lens distortion (SPEED+) is not supported')
 
     @staticmethod
     def load_3d_keypoints(mat_path: str, name: str = 'tango3Dpoints') -> np.ndarray:
@@ -33,11 +29,27 @@ class KeyPoints:
         return np.transpose(np.array(loadmat(mat_path)[name], dtype=np.float32))
 
     def project(self, ori: np.ndarray, pos: np.ndarray) -> np.ndarray:
-        """Pin-hole projection (keypoints_utils.py:47-86 without distortion): -> [2 x (N+1)] pixels, origin first."""
+        """Projection (keypoints_utils.py:47-86): -> [2 x (N+1)] pixels, origin first; the camera's distCoeffs
+        (k1, k2, p1, p2, k3), when it has them, add the radial + tangential distortion of :74-80 (SPEED+)."""
         pts = np.concatenate([np.zeros((1, 3)), self.keypoints3d.astype(np.float64)], axis=0)
         xc = pts @ Q.quat2dcm(ori).T + np.asarray(pos, np.float64)
         K = np.asarray(self.camera.K, np.float64)
-        return np.stack([K[0, 0] * xc[:, 0] / xc[:, 2] + K[0, 2], K[1, 1] * xc[:, 1] / xc[:, 2] + K[1, 2]])
+        x, y = xc[:, 0] / xc[:, 2], xc[:, 1] / xc[:, 2]
+        d = getattr(self.camera, 'distCoeffs', None)
+        if d is not None:
+            d = np.asarray(d, np.float64).reshape(-1)
+            r2 = x * x + y * y
+            cdist = 1 + d[0] * r2 + d[1] * r2 * r2 + d[4] * r2 * r2 * r2
+            x, y = (x * cdist + d[2] * 2 * x * y + d[3] * (r2 + 2 * x * x),
+                    y * cdist + d[2] * (r2 + 2 * y * y) + d[3] * 2 * x * y)
+        return np.stack([K[0, 0] * x + K[0, 2], K[1, 1] * y + K[1, 2]])
+
+    def create_bbox_from_keypoints(self, keypoints2d: np.ndarray) -> np.ndarray:
+        """keypoints_utils.py:176-198: [x_min, y_min, x_max, y_max] of normalised (x0, y0, x1, y1, ...)."""
+        x = keypoints2d[::2] * self.camera.nu
+        y = keypoints2d[1::2] * self.camera.nv
+        return np.array([np.min(x) / self.camera.nu, np.min(y) / self.camera.nv, np.max(x) / self.camera.nu,
+                         np.max(y) / self.camera.nv])
 
     def create_keypoints2d(self, ori: np.ndarray, pos: np.ndarray) -> np.ndarray:
         """keypoints_utils.py:88-110: normalised (x0, y0, x1, y1, ...) float32 vector incl. the frame origin."""

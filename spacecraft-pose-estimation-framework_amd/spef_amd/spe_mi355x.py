@@ -65,7 +65,7 @@ class SPEMi355x:
                 raise ValueError('keypoints mode needs SPEUtils.keypoints (a KeyPoints with keypoints3d)')
             cam = kp.camera
             self.engine.set_keypoints(np.asarray(kp.keypoints3d, np.float32), np.asarray(cam.K, np.float64),
-                                      float(cam.nu), float(cam.nv))
+                                      float(cam.nu), float(cam.nv), getattr(cam, 'distCoeffs', None))
             if self.engine.n_out0 != 2 * (kp.keypoints3d.shape[0] + 1):   # model.py:236
                 raise AssertionError(f'keypoint head width {self.engine.n_out0} != 2 * (n_keypoints + 1)')
             return

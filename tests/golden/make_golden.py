@@ -24,8 +24,12 @@ Fixtures (all small):
                    (L2 normalise) + position regression.
   kp_head_240x384_b2.npz  reference ModelWrapper(MobileNetV2, KeypointRegressionHead) raw outputs + the
                    SPEUtils keypoint-mode sigmoid.
+  keypoints_speedplus.npz reference KeyPoints.create_keypoints2d with the SPEED+ camera's lens distortion
+                   (1,800 valid.json poses) + create_bbox_from_keypoints.
+  temporal_pdf.npz reference TemporalPDF.update_pdf sequences (every distance metric, the Inference engine's
+                   orientation and position settings).
 
-Run with ``--only predict,kp_head`` to (re)write only the named groups.
+Run with ``--only predict,kp_head,kp_plus,temporal`` to (re)write only the named groups.
 """
 from __future__ import annotations
 
@@ -140,6 +144,46 @@ def kp_head_fixture(ref_root):
     print('kp head', raw.shape, float(np.abs(raw).max()))
 
 
+def kp_plus_fixture(ref_root):
+    """Reference KeyPoints.project / create_keypoints2d WITH lens distortion: the SPEED+ camera (speed_plus.py:18-40,
+    keypoints_utils.py:74-80) on the 1,800 valid.json poses, plus the bounding boxes (create_bbox_from_keypoints,
+    :176-198) of the first 64."""
+    from src.spe.keypoints_utils import KeyPoints
+    from src.data.datasets.speed_plus import Camera
+    cam = Camera()
+    kp = KeyPoints(cam, os.path.join(ref_root, 'models', '3d_models', 'tangoPoints.mat'))
+    valid = json.load(open(os.path.join(ref_root, 'src/data/datasets/speed_split/valid.json')))
+    q = np.array([v['q_vbs2tango'] for v in valid], np.float32)
+    t = np.array([v['r_Vo2To_vbs_true'] for v in valid], np.float32)
+    k2d = np.stack([kp.create_keypoints2d(q[i], t[i]) for i in range(len(valid))])
+    bbox = np.stack([kp.create_bbox_from_keypoints(k2d[i]) for i in range(64)])
+    np.savez_compressed(os.path.join(HERE, 'keypoints_speedplus.npz'), q=q, t=t, kp2d=k2d, bbox=bbox,
+                        kp3d=kp.keypoints3d, K=cam.K, nu=cam.nu, nv=cam.nv,
+                        dist=np.asarray(cam.distCoeffs, np.float64))
+    print('kp_plus', k2d.shape, float(np.abs(k2d).max()))
+
+
+def temporal_fixture(ref_root):
+    """Reference TemporalPDF.update_pdf (temporal/pdf_compare.py:94-134) over a sequence of random PDFs, for every
+    distance metric (:32-78), with the Inference engine's ori/pos settings (temporal/inference.py:38-39)."""
+    from src.temporal.pdf_compare import TemporalPDF
+    rng = np.random.Generator(np.random.PCG64(77))
+    seq = rng.random((6, 1728)).astype(np.float32) ** 8          # peaked, strictly positive
+    out = {'seq': seq}
+    for metric in ('l2', 'kl', 'js', 'hellinger', 'tv', 'wasserstein'):
+        for n, alpha, tag in ((0.8, 16.49, 'ori'), (0.5, 48.64, 'pos')):
+            f = TemporalPDF(n=n, alpha=alpha, distance_metric=metric)
+            pdfs, dists = [], []
+            for i in range(seq.shape[0]):
+                pdf, d = f.update_pdf(seq[i])
+                pdfs.append(pdf)
+                dists.append(d)
+            out[f'{metric}_{tag}_pdf'] = np.stack(pdfs)
+            out[f'{metric}_{tag}_dist'] = np.asarray(dists, np.float64)
+    np.savez_compressed(os.path.join(HERE, 'temporal_pdf.npz'), **out)
+    print('temporal', len(out))
+
+
 def main(ref_root='/root/reference', only=None):
     _install_stubs()
     sys.dont_write_bytecode = True
@@ -158,7 +202,8 @@ def main(ref_root='/root/reference', only=None):
     seed = 1001
     if only:
         for grp in only:
-            {'predict': predict_fixtures, 'kp_head': kp_head_fixture}[grp](ref_root)
+            {'predict': predict_fixtures, 'kp_head': kp_head_fixture, 'kp_plus': kp_plus_fixture,
+             'temporal': temporal_fixture}[grp](ref_root)
         return
 
     # ---------------------------------------------------------------- forward fixtures

@@ -52,6 +52,47 @@ def test_epnp_matches_oracle_on_noisy_keypoints(kp_engine, golden):
     assert np.median(dt) < 1e-5 and dt.max() < 1e-3               # < 1 mm
 
 
+def _cfg_plus(engine, golden):
+    g = golden('keypoints_speedplus.npz')
+    engine.set_keypoints(g['kp3d'], g['K'], float(g['nu']), float(g['nv']), g['dist'])
+    return g
+
+
+def test_epnp_with_lens_distortion_kat(kp_engine, golden):
+    """SPEED+ camera (lens distortion, speed_plus.py:18-40): the reference's own distorted projections of the 1,800
+    valid.json poses (tests/golden/keypoints_speedplus.npz) -> undistortPoints (5 iterations, as cv2.solvePnP) +
+    EPnP on the GPU recovers every pose, and agrees with the oracle's restatement of the same steps."""
+    eng, _ = kp_engine
+    try:
+        g = _cfg_plus(eng, golden)
+        out = eng.decode_keypoints(torch.from_numpy(g['kp2d']).cuda(), apply_sigmoid=False)
+        q, t = out['ori'].cpu().numpy(), out['pos'].cpu().numpy()
+        assert not out['status'].cpu().numpy().any()
+        assert D.angle_deg_stable(q, g['q']).max() < 5e-4
+        assert np.linalg.norm(t - g['t'], axis=1).max() < 2e-4
+        rq, rt = E.decode_batch(g['kp2d'][:200], g['kp3d'], g['K'], float(g['nu']), float(g['nv']), g['dist'])
+        assert D.angle_deg_stable(q[:200], rq).max() < 1e-5
+        assert np.abs(t[:200] - rt).max() < 1e-5
+    finally:
+        _cfg(eng, golden)
+
+
+def test_epnp_with_lens_distortion_noisy(kp_engine, golden):
+    eng, _ = kp_engine
+    try:
+        g = _cfg_plus(eng, golden)
+        rng = np.random.default_rng(4)
+        kp = (g['kp2d'][:256] + rng.normal(0, 3 / 1920, (256, 24))).astype(np.float32)
+        out = eng.decode_keypoints(torch.from_numpy(kp).cuda(), apply_sigmoid=False)
+        rq, rt = E.decode_batch(kp, g['kp3d'], g['K'], float(g['nu']), float(g['nv']), g['dist'])
+        ang = D.angle_deg_stable(out['ori'].cpu().numpy(), rq)
+        dt = np.linalg.norm(out['pos'].cpu().numpy() - rt, axis=1)
+        assert np.median(ang) < 1e-4 and ang.max() < 0.1
+        assert np.median(dt) < 1e-5 and dt.max() < 1e-3
+    finally:
+        _cfg(eng, golden)
+
+
 def test_sigmoid_then_epnp(kp_engine, golden):
     eng, _ = kp_engine
     g = _cfg(eng, golden)

@@ -114,3 +114,34 @@ def test_host_keypoints_mirror_matches_golden(golden):
         np.testing.assert_allclose(kp.create_keypoints2d(g['q'][i], g['t'][i]), g['kp2d'][i], rtol=1e-6, atol=1e-7)
     su = SPEUtils(SpeedCamera, 'keypoints', pos_mode='keypoints', keypoints_path=kp)
     assert su.keypoints is kp
+
+
+def test_distorted_projection_and_bbox(golden):
+    """SPEED+ camera: the oracle's and the host mirror's projections with lens distortion (keypoints_utils.py:74-80)
+    equal the reference's (keypoints_speedplus.npz), and so do the bounding boxes (:176-198)."""
+    from spef_amd.spe.camera import SpeedPlusCamera
+    from spef_amd.spe.keypoints import KeyPoints
+    g = golden('keypoints_speedplus.npz')
+    np.testing.assert_allclose(SpeedPlusCamera.K, g['K'])
+    np.testing.assert_allclose(SpeedPlusCamera.distCoeffs, g['dist'])
+    kp = KeyPoints(SpeedPlusCamera, g['kp3d'])
+    for i in range(0, 1800, 37):
+        ref = g['kp2d'][i]
+        np.testing.assert_allclose(D.create_keypoints2d(g['q'][i], g['t'][i], g['kp3d'], g['K'], float(g['nu']),
+                                                        float(g['nv']), g['dist']), ref, rtol=1e-6, atol=1e-7)
+        np.testing.assert_allclose(kp.create_keypoints2d(g['q'][i], g['t'][i]), ref, rtol=1e-6, atol=1e-7)
+    for i in range(64):
+        np.testing.assert_allclose(D.create_bbox_from_keypoints(g['kp2d'][i], float(g['nu']), float(g['nv'])),
+                                   g['bbox'][i], rtol=1e-12)
+        np.testing.assert_allclose(kp.create_bbox_from_keypoints(g['kp2d'][i]), g['bbox'][i], rtol=1e-12)
+
+
+def test_epnp_oracle_with_lens_distortion(golden):
+    """solvePnP's undistortPoints (5 iterations) + EPnP restated in the oracle recovers the reference's distorted
+    SPEED+ projections of the valid.json poses (parity with OpenCV itself: unpinned, OpenCV absent)."""
+    from oracle import epnp_ref as E
+    g = golden('keypoints_speedplus.npz')
+    idx = np.arange(0, g['q'].shape[0], 15)
+    q, t = E.decode_batch(g['kp2d'][idx], g['kp3d'], g['K'], float(g['nu']), float(g['nv']), g['dist'])
+    assert D.angle_deg_stable(q, g['q'][idx]).max() < 5e-4
+    assert np.linalg.norm(t - g['t'][idx], axis=1).max() < 2e-4
