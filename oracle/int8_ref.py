@@ -23,6 +23,10 @@ unpinned against Brevitas**. This module fixes the integer semantics the MI355X 
 the GPU is held to BIT-EXACTLY (``int8_forward``), and restates the Brevitas float fake-quant graph
 (``fake_quant_forward``) to measure how far the integer semantics sit from it (rare 1-LSB rounding flips).
 
+Bit widths (``qp['bits']``, the reference's bit_width.json as spef_amd.quant.BitWidths; None = all 8): every
+quantizer below keeps its own width b in 3..8 -- weights L = 2^(b-1) - 1, unsigned ReLU quantizers [0, 2^b - 1],
+signed input / shared quantizers [-2^(b-1), 2^(b-1) - 1] (the 8-bit values are written out below).
+
 Integer semantics (every scale a float64 on the host):
   weights       s_w[c] = max|W[c]| / 127 (>= 2e-16); q_w = clip(rint(W / s_w), -127, 127)
   conv+BN+quant acc = sum q_x q_w (exact int); y / s_out = acc * m[c] + b[c] with
@@ -32,8 +36,8 @@ Integer semantics (every scale a float64 on the host):
   residual      q_sum = q_proj + q_in (both at the block's shared scale s_q), then requantised to the next
                 consumer's scale: clip_s8(fixed(q_sum, s_q / s_next, 0))
   input         u8 frame -> q = clip(rint(f32(f32(u) / 255) / f32(s_img)), -128, 127) (float32 ops)
-  pool          sum over the H*W map, shifted right by tb = ceil(log2(H*W)) (TruncTo8bit floor):
-                pooled u8 at scale s_pool = s_l * 2**tb / (H*W)
+  pool          sum over the H*W map, shifted right by tb = b_last + ceil(log2(H*W)) - b_pool (TruncTo8bit
+                floor; ceil(log2(H*W)) at 8 bits): pooled u8 at scale s_pool = s_l * 2**tb / (H*W)
   FC            q_b[c] = clip(rint(b[c] / (s_pool * s_w[c])), -128, 127); out = f32(acc) * f32(s_pool * s_w[c])
 """
 from __future__ import annotations
@@ -64,11 +68,27 @@ def blocks_topology(residual: bool = True) -> List[Tuple[int, int, int, int, int
     return out
 
 
-def weight_q(w):
-    """IntWeightQuant, 8 bit, per output channel (quantizers.py:16-20): -> (q int64, s float64 [cout])."""
+class _Bits:
+    """Quantizer widths of ``qp['bits']`` (duck-typed spef_amd.quant.BitWidths; None = every width 8)."""
+
+    def __init__(self, bw):
+        self.bw = bw
+
+    def __getattr__(self, k):
+        if self.bw is None:
+            return (8, 8) if k in ('first_conv', 'last_conv', 'fully_connected') else 8
+        return getattr(self.bw, k)
+
+    def block(self, i):
+        return (8, 8, 8, 8, 8) if self.bw is None else tuple(8 if v is None else v for v in self.bw.block(i))
+
+
+def weight_q(w, bits: int = 8):
+    """IntWeightQuant, per output channel, narrow range (quantizers.py:16-20): -> (q int64, s float64 [cout])."""
     w = _np(w).astype(np.float64)
-    s = np.maximum(np.abs(w.reshape(w.shape[0], -1)).max(axis=1) / 127.0, 2e-16)
-    q = np.clip(np.rint(w / s.reshape((-1,) + (1,) * (w.ndim - 1))), -127, 127).astype(np.int64)
+    L = (1 << (bits - 1)) - 1
+    s = np.maximum(np.abs(w.reshape(w.shape[0], -1)).max(axis=1) / L, 2e-16)
+    q = np.clip(np.rint(w / s.reshape((-1,) + (1,) * (w.ndim - 1))), -L, L).astype(np.int64)
     return q, s
 
 
@@ -112,19 +132,20 @@ def requant(acc, M, B, S, lo, hi, axis=1):
     return np.clip(v, lo, hi)
 
 
-def conv_requant_params(sd, prefix, s_in, s_out):
+def conv_requant_params(sd, prefix, s_in, s_out, wbits: int = 8):
     """QConvBnAct weights + fixed-point requant (shared by the stem, expand, dw, project, last conv)."""
-    q, s_w = weight_q(sd[f'{prefix}.0.weight'])
+    q, s_w = weight_q(sd[f'{prefix}.0.weight'], wbits)
     g, h = bn(sd, prefix)
     m = (s_in * s_w * g) / s_out
     b = h / s_out
     return q, fixed(m, b)
 
 
-def input_lut(s_img: float) -> np.ndarray:
-    """uint8 frame value -> quantized input (ToTensor /255 in float32, then round(x / s_img) in float32)."""
+def input_lut(s_img: float, bits: int = 8) -> np.ndarray:
+    """uint8 frame value -> quantized input (ToTensor /255 in float32, then round(x / s_img) in float32), clipped to
+    the signed input quantizer (QuantIdentity(signed=True), mobilenet_v2.py:177-178)."""
     x = np.arange(256, dtype=np.float32) / np.float32(255.0)
-    return np.clip(np.rint(x / np.float32(s_img)), -128, 127).astype(np.int64)
+    return np.clip(np.rint(x / np.float32(s_img)), -(1 << (bits - 1)), (1 << (bits - 1)) - 1).astype(np.int64)
 
 
 def _conv_int(x, q, stride, groups):
@@ -135,20 +156,23 @@ def _conv_int(x, q, stride, groups):
     return np.rint(y.numpy()).astype(np.int64)
 
 
-def pool_shift(hw: int) -> int:
-    """ceil(log2(hw)): the accumulator growth TruncTo8bit removes."""
-    return (hw - 1).bit_length()
+def pool_shift(hw: int, last_bits: int = 8, pool_bits: int = 8) -> int:
+    """The TruncTo8bit shift: the sum of hw b_last-bit codes has b_last + ceil(log2(hw)) bits, truncated to the
+    pooling width (ceil(log2(hw)) when both are 8)."""
+    return max(last_bits + (hw - 1).bit_length() - pool_bits, 0)
 
 
 def head_params(sd, qp: Dict, hw: int):
     """Per-launch FC constants for a feature map of ``hw`` pixels: -> dict of (q_w, q_b, sc) per branch."""
-    tb = pool_shift(hw)
+    bits = _Bits(qp.get('bits'))
+    tb = pool_shift(hw, bits.last_conv[1], bits.pooling)
     s_pool = qp['last'] * 2.0 ** tb / hw
+    wb, bb = bits.fully_connected
     out = {}
     for name, key in (('ori', 'head.ori.1'), ('pos', 'head.pos.0')):
-        q, s_w = weight_q(sd[f'{key}.weight'])
+        q, s_w = weight_q(sd[f'{key}.weight'], wb)
         b = _np(sd[f'{key}.bias']).astype(np.float64)
-        qb = np.clip(np.rint(b / (s_pool * s_w)), -128, 127).astype(np.int64)
+        qb = np.clip(np.rint(b / (s_pool * s_w)), -(1 << (bb - 1)), (1 << (bb - 1)) - 1).astype(np.int64)
         out[name] = (q, qb, (s_pool * s_w).astype(np.float32))
     return tb, out
 
@@ -156,9 +180,11 @@ def head_params(sd, qp: Dict, hw: int):
 def int8_forward(frames_u8: np.ndarray, sd: Dict, qp: Dict, residual: bool = True, upto: int | None = None):
     """uint8 NHWC frames -> (ori logits f32, pos f32), or the integer activation after block ``upto``
     (NCHW int64; 0 = stem output) / ``upto='last'`` (last conv output) / ``upto='pool'``."""
-    x = input_lut(qp['image'])[frames_u8.astype(np.int64)].transpose(0, 3, 1, 2)       # NCHW int
-    q, (M, B, S) = conv_requant_params(sd, f'{FP}.0', qp['image'], qp['stem'])
-    x = requant(_conv_int(x, q, 2, 1), M, B, S, 0, 255)
+    bits = _Bits(qp.get('bits'))
+    slo, shi = -(1 << (bits.shared_act - 1)), (1 << (bits.shared_act - 1)) - 1
+    x = input_lut(qp['image'], bits.image)[frames_u8.astype(np.int64)].transpose(0, 3, 1, 2)       # NCHW int
+    q, (M, B, S) = conv_requant_params(sd, f'{FP}.0', qp['image'], qp['stem'], bits.first_conv[0])
+    x = requant(_conv_int(x, q, 2, 1), M, B, S, 0, (1 << bits.first_conv[1]) - 1)
     if upto == 0:
         return x
     s_x = qp['stem']
@@ -170,27 +196,28 @@ def int8_forward(frames_u8: np.ndarray, sd: Dict, qp: Dict, residual: bool = Tru
         # the block input arrives already at s_q (the previous project requantised to it) or, for block 1,
         # as the stem's unsigned output
         s_in = s_q if s_q is not None else s_x
+        ew, ea, dwb, da, pw = bits.block(n)
         y, j = x, 0
         if t != 1:
-            q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.0', s_in, bq['expand'])
-            y = requant(_conv_int(y, q, 1, 1), M, B, S, 0, 255)
+            q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.0', s_in, bq['expand'], ew)
+            y = requant(_conv_int(y, q, 1, 1), M, B, S, 0, (1 << ea) - 1)
             s_y, j = bq['expand'], 1
         else:
             s_y = s_in
-        q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.{j}', s_y, bq['dw'])
-        y = requant(_conv_int(y, q, stride, q.shape[0]), M, B, S, 0, 255)
+        q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.{j}', s_y, bq['dw'], dwb)
+        y = requant(_conv_int(y, q, stride, q.shape[0]), M, B, S, 0, (1 << da) - 1)
         if res:
-            q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.{j + 1}', bq['dw'], s_q)
-            p = requant(_conv_int(y, q, 1, 1), M, B, S, -128, 127)
+            q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.{j + 1}', bq['dw'], s_q, pw)
+            p = requant(_conv_int(y, q, 1, 1), M, B, S, slo, shi)
             R, RB, RS = fixed(s_q / s_next, 0.0)
-            x = np.clip(((p + x) * R[0] + RB[0]) >> RS[0], -128, 127)
+            x = np.clip(((p + x) * R[0] + RB[0]) >> RS[0], slo, shi)
         else:
-            q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.{j + 1}', bq['dw'], s_next)
-            x = requant(_conv_int(y, q, 1, 1), M, B, S, -128, 127)
+            q, (M, B, S) = conv_requant_params(sd, f'{FP}.{idx}.conv.{j + 1}', bq['dw'], s_next, pw)
+            x = requant(_conv_int(y, q, 1, 1), M, B, S, slo, shi)
         if upto == idx:
             return x
-    q, (M, B, S) = conv_requant_params(sd, f'{FP}.18', qp['final'], qp['last'])
-    x = requant(_conv_int(x, q, 1, 1), M, B, S, 0, 255)
+    q, (M, B, S) = conv_requant_params(sd, f'{FP}.18', qp['final'], qp['last'], bits.last_conv[0])
+    x = requant(_conv_int(x, q, 1, 1), M, B, S, 0, (1 << bits.last_conv[1]) - 1)
     if upto == 'last':
         return x
     hw = x.shape[2] * x.shape[3]
@@ -219,43 +246,52 @@ def fake_quant_forward(frames_u8: np.ndarray, sd: Dict, qp: Dict, residual: bool
     """The same network as Brevitas evaluates it: float32 tensors holding quantized values, dequantized
     weights, float BatchNorm, round-half-even quantizers (for measuring the integer semantics' distance)."""
     f32 = torch.float32
+    bits = _Bits(qp.get('bits'))
+    slo, shi = -(1 << (bits.shared_act - 1)), (1 << (bits.shared_act - 1)) - 1
 
-    def wq(key):
-        q, s = weight_q(sd[key])
+    def wq(key, wb):
+        q, s = weight_q(sd[key], wb)
         return torch.from_numpy((q * s.reshape((-1,) + (1,) * (q.ndim - 1))).astype(np.float32))
 
-    def cbn(x, prefix, stride, groups):
-        w = wq(f'{prefix}.0.weight')
+    def cbn(x, prefix, stride, groups, wb):
+        w = wq(f'{prefix}.0.weight', wb)
         k = w.shape[-1]
         x = F.conv2d(x, w, None, stride, (k - 1) // 2, 1, groups)
         t = lambda n: torch.as_tensor(_np(sd[f'{prefix}.1.{n}']), dtype=f32)
         return F.batch_norm(x, t('running_mean'), t('running_var'), t('weight'), t('bias'), False, 0.1, 1e-5)
 
     x = torch.from_numpy(frames_u8).permute(0, 3, 1, 2).to(f32) / 255.0
-    x = _fq(x, float(np.float32(qp['image'])), -128, 127)
-    x = _fq(F.relu(cbn(x, f'{FP}.0', 2, 1)), float(np.float32(qp['stem'])), 0, 255)
+    ib = bits.image
+    x = _fq(x, float(np.float32(qp['image'])), -(1 << (ib - 1)), (1 << (ib - 1)) - 1)
+    x = _fq(F.relu(cbn(x, f'{FP}.0', 2, 1, bits.first_conv[0])), float(np.float32(qp['stem'])), 0,
+            (1 << bits.first_conv[1]) - 1)
     for n, (idx, cin, cout, stride, t, res) in enumerate(blocks_topology(residual)):
         bq = qp['blocks'][n]
+        ew, ea, dwb, da, pw = bits.block(n)
         if bq['quant'] is not None:
-            x = _fq(x, float(np.float32(bq['quant'])), -128, 127)
+            x = _fq(x, float(np.float32(bq['quant'])), slo, shi)
         y, j = x, 0
         if t != 1:
-            y = _fq(F.relu(cbn(y, f'{FP}.{idx}.conv.0', 1, 1)), float(np.float32(bq['expand'])), 0, 255)
+            y = _fq(F.relu(cbn(y, f'{FP}.{idx}.conv.0', 1, 1, ew)), float(np.float32(bq['expand'])), 0, (1 << ea) - 1)
             j = 1
-        y = _fq(F.relu(cbn(y, f'{FP}.{idx}.conv.{j}', stride, y.shape[1])), float(np.float32(bq['dw'])), 0, 255)
-        y = cbn(y, f'{FP}.{idx}.conv.{j + 1}', 1, 1)
-        x = _fq(y, float(np.float32(bq['quant'])), -128, 127) + x if res else y
-    x = _fq(x, float(np.float32(qp['final'])), -128, 127)
-    x = _fq(F.relu(cbn(x, f'{FP}.18', 1, 1)), float(np.float32(qp['last'])), 0, 255)
+        y = _fq(F.relu(cbn(y, f'{FP}.{idx}.conv.{j}', stride, y.shape[1], dwb)), float(np.float32(bq['dw'])), 0,
+                (1 << da) - 1)
+        y = cbn(y, f'{FP}.{idx}.conv.{j + 1}', 1, 1, pw)
+        x = _fq(y, float(np.float32(bq['quant'])), slo, shi) + x if res else y
+    x = _fq(x, float(np.float32(qp['final'])), slo, shi)
+    x = _fq(F.relu(cbn(x, f'{FP}.18', 1, 1, bits.last_conv[0])), float(np.float32(qp['last'])), 0,
+            (1 << bits.last_conv[1]) - 1)
     hw = x.shape[2] * x.shape[3]
-    tb = pool_shift(hw)
+    tb = pool_shift(hw, bits.last_conv[1], bits.pooling)
     s_l = float(np.float32(qp['last']))
     pooled = torch.floor(torch.round(x / s_l).sum(dim=(2, 3)) / 2 ** tb) * (s_l * 2 ** tb / hw)
     outs = []
+    wb, bb = bits.fully_connected
     for key in ('head.ori.1', 'head.pos.0'):
-        w = wq(f'{key}.weight')
-        q, s_w = weight_q(sd[f'{key}.weight'])
+        w = wq(f'{key}.weight', wb)
+        q, s_w = weight_q(sd[f'{key}.weight'], wb)
         s_b = torch.from_numpy((s_l * 2.0 ** tb / hw * s_w).astype(np.float32))
-        b = torch.clamp(torch.round(torch.as_tensor(_np(sd[f'{key}.bias']), dtype=f32) / s_b), -128, 127) * s_b
+        b = torch.clamp(torch.round(torch.as_tensor(_np(sd[f'{key}.bias']), dtype=f32) / s_b), -(1 << (bb - 1)),
+                        (1 << (bb - 1)) - 1) * s_b
         outs.append(F.linear(pooled, w, b))
     return outs[0], outs[1]

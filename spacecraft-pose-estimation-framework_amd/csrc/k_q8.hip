@@ -23,6 +23,7 @@ struct Rq {   // per-channel requant parameters, struct-of-arrays over Np channe
   const int64_t* M;
   const int64_t* B;
   const int32_t* S;
+  int lo, hi;   // output quantizer range: [0, 2^b - 1] unsigned, [-2^(b-1), 2^(b-1) - 1] signed (bit width b <= 8)
 };
 
 __device__ __forceinline__ int requant(int acc, int64_t M, int64_t B, int S, int lo, int hi) {
@@ -41,7 +42,8 @@ __device__ __forceinline__ int requant(int acc, int64_t M, int64_t B, int S, int
 constexpr int kStemTH = 4, kStemTW = 64, kStemIH = 2 * kStemTH + 1, kStemIW = 2 * kStemTW + 1;
 template <bool F32IN>
 __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict__ in, const int8_t* __restrict__ lut,
-                                                          float s_img, const int8_t* __restrict__ w28, Rq rq,
+                                                          float s_img, int in_lo, int in_hi,
+                                                          const int8_t* __restrict__ w28, Rq rq,
                                                           uint8_t* __restrict__ Y, int H, int W, int OH, int OW,
                                                           int tiles_x, int tiles_y, size_t nbytes) {
   __shared__ int Xs[kStemIH * kStemIW];
@@ -132,7 +134,7 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
         for (int ci = 0; ci < 3; ++ci) {
           int q;
           if (F32IN) {
-            q = (int)fminf(fmaxf(rintf(fv[it * 3 + ci] / s_img), -128.f), 127.f);
+            q = (int)fminf(fmaxf(rintf(fv[it * 3 + ci] / s_img), (float)in_lo), (float)in_hi);
           } else {   // byte (ix - cx0) * 3 + ci of window row r's span, which starts (rs & 3) bytes into Raw
             const int r = i / kStemIW, ix = ix0 + (i - r * kStemIW);
             const int iy = iy0 + r;
@@ -202,9 +204,9 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
         int v;
         if (fast) {
           v = (int)(((int64_t)acc * (int)Mr[e] + Br[e]) >> 32) >> (Sr[e] - 32);
-          v = min(max(v, 0), 255);
+          v = min(max(v, 0), rq.hi);
         } else {
-          v = requant(acc, Mr[e], Br[e], Sr[e], 0, 255);
+          v = requant(acc, Mr[e], Br[e], Sr[e], 0, rq.hi);
         }
         w |= (uint32_t)v << (8 * i);
       }
@@ -257,7 +259,7 @@ __global__ __launch_bounds__(256) void q_dw_kernel(const uint8_t* __restrict__ X
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const int c = c0 + e;
-    const uint32_t q = (uint32_t)(requant(acc[e], rq.M[c], rq.B[c], rq.S[c], 0, 255) ^ 0x80);
+    const uint32_t q = (uint32_t)(requant(acc[e], rq.M[c], rq.B[c], rq.S[c], 0, rq.hi) ^ 0x80);
     if (e < 4) lo |= q << (8 * e);
     else hi |= q << (8 * (e - 4));
   }
@@ -402,13 +404,13 @@ __global__ __launch_bounds__(256) void q_gemm_kernel(const int8_t* __restrict__ 
         const int c = i + e;
         int q;
         if constexpr (EPI == QEPI_RELU) {
-          q = requant(v[e], rq.M[c], rq.B[c], rq.S[c], 0, 255);
+          q = requant(v[e], rq.M[c], rq.B[c], rq.S[c], 0, rq.hi);
         } else if constexpr (EPI == QEPI_PROJ) {
-          q = requant(v[e], rq.M[c], rq.B[c], rq.S[c], -128, 127);
-        } else {   // QEPI_PROJ_RES: residual join, then requantise to the next consumer's scale
-          const int p = requant(v[e], rq.M[c], rq.B[c], rq.S[c], -128, 127) + (int)R[(size_t)m * N + c];
+          q = requant(v[e], rq.M[c], rq.B[c], rq.S[c], rq.lo, rq.hi);
+        } else {   // QEPI_PROJ_RES: residual join, then requantise to the next consumer's scale (same width)
+          const int p = requant(v[e], rq.M[c], rq.B[c], rq.S[c], rq.lo, rq.hi) + (int)R[(size_t)m * N + c];
           const int64_t t = ((int64_t)p * RM + RB) >> RS;
-          q = (int)(t < -128 ? -128 : (t > 127 ? 127 : t));
+          q = (int)(t < rq.lo ? rq.lo : (t > rq.hi ? rq.hi : t));
         }
         packed |= ((uint32_t)q & 0xffu) << (8 * e);
       }
@@ -465,31 +467,33 @@ hipError_t launch_q_to_f32(const void* x, float* y, int64_t n, int is_unsigned, 
   return hipGetLastError();
 }
 
-hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_img, const int8_t* w28,
-                         const int64_t* M, const int64_t* Bq, const int32_t* S, uint8_t* y, int B, int H, int W,
-                         int OH, int OW, hipStream_t s) {
+hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_img, int in_bits, const int8_t* w28,
+                         const int64_t* M, const int64_t* Bq, const int32_t* S, int out_bits, uint8_t* y, int B, int H,
+                         int W, int OH, int OW, hipStream_t s) {
+  if (in_bits < 2 || in_bits > 8 || out_bits < 2 || out_bits > 8) return hipErrorInvalidValue;
+  const int in_lo = -(1 << (in_bits - 1)), in_hi = (1 << (in_bits - 1)) - 1;
   const int tiles_x = (OW + kStemTW - 1) / kStemTW, tiles_y = (OH + kStemTH - 1) / kStemTH;
   const size_t nbytes = (size_t)B * H * W * 3;   // u8 NHWC frame buffer (the f32 form does not use it)
   const int64_t nb = (int64_t)tiles_x * tiles_y * B;
   if (nb > 0x7fffffff) return hipErrorInvalidValue;
   if (nb == 0) return hipSuccess;
-  Rq rq{M, Bq, S};
+  Rq rq{M, Bq, S, 0, (1 << out_bits) - 1};
   if (f32in)
-    q_stem_rows_kernel<true><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y,
-                                                           nbytes);
+    q_stem_rows_kernel<true><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, in_lo, in_hi, w28, rq, y, H, W, OH, OW,
+                                                           tiles_x, tiles_y, nbytes);
   else
-    q_stem_rows_kernel<false><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, w28, rq, y, H, W, OH, OW, tiles_x, tiles_y,
-                                                            nbytes);
+    q_stem_rows_kernel<false><<<(unsigned)nb, 256, 0, s>>>(in, lut, s_img, in_lo, in_hi, w28, rq, y, H, W, OH, OW,
+                                                            tiles_x, tiles_y, nbytes);
   return hipGetLastError();
 }
 
 hipError_t launch_q_dw(const uint8_t* x, const int8_t* w9, const int64_t* M, const int64_t* Bq, const int32_t* S,
-                       int8_t* y, int B, int H, int W, int C, int stride, int OH, int OW, hipStream_t s) {
-  if (C & 7) return hipErrorInvalidValue;
+                       int out_bits, int8_t* y, int B, int H, int W, int C, int stride, int OH, int OW, hipStream_t s) {
+  if ((C & 7) || out_bits < 2 || out_bits > 8) return hipErrorInvalidValue;
   const int64_t n = (int64_t)B * OH * OW * (C >> 3);
   const int64_t nb = (n + 255) / 256;
   if (nb > 0x7fffffff) return hipErrorInvalidValue;
-  q_dw_kernel<<<(unsigned)nb, 256, 0, s>>>(x, w9, Rq{M, Bq, S}, y, B, H, W, C, stride, OH, OW);
+  q_dw_kernel<<<(unsigned)nb, 256, 0, s>>>(x, w9, Rq{M, Bq, S, 0, (1 << out_bits) - 1}, y, B, H, W, C, stride, OH, OW);
   return hipGetLastError();
 }
 
@@ -502,7 +506,10 @@ static hipError_t q_gemm_go(const QGemmArgs& a, hipStream_t s) {
   const int64_t nwg64 = (a.M + BM - 1) / BM * n_chunks;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  const Rq rq{a.rqM, a.rqB, a.rqS};
+  if (a.out_bits < 2 || a.out_bits > 8) return hipErrorInvalidValue;
+  const bool sgn = a.epi == QEPI_PROJ || a.epi == QEPI_PROJ_RES;
+  const Rq rq{a.rqM, a.rqB, a.rqS, sgn ? -(1 << (a.out_bits - 1)) : 0,
+              sgn ? (1 << (a.out_bits - 1)) - 1 : (1 << a.out_bits) - 1};
 #define SPEF_QG(E)                                                                                             \
   q_gemm_kernel<WN, NT, MT, E><<<nwg, 256, 0, s>>>(a.x, a.w, a.init, rq, a.r, a.rm, a.rb, a.rs, a.y, a.y1, a.sc, \
                                                    a.n_split, a.M, a.K, a.N, Kp, Np, n_chunks, nwg)

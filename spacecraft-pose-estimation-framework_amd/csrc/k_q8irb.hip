@@ -56,14 +56,14 @@ struct RQR {
 // has an 11-bit significand): two values pack into one dword with a shift-or, no int -> float conversion. The
 // depthwise sum then carries + 1024 * sum_taps w, which the packer folded into the depthwise requant offset.
 constexpr uint32_t kF16Bias2 = 0x64006400u;   // two fp16 1024.0
-// expand output: u8 n of two channels -> one dword of fp16 (1024 + n)
+// expand output: u8 n (unsigned quantizer of eh + 1 levels, eh = 2^b - 1) of two channels -> one dword of fp16 (1024 + n)
 template <bool SH32>
-__device__ __forceinline__ uint32_t expand_pair(const RQR<SH32>& r0, int a0, const RQR<SH32>& r1, int a1) {
-  if constexpr (SH32) {   // the offset carries + 0x6400: clamp to [0x6400, 0x64ff], two low halves -> one v_perm_b32
-    const int v0 = min(max(r0.hi(a0), 0x6400), 0x64ff), v1 = min(max(r1.hi(a1), 0x6400), 0x64ff);
+__device__ __forceinline__ uint32_t expand_pair(const RQR<SH32>& r0, int a0, const RQR<SH32>& r1, int a1, int eh) {
+  if constexpr (SH32) {   // the offset carries + 0x6400: clamp to [0x6400, 0x6400 + eh], two low halves -> one v_perm_b32
+    const int v0 = min(max(r0.hi(a0), 0x6400), 0x6400 + eh), v1 = min(max(r1.hi(a1), 0x6400), 0x6400 + eh);
     return __builtin_amdgcn_perm((uint32_t)v1, (uint32_t)v0, 0x05040100u);
   } else {
-    const int v0 = min(max(r0.hi(a0), 0), 255), v1 = min(max(r1.hi(a1), 0), 255);
+    const int v0 = min(max(r0.hi(a0), 0), eh), v1 = min(max(r1.hi(a1), 0), eh);
     return ((uint32_t)v1 << 16) | (uint32_t)v0 | kF16Bias2;
   }
 }
@@ -99,7 +99,9 @@ template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, b
 __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
     const int8_t* __restrict__ X, const int8_t* __restrict__ We, const int8_t* __restrict__ Wp,
     const int32_t* __restrict__ pinit, const uint8_t* __restrict__ tabs, int64_t RM, int64_t RB, int RSH,
-    int8_t* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y, uint32_t nwg) {
+    int eh, int dh, int slo, int shi, int8_t* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
+    uint32_t nwg) {
+  // eh, dh: top levels of the expand / depthwise ReLU quantizers (2^b - 1); [slo, shi]: the shared signed quantizer
   using G = QGeom<CIN, HID, COUT, S, TH, TW, RES, NW>;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   // t == 1 without residual (block 1) never reads an int8 input copy: no Xs region, more workgroups per CU
@@ -287,8 +289,8 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
           e0 = mfma_i8(a0[ks], bx, e0);
           e1 = mfma_i8(a1[ks], bx, e1);
         }
-        uint2 u0 = {expand_pair(r0[0], e0[0], r0[1], e0[1]), expand_pair(r0[2], e0[2], r0[3], e0[3])};
-        uint2 u1 = {expand_pair(r1[0], e1[0], r1[1], e1[1]), expand_pair(r1[2], e1[2], r1[3], e1[3])};
+        uint2 u0 = {expand_pair(r0[0], e0[0], r0[1], e0[1], eh), expand_pair(r0[2], e0[2], r0[3], e0[3], eh)};
+        uint2 u1 = {expand_pair(r1[0], e1[0], r1[1], e1[1], eh), expand_pair(r1[2], e1[2], r1[3], e1[3], eh)};
         if (!interior && !((pvmask >> j) & 1u)) {   // pixel outside the image: the depthwise zero padding (n = 0)
           u0 = make_uint2(kF16Bias2, kF16Bias2);
           u1 = u0;
@@ -312,7 +314,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
         if constexpr (SH32) {
           int q[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) q[e] = min(max(rd[e].hi((int)a8[e]), -128), 127);
+          for (int e = 0; e < 8; ++e) q[e] = min(max(rd[e].hi((int)a8[e]), -128), dh - 128);
           const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)q[1], (uint32_t)q[0], 0x0c0c0400u);
           const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)q[3], (uint32_t)q[2], 0x0c0c0400u);
           const uint32_t p45 = __builtin_amdgcn_perm((uint32_t)q[5], (uint32_t)q[4], 0x0c0c0400u);
@@ -324,7 +326,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
           hi = 0;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const uint32_t q = (uint32_t)min(max(rd[e].hi((int)a8[e]), 0), 255);
+            const uint32_t q = (uint32_t)min(max(rd[e].hi((int)a8[e]), 0), dh);
             if (e < 4) lo |= q << (8 * e);
             else hi |= q << (8 * (e - 4));
           }
@@ -400,11 +402,11 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
       uint32_t packed = 0;
 #pragma unroll
       for (int r = 0; r < 4; ++r) {
-        int q = rq_apply(acc[qi][t][r], RqP[o + r], -128, 127);
+        int q = rq_apply(acc[qi][t][r], RqP[o + r], slo, shi);
         if constexpr (RES) {
           q += (int)Xs[((oy + 1) * G::IW + (ox + 1)) * G::XSB + o + r];
           const int64_t v = ((int64_t)q * RM + RB) >> RSH;
-          q = (int)(v < -128 ? -128 : (v > 127 ? 127 : v));
+          q = (int)(v < slo ? slo : (v > shi ? shi : v));
         }
         packed |= ((uint32_t)q & 0xffu) << (8 * r);
       }
@@ -415,7 +417,9 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int NW, bool EXPAND, bool SH32>
 hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const int32_t* pinit, const uint8_t* tabs,
-                    int64_t rm, int64_t rb, int rs, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
+                    int64_t rm, int64_t rb, int rs, QBits qb, int8_t* y, int B, int H, int W, int OH, int OW,
+                    hipStream_t s) {
+  if (qb.eb < 2 || qb.eb > 8 || qb.db < 2 || qb.db > 8 || qb.sb < 2 || qb.sb > 8) return hipErrorInvalidValue;
   using G = QGeom<CIN, HID, COUT, S, TH, TW, RES, NW>;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
@@ -429,7 +433,8 @@ hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  k<<<nwg, NW * 64, lds, s>>>(x, we, wp, pinit, tabs, rm, rb, rs, y, H, W, OH, OW, tiles_x, tiles_y, nwg);
+  k<<<nwg, NW * 64, lds, s>>>(x, we, wp, pinit, tabs, rm, rb, rs, (1 << qb.eb) - 1, (1 << qb.db) - 1,
+                              -(1 << (qb.sb - 1)), (1 << (qb.sb - 1)) - 1, y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   return hipGetLastError();
 }
 
@@ -460,13 +465,13 @@ bool q_irb_supported(int cin, int hid, int cout, int stride, bool res, bool expa
 
 hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, bool sh32, const int8_t* x,
                         const int8_t* we, const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm,
-                        int64_t rb, int rs, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
+                        int64_t rb, int rs, QBits qb, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
 #define SPEF_QIRB_CASE(CI, HI, CO, ST, TH_, TW_, RS, NW_, EX)                                                         \
   if (cin == CI && hid == HI && cout == CO && stride == ST && res == RS && expand == EX)                                \
-    return sh32 ? q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX, true>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, \
-                                                                        OH, OW, s)                                      \
-                : q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX, false>(x, we, wp, pinit, tabs, rm, rb, rs, y, B, H, W, \
-                                                                         OH, OW, s);
+    return sh32 ? q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX, true>(x, we, wp, pinit, tabs, rm, rb, rs, qb, y, B,  \
+                                                                        H, W, OH, OW, s)                                \
+                : q_irb_go<CI, HI, CO, ST, TH_, TW_, RS, NW_, EX, false>(x, we, wp, pinit, tabs, rm, rb, rs, qb, y, B, \
+                                                                         H, W, OH, OW, s);
   SPEF_QIRB_TABLE(SPEF_QIRB_CASE)
 #undef SPEF_QIRB_CASE
   return hipErrorNotSupported;

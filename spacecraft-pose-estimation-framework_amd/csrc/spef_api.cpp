@@ -76,6 +76,7 @@ struct spef_ctx {
   float* q8_fc_sc = nullptr;       // [Np] f32(s_pool * s_w)
   int q8_fc_hw = 0, q8_fc_tb = 0;
   float q8_s_img = 0.f;                        // input scale (f32 NCHW path)
+  int q8_last_bits = 8, q8_pool_bits = 8, q8_fc_bias_bits = 8;   // bit_width.json: last_conv act, pooling, FC bias
   // preprocessing (Pillow BILINEAR resize): coefficient tables for the last (Hin, Win, H, W), temp image
   int pre_key[4] = {0, 0, 0, 0};
   int* pre_bh = nullptr;   // [W][2] (xmin, count), then [W][ksize_h] coefficients
@@ -166,6 +167,18 @@ const char* pw_key(int dt, int epi, int N) {
 template <typename T>
 inline const T* ptr(const spef_ctx* c, uint64_t off) {
   return off == kAbsent ? nullptr : reinterpret_cast<const T*>(c->d_data + off);
+}
+
+// quantizer bit width of an int8 op (spef_blob.hpp qbits; 0 = 8)
+static inline int qbits(const OpDesc& op, int i) { return op.qbits[i] ? op.qbits[i] : 8; }
+
+// QuantAvgPool2d + TruncTo8bit (ursonet.py:61-62, 88): the HW-pixel sum of last_conv's b_last-bit codes has
+// b_last + ceil(log2 HW) bits; truncation to the pooling width drops the rest (oracle/int8_ref.py pool_shift).
+static inline int q8_pool_shift(const spef_ctx* c, int hw) {
+  int tb = 0;
+  while ((1 << tb) < hw) ++tb;
+  const int sh = c->q8_last_bits + tb - c->q8_pool_bits;
+  return sh > 0 ? sh : 0;
 }
 
 size_t elem_size(const spef_ctx* c) { return c->hdr.dtype == DT_I8 ? 1 : 2; }  // int8 | fp16 / bf16 activations
@@ -403,8 +416,9 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
       const double px = (double)B * OH * OW;
       HIP_TRY(prof_launch(c, s, layout == IN_U8_NHWC ? "q_stem_kernel<u8>" : "q_stem_kernel<f32>",
                           (double)B * h * w * 3 * (layout == IN_U8_NHWC ? 1 : 4) + px * 32, px * 2 * 27 * 32, [&] {
-        return launch_q_stem(input, layout == IN_F32_NCHW, ptr<int8_t>(c, op.w1), s_img, ptr<int8_t>(c, op.w0),
-                             rqM(op.b0), rqB(op.b0, 32), rqS(op.b0, 32), y, B, h, w, OH, OW, s);
+        return launch_q_stem(input, layout == IN_F32_NCHW, ptr<int8_t>(c, op.w1), s_img, qbits(op, 1),
+                             ptr<int8_t>(c, op.w0), rqM(op.b0), rqB(op.b0, 32), rqS(op.b0, 32), qbits(op, 0), y, B, h,
+                             w, OH, OW, s);
       }));
       cur = y;
       h = OH;
@@ -428,7 +442,8 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
           return launch_q_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, op.expand != 1,
                               (op.flags & 4u) != 0, (const int8_t*)x,
                               ptr<int8_t>(c, op.w0), ptr<int8_t>(c, op.w2), ptr<int32_t>(c, op.x0),
-                              ptr<uint8_t>(c, op.x2), r3[0], r3[1], (int)r3[2], (int8_t*)y, B, h, w, OH, OW, s);
+                              ptr<uint8_t>(c, op.x2), r3[0], r3[1], (int)r3[2],
+                              QBits{qbits(op, 0), qbits(op, 1), qbits(op, 2)}, (int8_t*)y, B, h, w, OH, OW, s);
         }));
         cur = y;
         h = OH;
@@ -449,6 +464,7 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
         a.rqM = rqM(op.b0);
         a.rqB = rqB(op.b0, op.hidden);
         a.rqS = rqS(op.b0, op.hidden);
+        a.out_bits = qbits(op, 0);
         a.y = h1;
         a.M = M;
         a.K = (int)op.cin;
@@ -460,7 +476,8 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
       HIP_TRY(prof_launch(c, s, "q_dw_kernel", (double)(M + M2) * op.hidden + 9.0 * op.hidden,
                           18.0 * M2 * op.hidden, [&] {
         return launch_q_dw((const uint8_t*)h1, ptr<int8_t>(c, op.w1), rqM(op.b1), rqB(op.b1, op.hidden),
-                           rqS(op.b1, op.hidden), (int8_t*)h2, B, h, w, (int)op.hidden, (int)op.stride, OH, OW, s);
+                           rqS(op.b1, op.hidden), qbits(op, 1), (int8_t*)h2, B, h, w, (int)op.hidden, (int)op.stride,
+                           OH, OW, s);
       }));
       void* y = res ? pick({x, h2}) : pick({h2});
       QGemmArgs a{};
@@ -471,6 +488,7 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
       a.rqM = rqM(op.b2);
       a.rqB = rqB(op.b2, op.cout);
       a.rqS = rqS(op.b2, op.cout);
+      a.out_bits = qbits(op, 2);
       if (res) {
         const std::array<int64_t, 3>& r3 = c->q8_res[&op - c->ops.data()];
         a.r = (const int8_t*)x;
@@ -500,6 +518,7 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
       a.rqM = rqM(op.b0);
       a.rqB = rqB(op.b0, op.cout);
       a.rqS = rqS(op.b0, op.cout);
+      a.out_bits = qbits(op, 0);
       a.y = y;
       a.M = M;
       a.K = (int)op.cin;
@@ -510,8 +529,7 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
       ch = (int)op.cout;
       uns = 1;
       if (mode == 0) {
-        int tb = 0;
-        while ((1 << tb) < h * w) ++tb;
+        const int tb = q8_pool_shift(c, h * w);
         HIP_TRY(prof_launch(c, s, "q_pool_kernel", (double)M * op.cout + (double)B * op.cout, (double)M * op.cout, [&] {
           return launch_q_pool((const uint8_t*)cur, (int8_t*)c->pooled, B, h * w, (int)op.cout, tb, s);
         }));
@@ -532,16 +550,16 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
 // FC constants for a pooled map of `hw` pixels (oracle/int8_ref.py head_params, same float64 expression order).
 int q8_prepare_fc(spef_ctx* c, int hw) {
   if (c->q8_fc_hw == hw && c->q8_fc_init) return SPEF_OK;
-  int tb = 0;
-  while ((1 << tb) < hw) ++tb;
+  const int tb = q8_pool_shift(c, hw);
   const double s_pool = c->q8_sl * ldexp(1.0, tb) / hw;
+  const double blo = -ldexp(1.0, c->q8_fc_bias_bits - 1), bhi = ldexp(1.0, c->q8_fc_bias_bits - 1) - 1;
   const size_t np_ = c->q8_sw.size();
   std::vector<int32_t> init(np_, 0);
   std::vector<float> sc(np_, 0.f);
   for (size_t i = 0; i < np_; ++i) {
     if (c->q8_sw[i] == 0.0) continue;   // padding rows
     double qb = nearbyint(c->q8_bias[i] / (s_pool * c->q8_sw[i]));
-    qb = qb < -128 ? -128 : (qb > 127 ? 127 : qb);
+    qb = qb < blo ? blo : (qb > bhi ? bhi : qb);
     init[i] = c->q8_wsum[i] + (int32_t)qb;
     sc[i] = (float)(s_pool * c->q8_sw[i]);
   }
@@ -683,6 +701,9 @@ static int parse_blob(const uint8_t* head_bytes, size_t meta_bytes, size_t bytes
     const bool qop = op.kind >= OP_QSTEM && op.kind <= OP_QFC;
     if (qop != (h.dtype == DT_I8)) return fail(SPEF_ERR_BLOB, "op kind does not match the blob dtype");
     if (op.kind == OP_QSTEM && op.cout != 32) return fail(SPEF_ERR_BLOB, "int8 stem needs 32 outputs");
+    for (int k = 0; k < 4; ++k)
+      if (op.qbits[k] == 1 || op.qbits[k] > 8 || (op.qbits[k] && !qop))
+        return fail(SPEF_ERR_BLOB, "quantizer bit widths must be 2..8 (int8 ops only)");
     if (op.kind == OP_FC || op.kind == OP_QFC) {
       ++n_head;
       if (h.head != HEAD_URSONET || op.cin != h.feat_c || op.cout != h.n_out0 + h.n_out1)
@@ -731,6 +752,7 @@ static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_devi
   std::vector<int32_t> q8_wsum;
   double q8_sl = 0.0;
   float q8_s_img = 0.f;
+  int q8_last_bits = 8, q8_pool_bits = 8, q8_fc_bias_bits = 8;
   auto stage = [&]() -> int {
     HIP_TRY(hipMalloc(&dd, std::max<uint64_t>(h.data_bytes, 256)));
     const uint8_t* src = (const uint8_t*)blob + h.data_off;
@@ -740,6 +762,11 @@ static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_devi
       for (size_t i = 0; i < ops.size(); ++i) {
         const OpDesc& op = ops[i];
         if (op.kind == OP_QSTEM) HIP_TRY(hipMemcpy(&q8_s_img, dd + op.x0, sizeof(float), hipMemcpyDeviceToHost));
+        if (op.kind == OP_QLAST) {
+          q8_last_bits = qbits(op, 0);
+          q8_pool_bits = qbits(op, 1);
+        }
+        if (op.kind == OP_QFC) q8_fc_bias_bits = qbits(op, 0);
         if (op.kind == OP_QIRB && (op.flags & 1u))
           HIP_TRY(hipMemcpy(q8_res[i].data(), dd + op.x1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost));
         if (op.kind == OP_QFC) {
@@ -774,6 +801,9 @@ static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_devi
   c->q8_wsum = std::move(q8_wsum);
   c->q8_sl = q8_sl;
   c->q8_s_img = q8_s_img;
+  c->q8_last_bits = q8_last_bits;
+  c->q8_pool_bits = q8_pool_bits;
+  c->q8_fc_bias_bits = q8_fc_bias_bits;
   c->q8_fc_hw = 0;
   c->loaded = true;
   return SPEF_OK;

@@ -24,6 +24,11 @@
 //   OP_QLAST w0 int8 [Np][Kp64], b0 RQ
 //   OP_QFC   w0 int8 [Np][1280] (ori rows then pos), b0 fp64 [Np] weight scales, w1 fp64 [Np] float bias,
 //            x0 int32 [Np] 128 * sum_k q_w, x1 fp64 [1] last-conv activation scale
+// qbits (bit_width.json of the reference's QMobileNetV2 / QURSONetHead, model.py:16-45; 0 means 8; 2..8 allowed):
+//   OP_QSTEM [0] first_conv activation (unsigned), [1] image (signed, f32 NCHW input path; the u8 LUT has it built in)
+//   OP_QIRB  [0] expand activation, [1] depthwise activation (unsigned), [2] shared_act (signed output quantizer)
+//   OP_QLAST [0] last_conv activation (unsigned), [1] pooling (TruncTo8bit output: shift = [0] + ceil(log2 HW) - [1])
+//   OP_QFC   [0] fully_connected bias width (signed)
 // act = the activation storage type (fp16 or bf16); Kp = K rounded up to 32, Np = N rounded up to 16, padding 0.
 // BatchNorm (eps 1e-5) is folded: w' = w*g/sqrt(v+eps), b' = beta - mean*g/sqrt(v+eps).
 #pragma once
@@ -53,7 +58,8 @@ struct OpDesc {
   uint32_t kind, cin, cout, hidden, stride, expand, flags, pad0;
   uint64_t w0, b0, w1, b1, w2, b2;
   uint64_t x0, x1, x2;   // extra tensors (int8 ops; kAbsent otherwise)
-  uint8_t reserved[24];
+  uint8_t qbits[4];      // int8 ops: quantizer bit widths (0 = 8), see below
+  uint8_t reserved[20];
 };
 #pragma pack(pop)
 static_assert(sizeof(BlobHeader) == 128, "BlobHeader must be 128 bytes");

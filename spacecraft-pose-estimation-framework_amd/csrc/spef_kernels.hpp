@@ -97,12 +97,12 @@ enum QEpi : int { QEPI_RELU = 0, QEPI_PROJ = 1, QEPI_PROJ_RES = 2, QEPI_FC = 3 }
 
 // Input quant + stem (u8 NHWC via `lut`, or f32 NCHW via round(x / s_img)) -> u8 NHWC [B][OH][OW][32].
 // w28: int8 [32][28] (k = ky*9+kx*3+ci, k 27 zero); M/B/S: requant [32].
-hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_img, const int8_t* w28,
-                         const int64_t* M, const int64_t* Bq, const int32_t* S, uint8_t* y, int B, int H, int W,
-                         int OH, int OW, hipStream_t s);
+hipError_t launch_q_stem(const void* in, int f32in, const int8_t* lut, float s_img, int in_bits, const int8_t* w28,
+                         const int64_t* M, const int64_t* Bq, const int32_t* S, int out_bits, uint8_t* y, int B, int H,
+                         int W, int OH, int OW, hipStream_t s);
 // Depthwise 3x3: u8 in, int8 [9][C] weights -> ReLU-quant, stored offset (u - 128) int8.
 hipError_t launch_q_dw(const uint8_t* x, const int8_t* w9, const int64_t* M, const int64_t* Bq, const int32_t* S,
-                       int8_t* y, int B, int H, int W, int C, int stride, int OH, int OW, hipStream_t s);
+                       int out_bits, int8_t* y, int B, int H, int W, int C, int stride, int OH, int OW, hipStream_t s);
 struct QGemmArgs {
   int epi;
   const int8_t* x;          // [M][K] int8 rows
@@ -120,15 +120,21 @@ struct QGemmArgs {
   int n_split;
   int64_t M;
   int K, N;
+  int out_bits = 8;         // output quantizer bit width (RELU unsigned, PROJ / PROJ_RES signed; bit_width.json)
 };
 hipError_t launch_q_gemm(const QGemmArgs& a, hipStream_t s);
 // TruncTo8bit average pool over the whole map: u8 [B][HW][C] -> offset int8 [B][C] = ((sum) >> tb) - 128.
 hipError_t launch_q_pool(const uint8_t* x, int8_t* p, int B, int HW, int C, int tb, hipStream_t s);
 // Fused int8 inverted-residual block (expand blocks 2-17; k_q8irb.hip). tabs = blob OP_QIRB x2.
 bool q_irb_supported(int cin, int hid, int cout, int stride, bool res, bool expand);
+// Quantizer bit widths (bit_width.json, 2..8): eb / db expand / depthwise ReLU quantizers (unsigned), sb the
+// shared signed quantizer the block's output is requantised to.
+struct QBits {
+  int eb, db, sb;
+};
 hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, bool sh32, const int8_t* x, const int8_t* we,
                         const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm, int64_t rb, int rs,
-                        int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s);
+                        QBits qb, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 // int8 (is_unsigned 0) or u8 codes -> fp32 code * scale.
 hipError_t launch_q_to_f32(const void* x, float* y, int64_t n, int is_unsigned, float scale, hipStream_t s);
 

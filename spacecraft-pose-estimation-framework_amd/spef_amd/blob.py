@@ -170,7 +170,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
 
 def assemble(dtype_code: int, head: int, n0: int, n1: int, fh: int, fw: int, ops, data: _Data) -> bytes:
     """Header + op table + data section. An op is (kind, cin, cout, hidden, stride, expand, flags,
-    w0, b0, w1, b1, w2, b2[, x0, x1, x2])."""
+    w0, b0, w1, b1, w2, b2[, x0, x1, x2[, qbits]]) with qbits up to 4 quantizer widths (int8 ops)."""
     ops_off = _HDR.size
     data_off = ops_off + _OP.size * len(ops)
     data_off += (-data_off) % 256
@@ -178,8 +178,9 @@ def assemble(dtype_code: int, head: int, n0: int, n1: int, fh: int, fw: int, ops
                     ops_off, data_off, data.size, b'\0' * 56)
     out = bytearray(hdr)
     for o in ops:
-        x = tuple(o[13:16]) + (ABSENT,) * (16 - max(13, len(o)))
-        out += _OP.pack(*o[:7], 0, *o[7:13], *x, b'\0' * 24)
+        x = tuple(o[13:16]) + (ABSENT,) * (16 - max(13, min(len(o), 16)))
+        qb = bytes(o[16]) if len(o) > 16 else b''
+        out += _OP.pack(*o[:7], 0, *o[7:13], *x, qb + b'\0' * (24 - len(qb)))
     out += b'\0' * (data_off - len(out))
     for ch in data.chunks:
         out += ch

@@ -5,7 +5,9 @@ conv -> BatchNorm -> QuantReLU / shared-quantizer chain of brevitas_layers.py:10
 MI355X kernels execute (csrc/k_q8.hip); the formulas are written out in oracle/int8_ref.py's header and the
 op layout in csrc/spef_blob.hpp. Everything is computed in float64 on the host, once:
 
-  * weights: s_w[c] = max|W[c]| / 127, q_w = clip(rint(W / s_w), -127, 127)
+  * weights: s_w[c] = max|W[c]| / L, q_w = clip(rint(W / s_w), -L, L), L = 2^(b-1) - 1 (127 at 8 bits)
+  * bit widths (qp['bits'], bit_width.json as quant.BitWidths): weights quantised here; the activation
+    quantizers' widths go into each op's qbits (spef_blob.hpp) and set the kernels' clamp ranges
   * conv + BN + quant: m = (s_in * s_w * g) / s_out, b = h / s_out  (g = gamma/sqrt(var+eps), h = beta - mean*g),
     as fixed point (M, B, sh): q = (acc * M + B) >> sh
   * unsigned MFMA operands are stored offset by -128; the accumulator starts at 128 * sum_k q_w
@@ -19,15 +21,16 @@ import numpy as np
 
 from .arch import Arch, LAST_CHANNELS, arch_from_state_dict
 from .blob import ABSENT, DT_I8, HEAD_URSONET, OP_QFC, OP_QIRB, OP_QLAST, OP_QSTEM, _Data, _np, assemble
-from .quant import validate
+from .quant import BitWidths, validate
 
 BN_EPS = 1e-5
 
 
-def weight_q(w):
+def weight_q(w, bits: int = 8):
     w = _np(w).astype(np.float64)
-    s = np.maximum(np.abs(w.reshape(w.shape[0], -1)).max(axis=1) / 127.0, 2e-16)
-    q = np.clip(np.rint(w / s.reshape((-1,) + (1,) * (w.ndim - 1))), -127, 127).astype(np.int64)
+    L = (1 << (bits - 1)) - 1
+    s = np.maximum(np.abs(w.reshape(w.shape[0], -1)).max(axis=1) / L, 2e-16)
+    q = np.clip(np.rint(w / s.reshape((-1,) + (1,) * (w.ndim - 1))), -L, L).astype(np.int64)
     return q, s
 
 
@@ -73,8 +76,8 @@ def _rq(data: _Data, M, B, S) -> int:
     return data.add(m.tobytes() + bb.tobytes() + ss.tobytes())
 
 
-def _conv(sd, prefix, s_in, s_out):
-    q, s_w = weight_q(sd[f'{prefix}.0.weight'])
+def _conv(sd, prefix, s_in, s_out, wbits: int = 8):
+    q, s_w = weight_q(sd[f'{prefix}.0.weight'], wbits)
     g, h = _bn(sd, prefix)
     return q, fixed((s_in * s_w * g) / s_out, h / s_out)
 
@@ -125,18 +128,21 @@ def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None, shift32: bool = T
     if arch.head != 'ursonet':
         raise NotImplementedError('the int8 path mirrors QURSONetHead (ursonet.py:36-93) only')
     validate(qp)
+    bw = qp.get('bits') or BitWidths()
     fp = 'features.features'
     data = _Data()
     ops = []
 
     # stem + input quant
-    q, (M, B, S) = _conv(sd, f'{fp}.0', qp['image'], qp['stem'])
+    q, (M, B, S) = _conv(sd, f'{fp}.0', qp['image'], qp['stem'], bw.first_conv[0])
     w28 = np.zeros((32, 28), np.int8)
     w28[:, :27] = q.transpose(0, 2, 3, 1).reshape(32, 27)        # k = ky*9 + kx*3 + ci
     x = np.arange(256, dtype=np.float32) / np.float32(255.0)
-    lut = np.clip(np.rint(x / np.float32(qp['image'])), -128, 127).astype(np.int8)
+    ib = bw.image
+    lut = np.clip(np.rint(x / np.float32(qp['image'])), -(1 << (ib - 1)), (1 << (ib - 1)) - 1).astype(np.int8)
     ops.append((OP_QSTEM, 3, 32, 0, 2, 1, 0, data.add(w28.tobytes()), _rq(data, M, B, S), data.add(lut.tobytes()),
-                ABSENT, ABSENT, ABSENT, data.add(np.float32(qp['image']).tobytes()), ABSENT))
+                ABSENT, ABSENT, ABSENT, data.add(np.float32(qp['image']).tobytes()), ABSENT, ABSENT,
+                (bw.first_conv[1], ib)))
 
     s_x = qp['stem']
     nb = len(arch.blocks)
@@ -145,21 +151,22 @@ def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None, shift32: bool = T
         s_q = bq['quant']
         s_next = qp['blocks'][n + 1]['quant'] if n + 1 < nb else qp['final']
         s_in = s_q if s_q is not None else s_x
+        ew, ea, dwb, da, pw = bw.block(n)
         j = 0
         e_w = e_b = ABSENT
         e_rq = None
         if blk.expand != 1:
-            q, e_rq = _conv(sd, f'{fp}.{blk.index}.conv.0', s_in, bq['expand'])
+            q, e_rq = _conv(sd, f'{fp}.{blk.index}.conv.0', s_in, bq['expand'], ew)
             e_w, _ = _pw(data, q)
             e_b = _rq(data, *e_rq)
             s_y, j = bq['expand'], 1
         else:
             s_y = s_in
-        qdw, d_rq = _conv(sd, f'{fp}.{blk.index}.conv.{j}', s_y, bq['dw'])
+        qdw, d_rq = _conv(sd, f'{fp}.{blk.index}.conv.{j}', s_y, bq['dw'], dwb)
         w9 = np.ascontiguousarray(qdw[:, 0].reshape(qdw.shape[0], 9).T.astype(np.int8))   # [9][C], tap = ky*3+kx
         d_w, d_b = data.add(w9.tobytes()), _rq(data, *d_rq)
         p_out = s_q if blk.residual else s_next
-        q, p_rq = _conv(sd, f'{fp}.{blk.index}.conv.{j + 1}', bq['dw'], p_out)
+        q, p_rq = _conv(sd, f'{fp}.{blk.index}.conv.{j + 1}', bq['dw'], p_out, pw)
         p_w, init = _pw(data, q)
         p_b = _rq(data, *p_rq)
         x2 = ABSENT
@@ -177,16 +184,17 @@ def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None, shift32: bool = T
         if shift32 and fusable and all(np.all(r[2] == 32) for r in (e_rq, d_rq, p_rq)):
             flags |= 4       # every fused requant shift is exactly 32: the kernel's shift-free variant
         ops.append((OP_QIRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, flags,
-                    e_w, e_b, d_w, d_b, p_w, p_b, data.add(init.tobytes()), x1, x2))
+                    e_w, e_b, d_w, d_b, p_w, p_b, data.add(init.tobytes()), x1, x2,
+                    (ea if ea is not None else 8, da, bw.shared_act)))
 
-    q, (M, B, S) = _conv(sd, arch.last.prefix, qp['final'], qp['last'])
+    q, (M, B, S) = _conv(sd, arch.last.prefix, qp['final'], qp['last'], bw.last_conv[0])
     l_w, _ = _pw(data, q)
     ops.append((OP_QLAST, arch.last.cin, arch.last.cout, 0, 1, 1, 0, l_w, _rq(data, M, B, S),
-                ABSENT, ABSENT, ABSENT, ABSENT))
+                ABSENT, ABSENT, ABSENT, ABSENT, ABSENT, ABSENT, ABSENT, (bw.last_conv[1], bw.pooling)))
 
     rows, sws, bs = [], [], []
     for key in ('head.ori.1', 'head.pos.0'):
-        q, s_w = weight_q(sd[f'{key}.weight'])
+        q, s_w = weight_q(sd[f'{key}.weight'], bw.fully_connected[0])
         rows.append(q)
         sws.append(s_w)
         bs.append(_np(sd[f'{key}.bias']).astype(np.float64))
@@ -203,5 +211,5 @@ def pack_int8(sd: Dict, qp: Dict, arch: Optional[Arch] = None, shift32: bool = T
     wsum[:n] = 128 * q.sum(axis=1)
     ops.append((OP_QFC, LAST_CHANNELS, n, 0, 1, 1, 0, data.add(w.tobytes()), data.add(sw.tobytes()),
                 data.add(bias.tobytes()), ABSENT, ABSENT, ABSENT, data.add(wsum.tobytes()),
-                data.add(np.float64(qp['last']).tobytes())))
+                data.add(np.float64(qp['last']).tobytes()), ABSENT, (bw.fully_connected[1],)))
     return assemble(DT_I8, HEAD_URSONET, rows[0].shape[0], rows[1].shape[0], 0, 0, ops, data)

@@ -16,14 +16,22 @@ recomputed at pack time. ``QParams`` holds the activation scales in the referenc
 There is no QAT checkpoint in this environment (the reference's trained models are remote downloads), so
 ``calibrate`` sets the scales from activation statistics of the float model on calibration frames --
 Brevitas' own initialisation of ``ParameterFromRuntimeStats`` scales (a high percentile of |x|) -- which
-stands in for QAT. All bit widths are 8 (``config/train/exp_1/bit_width.json``); ``check_bit_width``
-rejects other widths.
+stands in for QAT.
+
+Bit widths (``BitWidths``, parsed from the reference's ``bit_width.json``, model.py:16-45): every quantizer
+keeps its own width from 3 to 8 bits, held in int8 containers -- weights per output channel in
+[-(2^(b-1) - 1), 2^(b-1) - 1] (narrow range), unsigned ReLU quantizers in [0, 2^b - 1], the signed shared /
+input quantizers in [-2^(b-1), 2^(b-1) - 1]. The reference's ``QMobileNetV2`` default is 3-bit weights and
+activations with a 4-bit shared quantizer (mobilenet_v2.py:140-167, ``BitWidths.qmobilenet_default()``);
+``config/train/exp_1/bit_width.json`` is all 8 (``BitWidths()``). Widths 1 and 2 select Brevitas' binary /
+ternary quantizers (quantizers.py:78-96), a different arithmetic, and are rejected.
 """
 from __future__ import annotations
 
 import ast
 import json
-from typing import Dict, List, Optional
+from dataclasses import dataclass
+from typing import Dict, List, Optional, Tuple
 
 import numpy as np
 import torch
@@ -34,22 +42,85 @@ from .arch import IR_SETTINGS, mobilenet_v2
 FP = 'features.features'
 
 
-def check_bit_width(path_or_dict) -> None:
-    """Accept a reference ``bit_width.json`` (model.py:16-45 format) only if every width is 8."""
+N_BLOCKS = 17
+
+
+@dataclass(frozen=True)
+class BitWidths:
+    """Quantizer bit widths of the reference's quantized model, in ``bit_width.json`` terms (model.py:16-45):
+    ``inverted_residual[i] = ((expand_w, expand_act), (dw_w, dw_act), (project_w,))``, ``(None, None)`` for the
+    expand of t == 1 blocks. Defaults: all 8 (``config/train/exp_1/bit_width.json``)."""
+    image: int = 8
+    first_conv: Tuple[int, int] = (8, 8)
+    last_conv: Tuple[int, int] = (8, 8)
+    fully_connected: Tuple[int, int] = (8, 8)
+    shared_act: int = 8
+    pooling: int = 8
+    inverted_residual: Tuple = tuple(((8, 8), (8, 8), (8,)) for _ in range(N_BLOCKS))
+
+    @staticmethod
+    def qmobilenet_default() -> 'BitWidths':
+        """QMobileNetV2's built-in default (mobilenet_v2.py:140-167) + QURSONetHead's 8-bit head."""
+        ir = (((None, None), (3, 3), (3,)),) + tuple(((3, 3), (3, 3), (3,)) for _ in range(N_BLOCKS - 1))
+        return BitWidths(8, (3, 3), (3, 3), (8, 8), 4, 8, ir)
+
+    def block(self, i: int):
+        """-> (expand_w, expand_act, dw_w, dw_act, project_w) of inverted residual i (0-based)."""
+        (ew, ea), (dw, da), (pw,) = self.inverted_residual[i]
+        return ew, ea, dw, da, pw
+
+    def all_widths(self) -> List[int]:
+        v = [self.image, *self.first_conv, *self.last_conv, *self.fully_connected, self.shared_act, self.pooling]
+        for b in self.inverted_residual:
+            v += [x for t in b for x in t if x is not None]
+        return v
+
+
+def parse_bit_width(path_or_dict) -> BitWidths:
+    """A reference ``bit_width.json`` (path, or the dict ``load_bit_width`` returns; string values are parsed with
+    ``ast.literal_eval`` like model.py:33-38) -> ``BitWidths``. Missing keys keep their 8-bit default."""
     d = path_or_dict
     if not isinstance(d, dict):
         with open(d) as f:
             d = json.load(f)
-    vals: List[int] = []
-    for k, v in d.items():
-        items = v if k == 'inverted_residual' else [v]
-        for it in items:
-            x = ast.literal_eval(it) if isinstance(it, str) else it
-            flat = [x] if isinstance(x, int) else [z for t in (x if isinstance(x, (list, tuple)) else [x])
-                                                      for z in (t if isinstance(t, tuple) else (t,))]
-            vals += [int(z) for z in flat if z is not None]
-    if any(v != 8 for v in vals):
-        raise NotImplementedError(f'only 8-bit Brevitas configs map to the int8 MFMA path (got {sorted(set(vals))})')
+    lit = lambda x: ast.literal_eval(x) if isinstance(x, str) else x   # noqa: E731
+    kw = {}
+    for k in ('image', 'shared_act', 'pooling'):
+        if k in d:
+            kw[k] = int(lit(d[k]))
+    for k in ('first_conv', 'last_conv', 'fully_connected'):
+        if k in d:
+            kw[k] = tuple(int(x) for x in lit(d[k]))
+    if 'inverted_residual' in d:
+        ir = [tuple(tuple(t) for t in lit(b)) for b in d['inverted_residual']]
+        if len(ir) != N_BLOCKS:
+            raise ValueError(f'inverted_residual needs {N_BLOCKS} entries, got {len(ir)}')
+        kw['inverted_residual'] = tuple(ir)
+    bw = BitWidths(**kw)
+    check_bit_width(bw)
+    return bw
+
+
+def check_bit_width(path_or_dict_or_widths) -> BitWidths:
+    """Validate a bit-width configuration for the int8 path: every width 3..8 (-> the parsed ``BitWidths``)."""
+    bw = path_or_dict_or_widths
+    if not isinstance(bw, BitWidths):
+        return parse_bit_width(bw)
+    bad = sorted({v for v in bw.all_widths() if not (3 <= int(v) <= 8)})
+    if bad:
+        raise NotImplementedError(f'bit widths {bad}: the int8 MFMA path holds 3..8-bit quantizers (1 and 2 bits '
+                                  f'are Brevitas binary / ternary quantizers, quantizers.py:78-96)')
+    return bw
+
+
+def uint_levels(bits: int) -> int:
+    """Top code of an unsigned b-bit quantizer."""
+    return (1 << bits) - 1
+
+
+def int_levels(bits: int) -> int:
+    """Top code of a signed b-bit quantizer (the scale unit of the signed activation quantizers)."""
+    return (1 << (bits - 1)) - 1
 
 
 def _bn(sd, p, x):
@@ -64,16 +135,19 @@ def _cbn(sd, p, x, stride, groups):
 
 
 @torch.no_grad()
-def calibrate(sd: Dict, frames_u8: np.ndarray, percentile: float = 99.999, residual: bool = True) -> Dict:
-    """Activation scales from the float model's statistics on ``frames_u8`` (B x H x W x 3 uint8)."""
+def calibrate(sd: Dict, frames_u8: np.ndarray, percentile: float = 99.999, residual: bool = True,
+              bw: Optional[BitWidths] = None) -> Dict:
+    """Activation scales from the float model's statistics on ``frames_u8`` (B x H x W x 3 uint8): the
+    percentile |x| over the top code of each quantizer's bit width (``bw``, default all 8)."""
+    bw = bw or BitWidths()
     def amax(*ts):
         v = torch.cat([t.abs().flatten() for t in ts]).numpy().astype(np.float64)
         return float(max(np.percentile(v, percentile), 1e-8))
 
     x = torch.from_numpy(frames_u8).permute(0, 3, 1, 2).float() / 255.0
-    qp: Dict = {'image': amax(x) / 127.0, 'blocks': []}
+    qp: Dict = {'image': amax(x) / int_levels(bw.image), 'blocks': []}
     x = F.relu(_cbn(sd, f'{FP}.0', x, 2, 1))
-    qp['stem'] = amax(x) / 255.0
+    qp['stem'] = amax(x) / uint_levels(bw.first_conv[1])
     cin, idx = 32, 1
     for t, c, n, s in IR_SETTINGS:
         for i in range(n):
@@ -83,19 +157,20 @@ def calibrate(sd: Dict, frames_u8: np.ndarray, percentile: float = 99.999, resid
             y, j = x, 0
             if t != 1:
                 y = F.relu(_cbn(sd, f'{FP}.{idx}.conv.0', y, 1, 1))
-                b['expand'] = amax(y) / 255.0
+                b['expand'] = amax(y) / uint_levels(bw.block(idx - 1)[1])
                 j = 1
             y = F.relu(_cbn(sd, f'{FP}.{idx}.conv.{j}', y, stride, y.shape[1]))
-            b['dw'] = amax(y) / 255.0
+            b['dw'] = amax(y) / uint_levels(bw.block(idx - 1)[3])
             y = _cbn(sd, f'{FP}.{idx}.conv.{j + 1}', y, 1, 1)
             if idx > 1:
-                b['quant'] = (amax(x, y) if res else amax(x)) / 127.0
+                b['quant'] = (amax(x, y) if res else amax(x)) / int_levels(bw.shared_act)
             x = x + y if res else y
             qp['blocks'].append(b)
             cin, idx = c, idx + 1
-    qp['final'] = amax(x) / 127.0
+    qp['final'] = amax(x) / int_levels(bw.shared_act)
     x = F.relu(_cbn(sd, f'{FP}.{idx}', x, 1, 1))
-    qp['last'] = amax(x) / 255.0
+    qp['last'] = amax(x) / uint_levels(bw.last_conv[1])
+    qp['bits'] = bw
     return qp
 
 
@@ -107,3 +182,5 @@ def validate(qp: Dict, residual: bool = True) -> None:
         assert (b['expand'] is None) == (blk.expand == 1)
     for k in ('image', 'stem', 'final', 'last'):
         assert qp[k] > 0
+    if qp.get('bits') is not None:
+        check_bit_width(qp['bits'])

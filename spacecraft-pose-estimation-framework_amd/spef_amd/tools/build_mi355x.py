@@ -18,7 +18,8 @@ import sys
 import time
 
 
-def build(sd, cfg, out_dir: str, dtype: str, calib_frames=None) -> dict:
+def build(sd, cfg, out_dir: str, dtype: str, calib_frames=None, bit_width=None) -> dict:
+    """``bit_width``: the experiment's bit_width.json as quant.BitWidths (int8 only; None = all 8 bits)."""
     from .. import blob as Bl
     from ..arch import arch_from_state_dict
     os.makedirs(out_dir, exist_ok=True)
@@ -28,10 +29,11 @@ def build(sd, cfg, out_dir: str, dtype: str, calib_frames=None) -> dict:
         from ..blob_q8 import pack_int8
         from ..quant import calibrate
         assert calib_frames is not None, 'int8 builds calibrate activation scales on frames'
-        qp = calibrate(sd, calib_frames, residual=cfg.MODEL.BACKBONE.RESIDUAL)
+        qp = calibrate(sd, calib_frames, residual=cfg.MODEL.BACKBONE.RESIDUAL, bw=bit_width)
         blob = pack_int8(sd, qp, arch)
+        import dataclasses
         with open(os.path.join(out_dir, 'qparams.json'), 'w') as f:
-            json.dump(qp, f, indent=1)
+            json.dump(dict(qp, bits=dataclasses.asdict(qp['bits'])), f, indent=1)
     else:
         blob = Bl.pack(sd, arch, dtype=dtype)
     with open(os.path.join(out_dir, 'model.spef'), 'wb') as f:
@@ -59,12 +61,14 @@ def main(argv=None):
     if a.experiment:
         cfg = load_config(os.path.join(a.experiment, 'config.yaml'))
         sd = torch.load(os.path.join(a.experiment, 'model', 'parameters.pt'), map_location='cpu', weights_only=True)
-        bw = os.path.join(a.experiment, 'model', 'bit_width.json')
-        if os.path.exists(bw):
-            from ..quant import check_bit_width
-            check_bit_width(bw)
+        bit_width = None
+        bw_path = os.path.join(a.experiment, 'model', 'bit_width.json')
+        if os.path.exists(bw_path):
+            from ..quant import parse_bit_width
+            bit_width = parse_bit_width(bw_path)
         name = os.path.basename(os.path.normpath(a.experiment))
     elif a.synthetic:
+        bit_width = None
         from ..arch import mobilenet_v2
         from ..weights import synthetic_state_dict
         cfg = load_config(None)
@@ -81,7 +85,7 @@ def main(argv=None):
     dtype = a.dtype or cfg.MI355X.DTYPE
     out = a.out or os.path.join('experiments', 'build', 'mi355x', name)
     calib = synth_frames(cfg.MI355X.CALIB_FRAMES, *cfg.DATA.IMG_SIZE, 900) if dtype == 'int8' else None
-    info = build(sd, cfg, out, dtype, calib)
+    info = build(sd, cfg, out, dtype, calib, bit_width)
     print(json.dumps(info))
     return 0
 

@@ -88,3 +88,71 @@ def test_int8_general_shift_kernels_bit_exact(q8):
         np.testing.assert_array_equal(p.cpu().numpy(), rp)
     finally:
         e.close()
+
+
+def _mixed_widths():
+    from spef_amd.quant import parse_bit_width
+    return parse_bit_width({'image': '6', 'first_conv': '(4, 5)', 'last_conv': '(5, 4)', 'fully_connected': '(6, 7)',
+                            'shared_act': '5', 'pooling': '7',
+                            'inverted_residual': ['[(None, None), (6, 5), (7,)]'] +
+                                                 ['[(5, 4), (6, 3), (4,)]', '[(3, 6), (4, 7), (5,)]'] * 8})
+
+
+@pytest.fixture(scope='module', params=['qmobilenet_default', 'mixed'])
+def q8low(request):
+    """Sub-8-bit quantizers in int8 containers (f2): the reference QMobileNetV2's default 3-bit / 4-bit-shared
+    config (mobilenet_v2.py:140-167) and a mixed 3..7-bit bit_width.json."""
+    from spef_amd.engine import Engine
+    from spef_amd.quant import BitWidths
+    sd = synthetic_state_dict(mobilenet_v2(), seed=1001)
+    bw = BitWidths.qmobilenet_default() if request.param == 'qmobilenet_default' else _mixed_widths()
+    qp = calibrate(sd, synth_frames(4, 128, 128, 900), bw=bw)
+    e = Engine(pack_int8(sd, qp), 'cuda:0')
+    yield e, sd, qp
+    e.close()
+
+
+def test_low_bit_activations_bit_exact(q8low):
+    eng, sd, qp = q8low
+    fr = synth_frames(2, 96, 64, 17)
+    x = torch.from_numpy(fr).cuda()
+    for op in (0, 1, 2, 3, 5, 8, 12, 14, 16, 17):
+        got = eng.probe(x, op).cpu().numpy()
+        ref = _nhwc(Q.int8_forward(fr, sd, qp, upto=op))
+        np.testing.assert_array_equal(got, ref.astype(np.float32), err_msg=f'op {op}')
+
+
+def test_low_bit_head_outputs_bit_exact(q8low):
+    """u8 frames and float NCHW frames (input quantizer of the configured width), and the general-shift fused
+    variant: every output bit-identical to the oracle."""
+    from spef_amd.engine import Engine
+    eng, sd, qp = q8low
+    fr = synth_frames(3, 128, 96, 19)
+    ro, rp = Q.int8_forward(fr, sd, qp)
+    o, p = eng.forward(torch.from_numpy(fr).cuda())
+    np.testing.assert_array_equal(o.cpu().numpy(), ro)
+    np.testing.assert_array_equal(p.cpu().numpy(), rp)
+    of, pf = eng.forward(M.u8_nhwc_to_nchw_f32(fr).contiguous().cuda())
+    np.testing.assert_array_equal(of.cpu().numpy(), ro)
+    np.testing.assert_array_equal(pf.cpu().numpy(), rp)
+    e = Engine(pack_int8(sd, qp, shift32=False), 'cuda:0')
+    try:
+        o2, p2 = e.forward(torch.from_numpy(fr).cuda())
+        np.testing.assert_array_equal(o2.cpu().numpy(), ro)
+        np.testing.assert_array_equal(p2.cpu().numpy(), rp)
+    finally:
+        e.close()
+
+
+def test_low_bit_unfused_schedule_bit_exact(q8low):
+    """The one-kernel-per-conv int8 schedule honours the same widths (stem, GEMM epilogues, depthwise, pool)."""
+    eng, sd, qp = q8low
+    fr = synth_frames(2, 64, 96, 23)
+    ro, rp = Q.int8_forward(fr, sd, qp)
+    eng.set_fused(False)
+    try:
+        o, p = eng.forward(torch.from_numpy(fr).cuda())
+    finally:
+        eng.set_fused(True)
+    np.testing.assert_array_equal(o.cpu().numpy(), ro)
+    np.testing.assert_array_equal(p.cpu().numpy(), rp)

@@ -68,10 +68,51 @@ def test_fixed_point_requant_matches_float():
     assert np.abs(got - want).max() <= 1 and (got != want).mean() < 1e-4
 
 
-def test_bit_width_config():
-    check_bit_width({'image': '8', 'first_conv': '(8, 8)', 'inverted_residual': ['[(8, 8), (8, 8), (8,)]']})
+def test_bit_width_config(golden):
+    """bit_width.json (model.py:16-45 string format) -> BitWidths: the reference's exp_1 file is all 8; the
+    QMobileNetV2 built-in default (mobilenet_v2.py:140-167) is 3-bit with a 4-bit shared quantizer; widths 1-2
+    (Brevitas binary / ternary quantizers) are rejected, as are malformed block lists."""
+    from spef_amd.quant import BitWidths, parse_bit_width
+    exp1 = {'image': '8', 'first_conv': '(8, 8)', 'last_conv': '(8, 8)', 'fully_connected': '(8, 8)',
+            'shared_act': '8', 'pooling': '8', 'inverted_residual': ['[(8, 8), (8, 8), (8,)]'] * 17}
+    assert parse_bit_width(exp1) == BitWidths() and check_bit_width(exp1) == BitWidths()
+    q = BitWidths.qmobilenet_default()
+    assert q.block(0) == (None, None, 3, 3, 3) and q.block(16) == (3, 3, 3, 3, 3) and q.shared_act == 4
+    mixed = dict(exp1, first_conv='(4, 5)', inverted_residual=['[(None, None), (6, 5), (7,)]'] +
+                 ['[(5, 4), (6, 3), (4,)]'] * 16)
+    bw = parse_bit_width(mixed)
+    assert bw.first_conv == (4, 5) and bw.block(3) == (5, 4, 6, 3, 4)
     with pytest.raises(NotImplementedError):
-        check_bit_width({'image': '8', 'first_conv': '(4, 4)'})
+        check_bit_width(dict(exp1, shared_act='2'))
+    with pytest.raises(ValueError):
+        parse_bit_width(dict(exp1, inverted_residual=['[(8, 8), (8, 8), (8,)]']))
+
+
+def test_low_bit_widths_oracle_and_blob(model):
+    """3/4-bit (QMobileNetV2 default): codes stay inside each quantizer's range, the blob carries the widths in
+    each op's qbits, and the integer network still tracks the FP32 model's head outputs."""
+    from spef_amd.quant import BitWidths
+    sd, _ = model
+    bw = BitWidths.qmobilenet_default()
+    qp = calibrate(sd, synth_frames(4, 128, 128, 900), bw=bw)
+    validate(qp)
+    fr = synth_frames(2, 64, 64, 5)
+    stem = Q.int8_forward(fr, sd, qp, upto=0)
+    assert stem.min() >= 0 and stem.max() <= 7
+    for op in (1, 4, 10, 17):
+        a = Q.int8_forward(fr, sd, qp, upto=op)
+        assert a.min() >= -8 and a.max() <= 7, op
+    last = Q.int8_forward(fr, sd, qp, upto='last')
+    assert last.min() >= 0 and last.max() <= 7
+    info = Bl.describe(pack_int8(sd, qp))
+    raw = pack_int8(sd, qp)
+    qb = [raw[info['ops_off'] + i * Bl._OP.size + 104: info['ops_off'] + i * Bl._OP.size + 108]
+          for i in range(info['n_ops'])]
+    assert qb[0][:2] == bytes([3, 8]) and qb[2][:3] == bytes([3, 3, 4]) and qb[18][:2] == bytes([3, 8])
+    assert qb[19][:1] == bytes([8])
+    o, p = Q.int8_forward(fr, sd, qp)
+    fo, fp = Q.fake_quant_forward(fr, sd, qp)
+    assert np.abs(o - fo.numpy()).max() < 0.05 * np.abs(fo.numpy()).max()
 
 
 def test_fixed_point_shift_rule():
