@@ -134,20 +134,45 @@ def _cbn(sd, p, x, stride, groups):
     return _bn(sd, p, F.conv2d(x, w, None, stride, (k - 1) // 2, 1, groups))
 
 
+def _mse_clip(v: np.ndarray, levels: int, signed: bool) -> float:
+    """The clip value c minimising the mean squared quantisation error of the values ``v`` for a quantizer with
+    ``levels`` top code (scale c / levels; signed: codes down to -levels - 1), searched over c = f max|v|."""
+    a = np.abs(v).max()
+    if a <= 0:
+        return 1e-8
+    lo = -levels - 1 if signed else 0
+    best, best_c = np.inf, a
+    for f in np.linspace(0.05, 1.0, 96):
+        sc = f * a / levels
+        e = np.mean((np.clip(np.rint(v / sc), lo, levels) * sc - v) ** 2)
+        if e < best:
+            best, best_c = e, f * a
+    return float(best_c)
+
+
 @torch.no_grad()
 def calibrate(sd: Dict, frames_u8: np.ndarray, percentile: float = 99.999, residual: bool = True,
-              bw: Optional[BitWidths] = None) -> Dict:
-    """Activation scales from the float model's statistics on ``frames_u8`` (B x H x W x 3 uint8): the
-    percentile |x| over the top code of each quantizer's bit width (``bw``, default all 8)."""
+              bw: Optional[BitWidths] = None, method: str = 'percentile') -> Dict:
+    """Activation scales from the float model's statistics on ``frames_u8`` (B x H x W x 3 uint8), one per
+    quantizer (per tensor, as Brevitas), over the top code of its bit width (``bw``, default all 8):
+    ``method='percentile'`` clips at the ``percentile`` of |x|; ``'mse'`` picks the clip that minimises the
+    quantisation MSE of the observed values (a common PTQ initialisation; QAT refines the scales further)."""
     bw = bw or BitWidths()
-    def amax(*ts):
-        v = torch.cat([t.abs().flatten() for t in ts]).numpy().astype(np.float64)
-        return float(max(np.percentile(v, percentile), 1e-8))
+    assert method in ('percentile', 'mse')
+    rng = np.random.default_rng(0)
+
+    def amax(*ts, levels=255, signed=False):
+        v = torch.cat([t.flatten() for t in ts]).numpy().astype(np.float64)
+        if method == 'mse':
+            if v.size > 1 << 20:
+                v = rng.choice(v, 1 << 20, replace=False)
+            return _mse_clip(v, levels, signed)
+        return float(max(np.percentile(np.abs(v), percentile), 1e-8))
 
     x = torch.from_numpy(frames_u8).permute(0, 3, 1, 2).float() / 255.0
-    qp: Dict = {'image': amax(x) / int_levels(bw.image), 'blocks': []}
+    qp: Dict = {'image': amax(x, levels=int_levels(bw.image), signed=True) / int_levels(bw.image), 'blocks': []}
     x = F.relu(_cbn(sd, f'{FP}.0', x, 2, 1))
-    qp['stem'] = amax(x) / uint_levels(bw.first_conv[1])
+    qp['stem'] = amax(x, levels=uint_levels(bw.first_conv[1])) / uint_levels(bw.first_conv[1])
     cin, idx = 32, 1
     for t, c, n, s in IR_SETTINGS:
         for i in range(n):
@@ -157,19 +182,22 @@ def calibrate(sd: Dict, frames_u8: np.ndarray, percentile: float = 99.999, resid
             y, j = x, 0
             if t != 1:
                 y = F.relu(_cbn(sd, f'{FP}.{idx}.conv.0', y, 1, 1))
-                b['expand'] = amax(y) / uint_levels(bw.block(idx - 1)[1])
+                lv = uint_levels(bw.block(idx - 1)[1])
+                b['expand'] = amax(y, levels=lv) / lv
                 j = 1
             y = F.relu(_cbn(sd, f'{FP}.{idx}.conv.{j}', y, stride, y.shape[1]))
-            b['dw'] = amax(y) / uint_levels(bw.block(idx - 1)[3])
+            lv = uint_levels(bw.block(idx - 1)[3])
+            b['dw'] = amax(y, levels=lv) / lv
             y = _cbn(sd, f'{FP}.{idx}.conv.{j + 1}', y, 1, 1)
             if idx > 1:
-                b['quant'] = (amax(x, y) if res else amax(x)) / int_levels(bw.shared_act)
+                lv = int_levels(bw.shared_act)
+                b['quant'] = (amax(x, y, levels=lv, signed=True) if res else amax(x, levels=lv, signed=True)) / lv
             x = x + y if res else y
             qp['blocks'].append(b)
             cin, idx = c, idx + 1
-    qp['final'] = amax(x) / int_levels(bw.shared_act)
+    qp['final'] = amax(x, levels=int_levels(bw.shared_act), signed=True) / int_levels(bw.shared_act)
     x = F.relu(_cbn(sd, f'{FP}.{idx}', x, 1, 1))
-    qp['last'] = amax(x) / uint_levels(bw.last_conv[1])
+    qp['last'] = amax(x, levels=uint_levels(bw.last_conv[1])) / uint_levels(bw.last_conv[1])
     qp['bits'] = bw
     return qp
 

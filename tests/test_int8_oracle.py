@@ -120,3 +120,31 @@ def test_fixed_point_shift_rule():
     M_, B_, S_ = Q.fixed(np.array([0.3, 1e-2, 2.0 ** -12, 1e-5, 0.7]), np.zeros(5))
     assert list(S_[:3]) == [32, 32, 32] and S_[3] > 32 and S_[4] < 32
     assert np.all(np.abs(M_) < 2 ** 31)
+
+
+def test_int8_pose_error_within_int8_bound(model):
+    """The INT8 accuracy bound the bench reports against (bench.py INT8_BOUND): pose decoded
+    from the integer network vs from FP32 on the same frames (8 SPEED-style frames at 256x256)."""
+    import bench
+    from oracle import decode_ref as D
+    sd, qp = model
+    fr = synth_frames(8, 256, 256, 10000)
+    o, p = Q.int8_forward(fr, sd, qp)
+    ro, rp = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd)
+    h, _ = D.orientation_histogram(12, False)
+    ang = D.angle_deg_stable(D.decode_orientation_batch(D.softmax_f32(o), h),
+                             D.decode_orientation_batch(D.softmax_f32(ro.numpy()), h))
+    lb, pb, ab = bench.INT8_BOUND
+    assert np.abs(o - ro.numpy()).max() < lb and np.abs(p - rp.numpy()).max() < pb and ang.max() < ab
+
+
+def test_mse_calibration_option(model):
+    """calibrate(method='mse') (quantisation-MSE-optimal clip per tensor) gives valid scales and stays within the
+    same accuracy class."""
+    sd, _ = model
+    qp = calibrate(sd, synth_frames(2, 96, 96, 900), method='mse')
+    validate(qp)
+    fr = synth_frames(2, 96, 96, 31)
+    o, _ = Q.int8_forward(fr, sd, qp)
+    ro, _ = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd)
+    assert np.abs(o - ro.numpy()).max() < 0.08 * np.abs(ro.numpy()).max()
