@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void pw_kernel(const typename DT::T* __restric
 }
 
 // ------------------------------------------------------------------------------------------ depthwise
-template <typename DT, int S>
+template <typename DT, int S, bool VP = false>
 __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restrict__ X, const typename DT::DW* __restrict__ W9,
                                                  const float* __restrict__ bias, typename DT::T* __restrict__ Y,
                                                  int B, int H, int W, int C, int OH, int OW) {
@@ -176,6 +176,35 @@ __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restric
     acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w;
     acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
   }
+  if constexpr (VP) {
+    // vertical pairs (k_irb.hip, fp16 blocks 2-7): per kernel column, even output rows (and every stride-2 row)
+    // dot2(ky 0, 1) then fma(ky 2); odd stride-1 rows fma(ky 0) then dot2(ky 1, 2). Rows outside the image are 0
+    // (the fused kernels' zero padding), so the same instructions see the same operands.
+    const bool odd = S == 1 && (oy & 1);
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ox * S - 1 + kx;
+      if (ix < 0 || ix >= W) continue;
+      f16x8 xv[3], wv[3];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int iy = oy * S - 1 + ky;
+        xv[ky] = (iy >= 0 && iy < H) ? *reinterpret_cast<const f16x8*>(X + (((int64_t)b * H + iy) * W + ix) * C + c)
+                                     : f16x8{};
+        wv[ky] = *reinterpret_cast<const f16x8*>(W9 + (ky * 3 + kx) * C + c);
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        if (!odd) {
+          acc[e] = dot2h(pack_h2(xv[0][e], xv[1][e]), pack_h2(wv[0][e], wv[1][e]), acc[e]);
+          acc[e] = fmaf((float)xv[2][e], (float)wv[2][e], acc[e]);
+        } else {
+          acc[e] = fmaf((float)xv[0][e], (float)wv[0][e], acc[e]);
+          acc[e] = dot2h(pack_h2(xv[1][e], xv[2][e]), pack_h2(wv[1][e], wv[2][e]), acc[e]);
+        }
+      }
+    }
+  } else
 #pragma unroll
   for (int kx = 0; kx < 3; ++kx) {        // kx outer, ky inner: the fused kernels' accumulation order
     const int ix = ox * S - 1 + kx;
@@ -335,10 +364,16 @@ hipError_t launch_pw(int dtype, int epi, const void* x, const void* wt, const fl
 }
 
 hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias, void* y, int B, int H, int W, int C,
-                     int stride, int OH, int OW, hipStream_t s) {
+                     int stride, int OH, int OW, bool pairs, hipStream_t s) {
   if (C & 7) return hipErrorInvalidValue;
+  if (pairs && dtype != DT_F16) return hipErrorInvalidValue;
   const unsigned g = blocks_for((int64_t)B * OH * OW * (C / 8), 256);
-  if (dtype == DT_F16) {
+  if (pairs) {
+    if (stride == 1)
+      dw_kernel<F16, 1, true><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
+    else
+      dw_kernel<F16, 2, true><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
+  } else if (dtype == DT_F16) {
     if (stride == 1)
       dw_kernel<F16, 1><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
     else

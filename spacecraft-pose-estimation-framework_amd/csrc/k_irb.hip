@@ -23,13 +23,29 @@
 
 namespace spef {
 
+// Vertical-pair depthwise (VP, fp16 stride-1 blocks 3, 5, 6): the hidden slab holds, per position (row pair pr,
+// column), one dword per channel = (row 2pr, row 2pr+1) -- the depthwise takes two taps of a kernel column with one
+// v_dot2_f32_f16 and the third with one v_fma_mix. The unfused dw_kernel uses the same order for these blocks
+// (irb_dw_pairs), so both schedules stay bit-identical. (Stride 2 measured slower: a 3-row window straddles two
+// pairs, so every output row reads 1.5x the slab bytes, and the odd input-tile height wastes half a pair row.)
+constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) { return f16 && expand && hid <= 192 && stride == 1; }
+
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
-          bool STW, int DWB = 4>
+          bool STW, int DWB = 4, bool VP = false>
 struct IrbGeom {
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW;
   static constexpr int PIN16 = (PIN + 15) / 16;
   static constexpr int PINP = PIN16 * 16;
+  // VP slab: 4 channel-group regions (channels 8g..8g+7, 32 B per position); regions 16 B apart mod 256 B so the
+  // depthwise's ds_read_b128 lane groups (kg 0/1 and 2/3 mixed) hit distinct bank slots
+  static constexpr int PR = (IH + 1) / 2;        // row pairs of the input tile
+  static constexpr int NQ = PR * IW;             // pair positions
+  static constexpr int NU = (NQ + 15) / 16;      // expand units: 16 positions = 2 MFMA pixel tiles (even, odd row)
+  static constexpr int NQP = NU * 16;
+  static constexpr int RS = NQP * 32 + 16;       // bytes per channel-group region
+  static constexpr int EPU = (NU + NW - 1) / NW; // expand units per wave
+  static constexpr int VSLAB = 3 * 64;           // dwords per chunk: [kx][(w0,w1) x 32 | (w1,w2) x 32]
   static constexpr bool K16 = CIN == 16;          // 16-channel input: K = 16 MFMA, no K padding in LDS
   static constexpr int CINP = K16 ? 16 : (CIN + 31) / 32 * 32;
   // Row strides: a multiple of 16 B that is 2 mod 4 granules makes ds_read_b128 of 16 consecutive rows
@@ -53,7 +69,8 @@ struct IrbGeom {
   static constexpr int WP_PIECES = STW ? NCTP * 4 : 0;
   static constexpr int W_PPT = (WE_PIECES + WP_PIECES + NW * 64 - 1) / (NW * 64);   // 16-B pieces per thread
   static constexpr int bytes_for(int xs, int es) {
-    return (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 + 2 * SLAB * DWB + BIAS * 4;
+    return VP ? (PINP * xs + WE_ELEMS + WP_ELEMS) * 2 + NBUF * 4 * RS + 2 * VSLAB * 4 + BIAS * 4
+              : (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 + 2 * SLAB * DWB + BIAS * 4;
   }
   static constexpr bool WIDE = (163840 / bytes_for(CINP + 16, 48)) >= (163840 / bytes_for(CINP + 8, 40));
   static constexpr int XS = WIDE ? CINP + 16 : CINP + 8;   // Xs row stride (elements)
@@ -77,8 +94,9 @@ struct IrbGeom {
   static_assert(!RES || (S == 1 && CIN == COUT), "residual needs stride 1 and cin == cout");
   static_assert(NW * 64 >= SLAB_PIECES, "slab fill needs one 16-B piece per thread");
   static_assert(SLAB % 4 == 0 && (NCH_ * 32) % 4 == 0, "float4 slabs");
-  static_assert(EPT <= 32, "validity mask is 32 bits");
+  static_assert(EPT <= 32 && 2 * EPU <= 32, "validity mask is 32 bits");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
+  static_assert(!VP || S == 2 || (TW == 16 && TH % 2 == 0), "VP stride 1: 16-wide tiles (wave-uniform row parity)");
 };
 
 // ABL (timing ablations only, never dispatched by default): 1 = depthwise centre tap only, 2 = no expand
@@ -92,18 +110,21 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
     int tiles_y, uint32_t nwg) {
   using DW = typename DT::DW;
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW)>;
+  constexpr bool VP = irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
   using x4 = typename DT::x4;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Xs = reinterpret_cast<T*>(smem);
-  T* Es0 = Xs + G::PINP * G::XS;
-  T* Es1 = Es0 + (G::NBUF == 2 ? G::PINP * G::ES : 0);
-  T* WEs = Es0 + G::NBUF * G::PINP * G::ES;                                // [3][32][WES] expand weights
+  T* Es0 = Xs + G::PINP * G::XS;                                            // hidden slab(s)
+  constexpr int ES_BYTES = VP ? 4 * G::RS : G::PINP * G::ES * 2;           // one slab buffer
+  T* Es1 = reinterpret_cast<T*>(reinterpret_cast<char*>(Es0) + (G::NBUF == 2 ? ES_BYTES : 0));
+  T* WEs = reinterpret_cast<T*>(reinterpret_cast<char*>(Es0) + G::NBUF * ES_BYTES);   // [3][32][WES] expand weights
   T* WPs = WEs + G::WE_ELEMS;                                               // [2][NCTP][WPS] project weights
   DW* Sl = reinterpret_cast<DW*>(WPs + G::WP_ELEMS);                        // [2][SLAB] dw weights
-  float* Bd = reinterpret_cast<float*>(Sl + 2 * G::SLAB);                   // [HIDP] dw bias
+  uint32_t* Slv = reinterpret_cast<uint32_t*>(Sl);                          // VP: [2][VSLAB] weight pairs
+  float* Bd = reinterpret_cast<float*>(reinterpret_cast<char*>(Sl) + (VP ? 2 * G::VSLAB * 4 : 2 * G::SLAB * (int)sizeof(DW)));
   float* Be = Bd + G::NCH * 32;                                             // [HIDP] expand bias
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -121,14 +142,35 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 
   // depthwise-weight slab of chunk cc: thread t < SLAB_PIECES moves one 16-B piece of [9][32]
   constexpr int EPP = 16 / (int)sizeof(DW);      // weights per piece
+  // VP: piece t < 48 builds 4 weight pairs (kx = t / 16, pair (ky, ky+1) with ky = (t / 8) % 2, channels 4 (t % 8)..)
+  // from two 8-B pieces of the [9][HID] fp16 weights
+  const int vt = NW * 64 - 1 - tid;   // VP piece index: the last wave (fewest expand units) builds the pairs
   auto slab_ok = [&](int cc) {
+    if constexpr (VP) return vt < 48 && cc < G::NCH && 32 * cc + 4 * (vt & 7) < HID;
     return ABL != 7 && tid < G::SLAB_PIECES && cc < G::NCH && 32 * cc + ((tid * EPP) & 31) < HID;
   };
   auto slab_load = [&](int cc) -> uint4 {
+    if constexpr (VP) {
+      const int kx = vt >> 4, ky = (vt >> 3) & 1, ch = 32 * cc + 4 * (vt & 7);
+      const bool ok = slab_ok(cc);
+      const uint2 a = *reinterpret_cast<const uint2*>(Wd + (ok ? (ky * 3 + kx) * HID + ch : 0));
+      const uint2 b = *reinterpret_cast<const uint2*>(Wd + (ok ? ((ky + 1) * 3 + kx) * HID + ch : 0));
+      return make_uint4(a.x, a.y, b.x, b.y);
+    }
     const int f = tid * EPP, tap = f >> 5, ch = 32 * cc + (f & 31);
     return *reinterpret_cast<const uint4*>(Wd + (slab_ok(cc) ? tap * HID + ch : 0));
   };
   auto slab_store = [&](int cc, uint4 v) {
+    if constexpr (VP) {
+      if (vt < 48) {
+        const int kx = vt >> 4, ky = (vt >> 3) & 1;
+        uint4 d = make_uint4((v.x & 0xffffu) | (v.z << 16), (v.x >> 16) | (v.z & 0xffff0000u),
+                             (v.y & 0xffffu) | (v.w << 16), (v.y >> 16) | (v.w & 0xffff0000u));
+        if (!slab_ok(cc)) d = make_uint4(0, 0, 0, 0);
+        *reinterpret_cast<uint4*>(Slv + (cc & 1) * G::VSLAB + kx * 64 + ky * 32 + 4 * (vt & 7)) = d;
+      }
+      return;
+    }
     if (tid < G::SLAB_PIECES)
       *reinterpret_cast<uint4*>(Sl + (cc & 1) * G::SLAB + tid * EPP) = slab_ok(cc) ? v : make_uint4(0, 0, 0, 0);
   };
@@ -229,7 +271,19 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   // interior tiles (whole input tile inside the image) need no padding mask in the expand epilogue
   const bool interior = iy0 >= 0 && ix0 >= 0 && iy0 + G::IH <= H && ix0 + G::IW <= W;
   uint32_t pvmask = 0;
-  if (EXPAND && !interior) {   // only edge tiles mask (workgroup-uniform branch)
+  if (VP && !interior) {       // VP: bits 2j / 2j+1 = even / odd row pixel of unit j
+#pragma unroll
+    for (int j = 0; j < G::EPU; ++j) {
+      const int q = (wave + NW * j) * 16 + r16;
+      if (q < G::NQ) {
+        const int pr = q / G::IW, col = q - pr * G::IW;
+        const int iy = iy0 + 2 * pr, ix = ix0 + col;
+        const bool cx = ix >= 0 && ix < W;
+        if (cx && iy >= 0 && iy < H) pvmask |= 1u << (2 * j);
+        if (cx && 2 * pr + 1 < G::IH && iy + 1 >= 0 && iy + 1 < H) pvmask |= 2u << (2 * j);
+      }
+    }
+  } else if (EXPAND && !interior) {   // only edge tiles mask (workgroup-uniform branch)
 #pragma unroll
     for (int j = 0; j < G::EPT; ++j) {
       const int p = (wave + NW * j) * 16 + r16;
@@ -340,6 +394,75 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       // LDS round trip + MFMA latency per tile.
       // (Only while the fragments fit in 12 VGPRs: measured slower for blocks 4 and 17, where they do not.)
       constexpr int NBX = G::K16 ? 1 : G::KS;
+      if constexpr (VP) {
+        // unit j = 16 pair positions q; lane r16 computes the even- and odd-row pixel of its position (two MFMA
+        // pixel tiles) and stores each channel's pair as one dword
+        using BX = typename std::conditional<G::K16, x4, x8>::type;
+        constexpr bool VBATCH = G::EPU * 2 * NBX * (G::K16 ? 2 : 4) <= 16;
+        BX vbx[G::EPU][2][NBX];
+        auto read_vbx = [&](int j) {
+          const int q = (wave + NW * j) * 16 + r16;
+          const int qc = q < G::NQ ? q : G::NQ - 1;
+          const int pr = qc / G::IW, col = qc - pr * G::IW;
+          const int p0 = 2 * pr * G::IW + col;
+          const int p1 = (G::IH % 2 == 0 || 2 * pr + 1 < G::IH) ? p0 + G::IW : p0;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const T* xr = Xs + (h ? p1 : p0) * G::XS;
+            if constexpr (G::K16) {
+              vbx[j][h][0] = *reinterpret_cast<const x4*>(xr + 4 * kg);
+            } else {
+#pragma unroll
+              for (int ks = 0; ks < G::KS; ++ks) vbx[j][h][ks] = *reinterpret_cast<const x8*>(xr + 8 * kg + 32 * ks);
+            }
+          }
+        };
+#pragma unroll
+        for (int j = 0; j < G::EPU; ++j) {
+          if (!VBATCH || wave + NW * j >= G::NU) break;
+          read_vbx(j);
+        }
+#pragma unroll
+        for (int j = 0; j < G::EPU; ++j) {
+          const int u = wave + NW * j;
+          if (u >= G::NU) break;
+          if (!VBATCH) read_vbx(j);
+          f32x4 e[2][2];
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            e[h][0] = f32x4{eb0.x, eb0.y, eb0.z, eb0.w};
+            e[h][1] = f32x4{eb1.x, eb1.y, eb1.z, eb1.w};
+            if constexpr (G::K16) {
+              e[h][0] = DT::mfma16(q0, vbx[j][h][0], e[h][0]);
+              e[h][1] = DT::mfma16(q1, vbx[j][h][0], e[h][1]);
+            } else {
+#pragma unroll
+              for (int ks = 0; ks < G::KS; ++ks) {
+                e[h][0] = DT::mfma(a0[ks], vbx[j][h][ks], e[h][0]);
+                e[h][1] = DT::mfma(a1[ks], vbx[j][h][ks], e[h][1]);
+              }
+            }
+          }
+          uint4 d[2];
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            d[t] = make_uint4(relu_pk2(e[0][t][0], e[1][t][0]), relu_pk2(e[0][t][1], e[1][t][1]),
+                              relu_pk2(e[0][t][2], e[1][t][2]), relu_pk2(e[0][t][3], e[1][t][3]));
+          if (!interior) {   // zero the halves of pixels outside the image (the depthwise padding)
+            const uint32_t m = (((pvmask >> (2 * j)) & 1u) ? 0x0000ffffu : 0u) |
+                               (((pvmask >> (2 * j)) & 2u) ? 0xffff0000u : 0u);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+              d[t].x &= m; d[t].y &= m; d[t].z &= m; d[t].w &= m;
+            }
+          }
+          // channels 4kg.. -> region kg/2, channels 16+4kg.. -> region 2+kg/2; 16-B half (kg & 1) of the record
+          typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+          char* er = reinterpret_cast<char*>(Ew) + (u * 16 + r16) * 32 + (kg & 1) * 16;
+          *reinterpret_cast<u32x4*>(er + (kg >> 1) * G::RS) = u32x4{d[0].x, d[0].y, d[0].z, d[0].w};
+          *reinterpret_cast<u32x4*>(er + (2 + (kg >> 1)) * G::RS) = u32x4{d[1].x, d[1].y, d[1].z, d[1].w};
+        }
+      } else {
       constexpr bool BATCH = G::EPT * NBX * (G::K16 ? 2 : 4) <= 12;
       typename std::conditional<G::K16, x4, x8>::type bxs[G::EPT][NBX];
       auto read_bx = [&](int j) {
@@ -389,6 +512,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
           *reinterpret_cast<uint2*>(er + 16) = u1;
         }
       }
+      }
       Es = Ew;
     } else {
       Es = Xs;
@@ -406,7 +530,95 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     // Tap order everywhere (here, the front kernel, the unfused dw_kernel): kx outer, ky inner -- the fused
     // and unfused schedules accumulate in the same order and stay bit-identical.
     const bool hv = 32 * c + 8 * kg < HID;    // this lane's 8 hidden channels exist
-    if constexpr (G::PAIR && ABL == 0) {
+    if constexpr (VP) {
+      // Per kernel column kx: two taps by v_dot2 on a row pair, the third by v_fma_mix on one half. Output row
+      // parity fixes the order: even rows (and every stride-2 row) dot2(ky 0,1) then fma(ky 2); odd rows
+      // fma(ky 0) then dot2(ky 1,2) -- exactly dw_kernel<.., VP>'s order.
+      // this lane's channels 8kg..8kg+7 live in region kg (32 B per position)
+      const char* er = reinterpret_cast<const char*>(Es) + kg * G::RS;
+      const uint32_t* sv = Slv + (c & 1) * G::VSLAB + 8 * kg;
+      auto rd8 = [&](const char* p, uint32_t v[8]) {
+        const uint4 a = *reinterpret_cast<const uint4*>(p), b = *reinterpret_cast<const uint4*>(p + 16);
+        v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+      };
+      auto bias8 = [&](float a[8]) {
+        const float4 u0 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg);
+        const float4 u1 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg + 4);
+        a[0] = u0.x; a[1] = u0.y; a[2] = u0.z; a[3] = u0.w; a[4] = u1.x; a[5] = u1.y; a[6] = u1.z; a[7] = u1.w;
+      };
+      if constexpr (G::PAIR) {
+#pragma unroll
+        for (int qi = 0; qi < G::QPW; qi += 2) {   // output rows oy (even) and oy + 1: pairs m = oy / 2 and m + 1
+          x8 bf0 = zero8<DT>(), bf1 = zero8<DT>();
+          if (hv) {
+            float a0[8], a1[8];
+            bias8(a0);
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a1[e] = a0[e];
+            const char* pb = er + ((oyq[qi] >> 1) * G::IW + oxq[qi]) * 32;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              uint32_t pc[8], pn[8], w01[8], w12[8];
+              rd8(pb + kx * 32, pc);
+              rd8(pb + (G::IW + kx) * 32, pn);
+              rd8(reinterpret_cast<const char*>(sv + kx * 64), w01);
+              rd8(reinterpret_cast<const char*>(sv + kx * 64 + 32), w12);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {   // (row oy + 1 first: its fma reads the shared bias, then dot2c
+                a1[e] = fmaf(h_hi(pc[e]), h_lo(w01[e]), a1[e]);   // accumulates in place without a copy)
+                a0[e] = dot2h(pc[e], w01[e], a0[e]);
+                a0[e] = fmaf(h_lo(pn[e]), h_hi(w12[e]), a0[e]);
+                a1[e] = dot2h(pn[e], w12[e], a1[e]);
+              }
+            }
+            bf0 = relu_cvt8<DT>(a0);
+            bf1 = relu_cvt8<DT>(a1);
+          }
+#pragma unroll
+          for (int t = 0; t < G::NCTW; ++t) {
+            acc[qi][t] = DT::mfma(pa[t], bf0, acc[qi][t]);
+            acc[qi + 1][t] = DT::mfma(pa[t], bf1, acc[qi + 1][t]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int qi = 0; qi < G::QPW; ++qi) {
+          x8 bf = zero8<DT>();
+          if (hv) {
+            float a8[8];
+            bias8(a8);
+            // stride 2: pair m = oy (rows 2oy, 2oy+1) + low half of m + 1; stride 1 (TW = 16): the wave's row
+            const int oy = S == 1 ? __builtin_amdgcn_readfirstlane(oyq[qi]) : oyq[qi];
+            const bool odd = S == 1 && (oy & 1);
+            const char* pb = er + ((S == 2 ? oy : oy >> 1) * G::IW + S * oxq[qi]) * 32;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              uint32_t pc[8], pn[8], w01[8], w12[8];
+              rd8(pb + kx * 32, pc);
+              rd8(pb + (G::IW + kx) * 32, pn);
+              rd8(reinterpret_cast<const char*>(sv + kx * 64), w01);
+              rd8(reinterpret_cast<const char*>(sv + kx * 64 + 32), w12);
+              if (!odd) {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  a8[e] = dot2h(pc[e], w01[e], a8[e]);
+                  a8[e] = fmaf(h_lo(pn[e]), h_hi(w12[e]), a8[e]);
+                }
+              } else {
+#pragma unroll
+                for (int e = 0; e < 8; ++e) {
+                  a8[e] = fmaf(h_hi(pc[e]), h_lo(w01[e]), a8[e]);
+                  a8[e] = dot2h(pn[e], w12[e], a8[e]);
+                }
+              }
+            }
+            bf = relu_cvt8<DT>(a8);
+          }
+#pragma unroll
+          for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
+        }
+      }
+    } else if constexpr (G::PAIR && ABL == 0) {
       // Two vertically adjacent output rows per step (tiles qi, qi+1 = rows oy, oy+1 of the same 16 columns):
       // per tap column the 3 weights and the 4 input rows are read once and feed both rows -- 21 instead of
       // 36 ds_read_b128 per 2 x 16 pixels x 8 channels.
@@ -552,7 +764,8 @@ static hipError_t irb_go(const void* x, const void* we, const float* be, const v
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                          hipStream_t s) {
   using DW = typename DT::DW;
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW)>;
+  constexpr bool VP = irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP>;
   using T = typename DT::T;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
@@ -614,6 +827,8 @@ static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stri
 #undef SPEF_IRB_CASE
   return hipErrorNotSupported;
 }
+
+bool irb_dw_pairs(int dtype, int hid, bool expand, int stride) { return irb_vp(dtype == DT_F16, hid, expand, stride); }
 
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
   return irb_has(0, cin, hid, cout, stride, expand, res);

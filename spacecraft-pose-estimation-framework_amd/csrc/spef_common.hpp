@@ -128,6 +128,25 @@ __device__ __forceinline__ void load_dw8(const typename DT::DW* p, float w[8]) {
   }
 }
 
+// Vertical-pair depthwise (fp16): a dword holds one channel of two vertically adjacent rows (lo = upper row).
+// Two taps of a kernel column are one v_dot2_f32_f16, the third a v_fma_mix on one half (op_sel), so a 3x3 tap
+// costs 6 VALU instead of 9. Fused and unfused kernels evaluate exactly these operations in the same order.
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ float h_lo(uint32_t v) { return (float)__builtin_bit_cast(f16x2, v)[0]; }
+__device__ __forceinline__ float h_hi(uint32_t v) { return (float)__builtin_bit_cast(f16x2, v)[1]; }
+__device__ __forceinline__ float dot2h(uint32_t x, uint32_t w, float acc) {
+  return __builtin_amdgcn_fdot2(__builtin_bit_cast(f16x2, x), __builtin_bit_cast(f16x2, w), acc, false);
+}
+__device__ __forceinline__ uint32_t pack_h2(_Float16 lo, _Float16 hi) {
+  return __builtin_bit_cast(uint32_t, f16x2{lo, hi});
+}
+// ReLU + fp16 rounding of two fp32 values into one dword (v_cvt_pk_f16_f32 + v_pk_max_f16, as relu_cvt4)
+__device__ __forceinline__ uint32_t relu_pk2(float lo, float hi) {
+  const f16x2 z = {(_Float16)0.0f, (_Float16)0.0f};
+  f16x2 p = {(_Float16)lo, (_Float16)hi};
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, z));
+}
+
 template <typename DT>
 __device__ __forceinline__ typename DT::x8 zero8() {
   typename DT::x8 z;
