@@ -112,10 +112,20 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
     w, b = fold_bn(sd, arch.stem)
     ws = np.ascontiguousarray(w.transpose(2, 3, 1, 0).reshape(27, arch.stem.cout), dtype=np.float32)
     # MFMA A operand of the fused front kernel (uint8 input): ToTensor's /255 folded in float32, split
-    # hi + lo in the activation dtype, [2][32 ch][32 k] (k = 27..31 zero)
+    # hi + lo in the activation dtype, [2][32 ch][32 k]. bf16: k = ky*9 + kx*3 + ci (27..31 zero). fp16: the front
+    # kernel's Lr order (k_front.hip front_vp_kernel) -- k = 2 d + h, dword d = 3 c + ky (c < 5), half h: tap
+    # j = 2 c + h = kx*3 + ci of input row ky (j = 9 and d = 15 are zero-weight pads)
     w255 = ws / np.float32(255.0)
     hi = np.zeros((arch.stem.cout, 32), np.float32)
-    hi[:, :27] = w255.T
+    if dtype == 'fp16':
+        for k in range(30):
+            d, h = divmod(k, 2)
+            c, ky = divmod(d, 3)
+            j = 2 * c + h
+            if j < 9:
+                hi[:, k] = w255[ky * 9 + j]
+    else:
+        hi[:, :27] = w255.T
     hi_r = _round_act(hi, dtype)
     lo_r = _round_act(hi - hi_r, dtype)
     ops.append((OP_STEM, 3, arch.stem.cout, 0, 2, 1, 0,

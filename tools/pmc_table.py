@@ -33,5 +33,5 @@ for k, d in sorted(mean.items()):
     if 'SQ_INSTS_MFMA' in d and d.get('SQ_WAVES'):
         w = d['SQ_WAVES']
         print(f'   per wave: valu {d["SQ_INSTS_VALU"] / w:.0f} lds {d["SQ_INSTS_LDS"] / w:.0f} mfma {d["SQ_INSTS_MFMA"] / w:.0f} '
-              f'vmem_rd {d["SQ_INSTS_VMEM_RD"] / w:.0f} salu {d.get("SQ_INSTS_SALU", 0) / w:.0f}; '
+              f'vmem_rd {d.get("SQ_INSTS_VMEM_RD", 0) / w:.0f} salu {d.get("SQ_INSTS_SALU", 0) / w:.0f}; '
               f'bank_conflict/idx_active {d["SQ_LDS_BANK_CONFLICT"] / max(1, d["SQ_LDS_IDX_ACTIVE"]):.2f}')
