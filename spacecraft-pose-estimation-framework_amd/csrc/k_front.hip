@@ -282,8 +282,8 @@ __global__ __launch_bounds__(NW * 64) void front_vp_kernel(
   const int sy0 = oy0 - 1, sx0 = ox0 - 1;
   const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;
 
-  // ---- 1. input bytes -> In (as front_kernel), dw weight pairs, biases
-  int mis = 0;
+  // ---- 1. input bytes -> Lr (interior tiles) or In (edge tiles, as front_kernel), dw weight pairs, biases
+  const bool fast = (W & 3) == 0 && ix0 >= 0 && ix0 + IW <= W;
   {
     constexpr int RB = IW * 3;
     constexpr int DPR = (RB + 3) / 4 + 1;
@@ -292,7 +292,6 @@ __global__ __launch_bounds__(NW * 64) void front_vp_kernel(
     const uint8_t* Xb = X + (size_t)b * H * W * 3;
     const int img_bytes = H * W * 3;
     const int k = lane & 31;
-    const bool fast = (W & 3) == 0 && ix0 >= 0 && ix0 + IW <= W;
     uint32_t v[NIT];
     int a[NIT], rs[NIT];
 #pragma unroll
@@ -320,11 +319,33 @@ __global__ __launch_bounds__(NW * 64) void front_vp_kernel(
       wb = *reinterpret_cast<const uint2*>(Wd + ((ky + 1) * 3 + kx) * 32 + ch);
     }
     if (fast) {
-      mis = ((iy0 * W + ix0) * 3) & 3;
+      // interior tiles: the rows go straight to Lr. Every row starts 3 bytes into its aligned dword (W % 4 == 0,
+      // ix0 = 32 tx - 3), so lane k holds tile bytes 4k-3 .. 4k: column dword 2k-1 = its bytes 1, 2 and column
+      // dword 2k = its byte 3 + the next lane's byte 0
+      static_assert(TW == 16, "fast-path byte phase assumes 16-wide tiles");
 #pragma unroll
       for (int i = 0; i < NIT; ++i) {
         const int r = 2 * (wave + NW * i) + (lane >> 5);
-        if (r < IH && k < DPR) *reinterpret_cast<uint32_t*>(In + r * IRS + 4 * k) = v[i];
+        const uint32_t vn = __shfl_down(v[i], 1, 32);
+        if (r < IH && k < DPR) {
+          const uint32_t p0 = __builtin_amdgcn_perm(0u, v[i], 0x0c020c01u);   // [b1, 0, b2, 0]
+          const uint32_t p1 = __builtin_amdgcn_perm(vn, v[i], 0x0c040c03u);   // [b3, 0, next b0, 0]
+          f16x2 h0 = __builtin_bit_cast(f16x2, p0 | 0x64006400u), h1 = __builtin_bit_cast(f16x2, p1 | 0x64006400u);
+          h0 = h0 - f16x2{(_Float16)1024.0f, (_Float16)1024.0f};
+          h1 = h1 - f16x2{(_Float16)1024.0f, (_Float16)1024.0f};
+          const uint32_t d0 = __builtin_bit_cast(uint32_t, h0), d1 = __builtin_bit_cast(uint32_t, h1);
+          // column dwords cd = 2k-1 (d0) and 2k (d1): Lr[spy][cd][ky] for every (spy, ky) with 2 spy + ky = r
+          uint32_t* l0 = Lr + (r >> 1) * RSL + 3 * (2 * k) + (r & 1);     // (spy = r/2, ky = r%2)
+          if ((r >> 1) < SH) {
+            if (k > 0) l0[-3] = d0;
+            l0[0] = d1;
+          }
+          if (!(r & 1) && r >= 2) {                                       // (spy = r/2 - 1, ky = 2)
+            uint32_t* l2 = l0 - RSL + 2;
+            if (k > 0) l2[-3] = d0;
+            l2[0] = d1;
+          }
+        }
       }
     } else {
 #pragma unroll
@@ -363,14 +384,15 @@ __global__ __launch_bounds__(NW * 64) void front_vp_kernel(
   const bool interior = sy0 >= 0 && sx0 >= 0 && sy0 + SH <= SH_img && sx0 + SW <= SW_img;
   __syncthreads();
 
-  // ---- 2. In -> Lr: lane = column dword cd, rows r = wave + NW i; exact fp16 via 0x6400 | byte, minus 1024
+  // ---- 2. edge tiles: In -> Lr, lane = column dword cd, rows r = wave + NW i; exact fp16 via 0x6400 | byte, minus 1024
+  if (!fast) {
   if (lane < NCD) {
     const int cd = lane;
 #pragma unroll
     for (int i = 0; i < (IH + NW - 1) / NW; ++i) {
       const int r = wave + NW * i;
       if (r >= IH) break;
-      const uint8_t* src = In + r * IRS + mis + 2 * cd;
+      const uint8_t* src = In + r * IRS + 2 * cd;
       const uint32_t bv = (uint32_t)src[0] | ((uint32_t)src[1] << 16);
       f16x2 hv = __builtin_bit_cast(f16x2, bv | 0x64006400u);
       hv = hv - f16x2{(_Float16)1024.0f, (_Float16)1024.0f};
@@ -384,6 +406,7 @@ __global__ __launch_bounds__(NW * 64) void front_vp_kernel(
     }
   }
   __syncthreads();
+  }
 
   // ---- 3. stem on MFMA, units of 16 (row pair, column) positions -> pair slab Ps (ReLU, fp16; zero outside the
   // stem map = block-1 depthwise padding)
@@ -471,17 +494,18 @@ __global__ __launch_bounds__(NW * 64) void front_vp_kernel(
     f32x4 acc0 = {pb.x, pb.y, pb.z, pb.w}, acc1 = acc0;
     acc0 = DT::mfma(pa, bf0, acc0);
     acc1 = DT::mfma(pa, bf1, acc1);
+    const int gy = oy0 + oy, gx = ox0 + ox;
+    T* yr = Y + (((size_t)b * SH_img + gy) * SW_img + gx) * 16 + 4 * kg;
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const int gy = oy0 + oy + h, gx = ox0 + ox;
-      if (gy < SH_img && gx < SW_img) {
+      if (gy + h < SH_img && gx < SW_img) {
         const f32x4& ac = h ? acc1 : acc0;
         x4 out;
         out[0] = (T)ac[0];
         out[1] = (T)ac[1];
         out[2] = (T)ac[2];
         out[3] = (T)ac[3];
-        *reinterpret_cast<x4*>(Y + (((size_t)b * SH_img + gy) * SW_img + gx) * 16 + 4 * kg) = out;
+        *reinterpret_cast<x4*>(yr + (size_t)h * SW_img * 16) = out;
       }
     }
   }
