@@ -151,10 +151,11 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   };
   auto slab_load = [&](int cc) -> uint4 {
     if constexpr (VP) {
-      const int kx = vt >> 4, ky = (vt >> 3) & 1, ch = 32 * cc + 4 * (vt & 7);
+      const int kx = vt >> 4, ky = (vt >> 3) & 1;
       const bool ok = slab_ok(cc);
-      const uint2 a = *reinterpret_cast<const uint2*>(Wd + (ok ? (ky * 3 + kx) * HID + ch : 0));
-      const uint2 b = *reinterpret_cast<const uint2*>(Wd + (ok ? ((ky + 1) * 3 + kx) * HID + ch : 0));
+      const int off = ok ? (ky * 3 + kx) * HID + 4 * (vt & 7) + 32 * cc : 0;
+      const uint2 a = *reinterpret_cast<const uint2*>(Wd + off);
+      const uint2 b = *reinterpret_cast<const uint2*>(Wd + (ok ? off + 3 * HID : 0));
       return make_uint4(a.x, a.y, b.x, b.y);
     }
     const int f = tid * EPP, tap = f >> 5, ch = 32 * cc + (f & 31);
@@ -318,17 +319,21 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   constexpr int NP16 = (HID + 15) / 16 * 16;
   x8 ca0[G::KS], ca1[G::KS];
   x4 cq0 = {}, cq1 = {};
+  // (row offsets are workgroup-uniform: scalar arithmetic plus one per-lane base, no per-lane 64-bit multiplies)
+  const T* we_lane = We + r16 * WKP + (G::K16 ? 4 : 8) * kg;
   auto ew_load = [&](int cc, x4& q0_, x4& q1_, x8* a0_, x8* a1_) {
     cc = cc < G::NCH ? cc : G::NCH - 1;
     const int h1 = 32 * cc + 16 < NP16 ? 32 * cc + 16 : 32 * cc;
+    const T* p0 = we_lane + 32 * cc * WKP;
+    const T* p1 = we_lane + h1 * WKP;
     if constexpr (G::K16) {
-      q0_ = *reinterpret_cast<const x4*>(We + (size_t)(32 * cc + r16) * WKP + 4 * kg);
-      q1_ = *reinterpret_cast<const x4*>(We + (size_t)(h1 + r16) * WKP + 4 * kg);
+      q0_ = *reinterpret_cast<const x4*>(p0);
+      q1_ = *reinterpret_cast<const x4*>(p1);
     } else {
 #pragma unroll
       for (int ks = 0; ks < G::KS; ++ks) {
-        a0_[ks] = load8<DT>(We + (size_t)(32 * cc + r16) * WKP + 32 * ks + 8 * kg);
-        a1_[ks] = load8<DT>(We + (size_t)(h1 + r16) * WKP + 32 * ks + 8 * kg);
+        a0_[ks] = load8<DT>(p0 + 32 * ks);
+        a1_[ks] = load8<DT>(p1 + 32 * ks);
       }
     }
   };
@@ -529,7 +534,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     // ---- 3. depthwise 3x3 on this hidden chunk -> project B fragment in registers; 4. project MFMA
     // Tap order everywhere (here, the front kernel, the unfused dw_kernel): kx outer, ky inner -- the fused
     // and unfused schedules accumulate in the same order and stay bit-identical.
-    const bool hv = 32 * c + 8 * kg < HID;    // this lane's 8 hidden channels exist
+    // (no channel-validity branch below: channels >= HID of a partial chunk are zero in the slab, the depthwise
+    // weights and bias, so they yield ReLU(0) = +0 exactly like an explicit zero fragment)
     if constexpr (VP) {
       // Per kernel column kx: two taps by v_dot2 on a row pair, the third by v_fma_mix on one half. Output row
       // parity fixes the order: even rows (and every stride-2 row) dot2(ky 0,1) then fma(ky 2); odd rows
@@ -549,8 +555,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       if constexpr (G::PAIR) {
 #pragma unroll
         for (int qi = 0; qi < G::QPW; qi += 2) {   // output rows oy (even) and oy + 1: pairs m = oy / 2 and m + 1
-          x8 bf0 = zero8<DT>(), bf1 = zero8<DT>();
-          if (hv) {
+          x8 bf0, bf1;
+          {   // (no channel-validity branch: channels >= HID are zero in the slab, weights and bias -> ReLU(0) = 0)
             float a0[8], a1[8];
             bias8(a0);
 #pragma unroll
@@ -583,8 +589,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       } else {
 #pragma unroll
         for (int qi = 0; qi < G::QPW; ++qi) {
-          x8 bf = zero8<DT>();
-          if (hv) {
+          x8 bf;
+          {
             float a8[8];
             bias8(a8);
             // stride 2: pair m = oy (rows 2oy, 2oy+1) + low half of m + 1; stride 1 (TW = 16): the wave's row
@@ -624,8 +630,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       // 36 ds_read_b128 per 2 x 16 pixels x 8 channels.
 #pragma unroll
       for (int qi = 0; qi < G::QPW; qi += 2) {
-        x8 bf0 = zero8<DT>(), bf1 = zero8<DT>();
-        if (hv) {
+        x8 bf0, bf1;
+        {
           float a0[8], a1[8];
           {
             const float4 u0 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg);
@@ -664,8 +670,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     } else
 #pragma unroll
     for (int qi = 0; qi < G::QPW; ++qi) {
-      x8 bf = zero8<DT>();
-      if (hv) {
+      x8 bf;
+      {
         float a8[8];
         {
           const float4 u0 = *reinterpret_cast<const float4*>(Bd + 32 * c + 8 * kg);
