@@ -72,9 +72,15 @@ struct IrbGeom {
     return VP ? (PINP * xs + WE_ELEMS + WP_ELEMS) * 2 + NBUF * 4 * RS + 2 * VSLAB * 4 + BIAS * 4
               : (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 + 2 * SLAB * DWB + BIAS * 4;
   }
-  static constexpr bool WIDE = (163840 / bytes_for(CINP + 16, 48)) >= (163840 / bytes_for(CINP + 8, 40));
-  static constexpr int XS = WIDE ? CINP + 16 : CINP + 8;   // Xs row stride (elements)
-  static constexpr int ES = EXPAND ? (WIDE ? 48 : 40) : XS; // hidden-chunk row stride
+  // Xs / slab row strides: the first of (conflict-free, +16 B, unpadded Xs) that reaches the most workgroups per
+  // CU. The LDS, not the VGPRs, sets the slab kernels' occupancy (3-5 waves per SIMD), and an unpadded input tile
+  // only costs bank conflicts on the few expand B-fragment reads.
+  static constexpr int occ_for(int xs, int es) { return 163840 / bytes_for(xs, es); }
+  static constexpr int LAYOUT = occ_for(CINP + 16, 48) >= occ_for(CINP + 8, 40)
+                                    ? (occ_for(CINP + 16, 48) >= occ_for(CINP, 40) ? 0 : 2)
+                                    : (occ_for(CINP + 8, 40) >= occ_for(CINP, 40) ? 1 : 2);
+  static constexpr int XS = LAYOUT == 0 ? CINP + 16 : LAYOUT == 1 ? CINP + 8 : CINP;   // Xs row stride (elements)
+  static constexpr int ES = EXPAND ? (LAYOUT == 0 ? 48 : 40) : XS; // hidden-chunk row stride
   static constexpr int EPT = (PIN16 + NW - 1) / NW;   // expand pixel tiles per wave
   static constexpr int NCH = (HID + 31) / 32;
   static constexpr int HIDP = NCH * 32;        // project K (blob pads to 32)
