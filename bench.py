@@ -56,13 +56,14 @@ def pmc_traffic(kernel_key: str, path: str):
     if kernel_key in kernels:
         return kernels[kernel_key]['hbm_bytes_per_launch']
     import re
-    m = re.fullmatch(r'(ir[bw]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
+    m = re.fullmatch(r'(ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
     if m:   # fused block key -> the one template instantiation profiled for that geometry
         geo = ','.join(m.groups()[1:]) + ','
         hits = [v for k, v in kernels.items() if re.match(m.group(1) + r'<B?F16,' + re.escape(geo), k)]
-    else:
-        prefix = kernel_key.split('<')[0] + '<'
-        hits = [v for k, v in kernels.items() if k.startswith(prefix)]
+    else:   # e.g. front_kernel<stem+block1> -> front_kernel<...> or its fp16 form front_vp_kernel<...>
+        base = kernel_key.split('<')[0]
+        prefixes = (base + '<', base.replace('_kernel', '_vp_kernel') + '<')
+        hits = [v for k, v in kernels.items() if k.startswith(prefixes)]
     return hits[0]['hbm_bytes_per_launch'] if len(hits) == 1 else None
 
 
