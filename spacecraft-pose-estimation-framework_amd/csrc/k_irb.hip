@@ -133,6 +133,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   float* Bd = reinterpret_cast<float*>(reinterpret_cast<char*>(Sl) + (VP ? 2 * G::VSLAB * 4 : 2 * G::SLAB * (int)sizeof(DW)));
   float* Be = Bd + G::NCH * 32;                                             // [HIDP] expand bias
 
+  SPEF_TRACE(0);   // timeline probes (tools/kbench/blk_trace.hip irb): nothing in the library build
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
   uint32_t L = xcd_remap(blockIdx.x, nwg);       // neighbouring tiles (shared halo rows) on one XCD
@@ -272,7 +273,9 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     }
   }
   wst_load(1, 0);      // in flight across the first expand
+  SPEF_TRACE(1);
   __syncthreads();
+  SPEF_TRACE(2);
 
   // per-lane validity of its expand pixels (inside the tile and the image): the depthwise zero padding
   // interior tiles (whole input tile inside the image) need no padding mask in the expand epilogue
@@ -345,8 +348,10 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   };
   if constexpr (EXPAND && !STW) ew_load(0, cq0, cq1, ca0, ca1);
 
+  constexpr bool TRC = 3 * G::NCH + 3 < SPEF_TRACE_SLOTS;   // per-chunk probes only where the slots suffice
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
+    if constexpr (TRC) SPEF_TRACE(3 + 3 * c);
     const uint4 slab_next = slab_load(c + 1);      // issued now, stored after this chunk's depthwise
     const DW* sl = Sl + (c & 1) * G::SLAB;
     // project weight fragments of this chunk (no STW): issued before the expand so their latency hides under it
@@ -529,7 +534,9 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       Es = Xs;
     }
     wst_store(c + 1, c);      // expand weights of chunk c+1, project weights of chunk c
+    if constexpr (TRC) SPEF_TRACE(4 + 3 * c);
     if constexpr (ABL != 5) __syncthreads();
+    if constexpr (TRC) SPEF_TRACE(5 + 3 * c);
     wst_load(c + 2, c + 1);   // next stage in flight across this depthwise/project and the next expand
     if constexpr (STW) {
       const T* wpp = WPs + (c & 1) * G::NCTP * G::WPS + (wc * G::NCTW * 16 + r16) * G::WPS + 8 * kg;
@@ -733,6 +740,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       *reinterpret_cast<x4*>(yr + co) = o;
     }
   }
+  SPEF_TRACE(SPEF_TRACE_SLOTS - 1);
 }
 
 // ------------------------------------------------------------------------------------------ dispatch

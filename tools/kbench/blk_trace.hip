@@ -1,13 +1,14 @@
-// Timeline harness for the role-split block kernels (csrc/k_irw.hip, csrc/k_irp.hip): times one geometry with HIP events and
+// Timeline harness for the fused block kernels (csrc/k_irb.hip, k_irw.hip, k_irp.hip): times one geometry with HIP events and
 // records every wave's s_memtime at the SPEF_TRACE probes of one launch, then prints where a workgroup's time goes
 // (prologue, per-chunk work and barrier wait per role, epilogue, launch ramp). Not part of the library.
 //
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -fno-honor-nans -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form \
 //     -I include -I spacecraft-pose-estimation-framework_amd/csrc tools/kbench/blk_trace.hip -o tools/kbench/blk_trace
-//   ./tools/kbench/blk_trace irw|irp CIN HID COUT STRIDE RES H W [B=64] [variant=0] [iters=50] [xscale=2]
+//   ./tools/kbench/blk_trace irb|irw|irp CIN HID COUT STRIDE RES H W [B=64] [variant=0] [iters=50] [xscale=2]
 #ifndef SPEF_KBENCH_TIMING_ONLY   // -DSPEF_KBENCH_TIMING_ONLY: same harness, probes compiled out (timing only)
 #define SPEF_KTRACE
 #endif
+#include "k_irb.hip"
 #include "k_irp.hip"
 #include "k_irw.hip"
 
@@ -49,10 +50,11 @@ static float* dev_random_f32(size_t n, float scale, unsigned seed) {
 
 int main(int argc, char** argv) {
   if (argc < 9) {
-    fprintf(stderr, "usage: %s irw|irp CIN HID COUT STRIDE RES H W [B] [variant] [iters] [xscale]\n", argv[0]);
+    fprintf(stderr, "usage: %s irb|irw|irp CIN HID COUT STRIDE RES H W [B] [variant] [iters] [xscale]\n", argv[0]);
     return 2;
   }
-  const bool irp = argv[1][2] == 'p';
+  const bool irp = argv[1][2] == 'p', irb = argv[1][2] == 'b';
+  const char* kname = irb ? "irb" : irp ? "irp" : "irw";
   ++argv;
   --argc;
   const int cin = atoi(argv[1]), hid = atoi(argv[2]), cout = atoi(argv[3]), st = atoi(argv[4]);
@@ -86,8 +88,11 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreate(&s));
   auto go = [&]() {
-    CK((irp ? launch_irp : launch_irw)(variant, DT_F16, cin, hid, cout, st, res, x, we, be, wd, bd, wp, bp, y, B, H, W,
-                                        OH, OW, s));
+    if (irb)
+      CK(launch_irb(variant, DT_F16, cin, hid, cout, st, true, res, x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s));
+    else
+      CK((irp ? launch_irp : launch_irw)(variant, DT_F16, cin, hid, cout, st, res, x, we, be, wd, bd, wp, bp, y, B, H,
+                                          W, OH, OW, s));
   };
   for (int i = 0; i < 5; ++i) go();
   hipEvent_t e0, e1;
@@ -102,7 +107,7 @@ int main(int argc, char** argv) {
   const double us = 1e3 * ms / iters;
 
 #ifndef SPEF_KTRACE
-  printf("%s avg launch %.2f us (%d iters, no probes)\n", irp ? "irp" : "irw", us, iters);
+  printf("%s avg launch %.2f us (%d iters, no probes)\n", kname, us, iters);
   return 0;
 #endif
   CK(hipMemset(tr, 0, tn * 8));
@@ -132,7 +137,7 @@ int main(int argc, char** argv) {
     }
   }
   const int nch = (hid + 31) / 32;
-  printf("%s geometry %d->%d->%d s%d res%d %dx%d B=%d variant %d: %d workgroups x %d waves, %d chunks\n", irp ? "irp" : "irw", cin, hid, cout,
+  printf("%s geometry %d->%d->%d s%d res%d %dx%d B=%d variant %d: %d workgroups x %d waves, %d chunks\n", kname, cin, hid, cout,
          st, (int)res, H, W, B, variant, nwg, nwaves, nch);
   printf("avg launch %.2f us (%d iters, probes compiled in); traced launch %.2f us\n", us, iters, 1e3 * ms);
   double wall = 0;
@@ -145,6 +150,27 @@ int main(int argc, char** argv) {
     wall += m;
   }
   printf("workgroup lifetime (max over its waves): %.0f cycles avg\n", wall / nwg);
+  if (irb) {   // slots: 0 start, 1 prologue done, 2 after first barrier, per chunk c: 3+3c start, 4+3c expand done,
+               // 5+3c after the chunk barrier (depthwise + project run to the next chunk's start), last = end
+    printf("wave  prologue  firstbar  per chunk: expand  barrier  dw+project   epilogue\n");
+    for (int v = 0; v < nwaves; ++v) {
+      double pro = 0, b0 = 0, ex = 0, ba = 0, dw = 0, epi = 0;
+      for (int g = 0; g < nwg; ++g) {
+        const unsigned long long* r = &h[((size_t)g * 16 + v) * SPEF_TRACE_SLOTS];
+        pro += D(r[0], r[1]);
+        b0 += D(r[1], r[2]);
+        for (int c = 0; c < nch; ++c) {
+          ex += D(r[3 + 3 * c], r[4 + 3 * c]);
+          ba += D(r[4 + 3 * c], r[5 + 3 * c]);
+          dw += D(r[5 + 3 * c], c + 1 < nch ? r[6 + 3 * c] : r[SPEF_TRACE_SLOTS - 1]);
+        }
+        epi += 0;
+      }
+      const double n = (double)nwg * nch;
+      printf("%4d  %8.0f  %8.0f  %17.0f  %7.0f  %10.0f\n", v, pro / nwg, b0 / nwg, ex / n, ba / n, dw / n);
+    }
+    return 0;
+  }
   printf("wave  prologue  firstbar  expand0  chunk-work  chunk-barrier  (per chunk: work  barrier)  epilogue\n");
   for (int v = 0; v < nwaves; ++v) {
     double pro = 0, sync0 = 0, w0 = 0, work = 0, wait = 0, epi = 0;
