@@ -226,55 +226,6 @@ __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restric
   *reinterpret_cast<typename DT::x8*>(Y + (((int64_t)b * OH + oy) * OW + ox) * C + c) = o;
 }
 
-// Depthwise on MFMA (the fused slab kernel's irb_dw_mode 2, k_irb.hip): one wave = 16 consecutive output pixels x
-// 16 channels; five v_mfma_f32_16x16x32_f16 with block-diagonal weight fragments (k slot 8 kg + e = tap
-// 2 s + (kg >> 1), channel 8 (kg & 1) + e; tap 9 a zero-weight pad reading tap 8's pixel) onto the bias -- the same
-// fragments, operands and order as the fused kernel, so the two schedules are bit-identical.
-template <int S>
-__global__ __launch_bounds__(256) void dw_mfma_kernel(const _Float16* __restrict__ X, const _Float16* __restrict__ W9,
-                                                      const float* __restrict__ bias, _Float16* __restrict__ Y, int B,
-                                                      int H, int W, int C, int OH, int OW) {
-  typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63, r16 = lane & 15, kg = lane >> 4;
-  const int64_t npx = (int64_t)B * OH * OW;
-  const int cgroups = C >> 4;
-  const int64_t wid = (int64_t)blockIdx.x * 4 + wave;
-  const int cg = (int)(wid % cgroups);
-  const int64_t pt = wid / cgroups;
-  if (pt * 16 >= npx) return;   // wave-uniform
-  const int64_t p = pt * 16 + r16;
-  const bool pv = p < npx;
-  const int64_t pc = pv ? p : npx - 1;
-  const int ox = (int)(pc % OW), oy = (int)((pc / OW) % OH), b = (int)(pc / ((int64_t)OW * OH));
-  const int c0 = 16 * cg;
-  const int e = r16 & 7;
-  const bool act = (r16 >> 3) == (kg & 1);
-  const uint32_t hm = (e & 1) ? 0xffff0000u : 0x0000ffffu;
-  uint32_t m[4];
-#pragma unroll
-  for (int j = 0; j < 4; ++j) m[j] = (act && j == (e >> 1)) ? hm : 0u;
-  const float4 bb = *reinterpret_cast<const float4*>(bias + c0 + 4 * kg);
-  f32x4 acc = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-  for (int s5 = 0; s5 < 5; ++s5) {
-    const int tr = 2 * s5 + (kg >> 1), t = tr < 9 ? tr : 8;
-    uint32_t w = *reinterpret_cast<const uint32_t*>(W9 + t * C + c0 + (r16 & ~1));
-    if (tr == 9) w = 0;
-    const f16x8 af = __builtin_bit_cast(f16x8, u32x4{w & m[0], w & m[1], w & m[2], w & m[3]});
-    const int iy = oy * S - 1 + t / 3, ix = ox * S - 1 + t % 3;
-    f16x8 bx = {};
-    if (iy >= 0 && iy < H && ix >= 0 && ix < W)
-      bx = *reinterpret_cast<const f16x8*>(X + (((int64_t)b * H + iy) * W + ix) * C + c0 + 8 * (kg & 1));
-    acc = F16::mfma(af, bx, acc);
-  }
-  if (pv) {
-    uint2 o;
-    o.x = relu_pk2(acc[0], acc[1]);
-    o.y = relu_pk2(acc[2], acc[3]);
-    *reinterpret_cast<uint2*>(Y + p * C + c0 + 4 * kg) = o;
-  }
-}
-
 // ------------------------------------------------------------------------------------------ last conv + mean
 // grid (Np / (16*NT), B). The 4 waves split the image's pixel tiles; ReLU(conv + bias) is summed over
 // pixels in fp32 registers (the 1280-channel map is never stored), reduced over the 16 pixel lanes by
@@ -413,20 +364,9 @@ hipError_t launch_pw(int dtype, int epi, const void* x, const void* wt, const fl
 }
 
 hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias, void* y, int B, int H, int W, int C,
-                     int stride, int OH, int OW, int mode, hipStream_t s) {
+                     int stride, int OH, int OW, bool pairs, hipStream_t s) {
   if (C & 7) return hipErrorInvalidValue;
-  if (mode && dtype != DT_F16) return hipErrorInvalidValue;
-  if (mode == 2) {
-    if (C & 15) return hipErrorInvalidValue;
-    const int64_t waves = ((int64_t)B * OH * OW + 15) / 16 * (C / 16);
-    const unsigned gm = (unsigned)((waves + 3) / 4);
-    if (stride == 1)
-      dw_mfma_kernel<1><<<gm, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
-    else
-      dw_mfma_kernel<2><<<gm, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
-    return hipGetLastError();
-  }
-  const bool pairs = mode == 1;
+  if (pairs && dtype != DT_F16) return hipErrorInvalidValue;
   const unsigned g = blocks_for((int64_t)B * OH * OW * (C / 8), 256);
   if (pairs) {
     if (stride == 1)

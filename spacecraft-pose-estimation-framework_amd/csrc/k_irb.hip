@@ -29,15 +29,6 @@ namespace spef {
 // (irb_dw_pairs), so both schedules stay bit-identical. (Stride 2 measured slower: a 3-row window straddles two
 // pairs, so every output row reads 1.5x the slab bytes, and the odd input-tile height wastes half a pair row.)
 constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) { return f16 && expand && hid <= 192 && stride == 1; }
-// MFMA depthwise (MD, fp16 stride-2 blocks 2, 4, 7): per 16 pixels x 16 channels, five v_mfma_f32_16x16x32_f16
-// with block-diagonal weight fragments -- k slot 8 kg + e of lane group kg is tap t = 2 s + (kg >> 1) (t = 9 a
-// zero-weight pad), channel 8 (kg & 1) + e -- accumulating onto the bias. The MFMA's 4-channel output layout is
-// transposed into the project operand's 8-channel layout by two lane swaps (v_permlane32_swap, v_permlane16_swap).
-// dw_mfma_kernel (k_conv.hip) runs the same MFMAs (irb_dw_mode 2), so fused == unfused stays bit-identical.
-// Measured: blocks 2, 4, 7 -1.5 % to -3 % against the scalar depthwise; on the stride-1 blocks 3, 5-6 it was +10-13 %
-// against VP (the MFMAs issue through the same port as the VALU work they replace, and each hidden chunk needs
-// ~40 VALU to build its ten fragments), so those keep the vertical pairs.
-constexpr bool irb_md(bool f16, int hid, bool expand, int stride) { return f16 && expand && hid <= 192 && stride == 2; }
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
           bool STW, int DWB = 4, bool VP = false>
@@ -125,8 +116,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
     int tiles_y, uint32_t nwg) {
   using DW = typename DT::DW;
-  constexpr bool MD = irb_md(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
-  constexpr bool VP = !MD && irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
+  constexpr bool VP = irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
   using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
@@ -358,24 +348,6 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   };
   if constexpr (EXPAND && !STW) ew_load(0, cq0, cq1, ca0, ca1);
 
-  // MD lane constants: lane (r16, kg) of a weight fragment is row (channel) r16; its only nonzero slot is
-  // e = r16 & 7 in lane groups with (kg & 1) == (r16 >> 3), i.e. dword e >> 1, half e & 1 of the fragment
-  uint32_t mdm[4] = {0, 0, 0, 0};   // per-dword masks (s < 4); s == 4 zeroes tap 9 (kg >> 1 == 1)
-  int mdt[5] = {0, 0, 0, 0, 0};     // tap of slot group s (9 -> 8: a valid address, zero weight)
-  int mdo[5] = {0, 0, 0, 0, 0};     // B-fragment offset (halves) of that tap from the pixel of tap (0, 0)
-  if constexpr (MD) {
-    const int e = r16 & 7;
-    const bool act = (r16 >> 3) == (kg & 1);
-    const uint32_t hm = (e & 1) ? 0xffff0000u : 0x0000ffffu;
-#pragma unroll
-    for (int j = 0; j < 4; ++j) mdm[j] = (act && j == (e >> 1)) ? hm : 0u;
-#pragma unroll
-    for (int s5 = 0; s5 < 5; ++s5) {
-      const int t = 2 * s5 + (kg >> 1) < 9 ? 2 * s5 + (kg >> 1) : 8;
-      mdt[s5] = t;
-      mdo[s5] = ((t / 3) * G::IW + t % 3) * G::ES + 8 * (kg & 1);
-    }
-  }
   constexpr bool TRC = 3 * G::NCH + 3 < SPEF_TRACE_SLOTS;   // per-chunk probes only where the slots suffice
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
@@ -577,46 +549,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     // and unfused schedules accumulate in the same order and stay bit-identical.
     // (no channel-validity branch below: channels >= HID of a partial chunk are zero in the slab, the depthwise
     // weights and bias, so they yield ReLU(0) = +0 exactly like an explicit zero fragment)
-    if constexpr (MD) {
-      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-      const bool z4 = (kg >> 1) != 0;   // slot group 4, lane groups 2-3: tap 9 (zero weight)
-      x8 af[2][5];                      // block-diagonal weight fragments of this chunk, channel groups g = 0, 1
-#pragma unroll
-      for (int g = 0; g < 2; ++g)
-#pragma unroll
-        for (int s5 = 0; s5 < 5; ++s5) {
-          uint32_t w = *reinterpret_cast<const uint32_t*>(sl + mdt[s5] * 32 + 16 * g + (r16 & ~1));
-          if (s5 == 4 && z4) w = 0;
-          af[g][s5] = __builtin_bit_cast(x8, u32x4{w & mdm[0], w & mdm[1], w & mdm[2], w & mdm[3]});
-        }
-      const float4 bb0 = *reinterpret_cast<const float4*>(Bd + 32 * c + 4 * kg);
-      const float4 bb1 = *reinterpret_cast<const float4*>(Bd + 32 * c + 16 + 4 * kg);
-#pragma unroll
-      for (int qi = 0; qi < G::QPW; ++qi) {
-        const T* pb = Es + ((oyq[qi] * S) * G::IW + oxq[qi] * S) * G::ES;
-        f32x4 d0 = {bb0.x, bb0.y, bb0.z, bb0.w}, d1 = {bb1.x, bb1.y, bb1.z, bb1.w};   // bias as MFMA C
-#pragma unroll
-        for (int s5 = 0; s5 < 5; ++s5) {
-          const x8 b0 = *reinterpret_cast<const x8*>(pb + mdo[s5]);
-          const x8 b1 = *reinterpret_cast<const x8*>(pb + mdo[s5] + 16);
-          d0 = DT::mfma(af[0][s5], b0, d0);
-          d1 = DT::mfma(af[1][s5], b1, d1);
-        }
-        // ReLU + fp16 (lane: channels 4kg..4kg+3 of groups 0 and 1), then lane swaps -> channels 8kg..8kg+7
-        uint32_t g0a = relu_pk2(d0[0], d0[1]), g0b = relu_pk2(d0[2], d0[3]);
-        uint32_t g1a = relu_pk2(d1[0], d1[1]), g1b = relu_pk2(d1[2], d1[3]);
-        {
-          auto ra = __builtin_amdgcn_permlane32_swap(g0a, g1a, false, false);
-          auto rb = __builtin_amdgcn_permlane32_swap(g0b, g1b, false, false);
-          auto sa = __builtin_amdgcn_permlane16_swap(ra[0], ra[1], false, false);
-          auto sb = __builtin_amdgcn_permlane16_swap(rb[0], rb[1], false, false);
-          g0a = sa[0]; g1a = sa[1]; g0b = sb[0]; g1b = sb[1];
-        }
-        const x8 bf = __builtin_bit_cast(x8, u32x4{g0a, g0b, g1a, g1b});
-#pragma unroll
-        for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
-      }
-    } else if constexpr (VP) {
+    if constexpr (VP) {
       // Per kernel column kx: two taps by v_dot2 on a row pair, the third by v_fma_mix on one half. Output row
       // parity fixes the order: even rows (and every stride-2 row) dot2(ky 0,1) then fma(ky 2); odd rows
       // fma(ky 0) then dot2(ky 1,2) -- exactly dw_kernel<.., VP>'s order.
@@ -851,8 +784,7 @@ static hipError_t irb_go(const void* x, const void* we, const float* be, const v
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                          hipStream_t s) {
   using DW = typename DT::DW;
-  constexpr bool MD = irb_md(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
-  constexpr bool VP = !MD && irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
+  constexpr bool VP = irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
   using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP>;
   using T = typename DT::T;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
@@ -916,9 +848,7 @@ static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stri
   return hipErrorNotSupported;
 }
 
-int irb_dw_mode(int dtype, int hid, bool expand, int stride) {
-  return irb_md(dtype == DT_F16, hid, expand, stride) ? 2 : irb_vp(dtype == DT_F16, hid, expand, stride) ? 1 : 0;
-}
+bool irb_dw_pairs(int dtype, int hid, bool expand, int stride) { return irb_vp(dtype == DT_F16, hid, expand, stride); }
 
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
   return irb_has(0, cin, hid, cout, stride, expand, res);
