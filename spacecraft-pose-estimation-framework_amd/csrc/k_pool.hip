@@ -9,24 +9,35 @@
 #include <type_traits>
 #include "spef_kernels.hpp"
 
+// Pixel tile of the K = 320 instantiation: MT 16-pixel tiles per wave, NWM pixel waves (2 channel waves each).
+// Measured at B = 64 (tools/ab.py): (MT, NWM) = (4, 4) 33.1 us, (2, 4) 30.9, (2, 2) 31.7-32.2 -- the kernel is bound
+// by its per-K-step LDS round trip and barrier, not by occupancy (1, 2 or 3 workgroups per CU).
+#ifndef SPEF_POOL_MT
+#define SPEF_POOL_MT 2
+#endif
+#ifndef SPEF_POOL_NWM
+#define SPEF_POOL_NWM 4
+#endif
+
 namespace spef {
 
 // KSC > 0: the K step count is a compile-time constant (K = 32 * KSC, the URSONet last conv has K = 320) and the K loop
 // is fully unrolled, which lets the compiler track the two register stages' outstanding loads exactly.
-template <typename DT, int KSC>
-__global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __restrict__ X,
+template <typename DT, int KSC, int MT = 4, int NWM = 4>
+__global__ __launch_bounds__(2 * NWM * 64) void pool_gemm_kernel(const typename DT::T* __restrict__ X,
                                                         const typename DT::T* __restrict__ Wt,
                                                         const float* __restrict__ bias, float* __restrict__ pooled,
                                                         int HW, int K, int Kp, int N) {
   using T = typename DT::T;
   using x8 = typename DT::x8;
-  constexpr int NT = 4, MT = 4;                 // wave tile: 64 channels x 64 pixels
-  constexpr int BN = 2 * 16 * NT, BM = 4 * 16 * MT;   // 128 x 256
+  constexpr int NT = 4;                         // wave tile: 64 channels x 16 MT pixels
+  constexpr int NTHR = 2 * NWM * 64;            // 2 channel waves x NWM pixel waves
+  constexpr int BN = 2 * 16 * NT, BM = NWM * 16 * MT;
   constexpr int RS = 48;                        // LDS row stride (96 B: conflict-free b128)
-  constexpr int XP = BM * 4 / 512, WP = BN * 4 / 512; // 16-B pieces per thread per K step
+  constexpr int XP = (BM * 4 + NTHR - 1) / NTHR, WP = (BN * 4 + NTHR - 1) / NTHR; // 16-B pieces per thread per K step
   __shared__ __attribute__((aligned(16))) T As[2][BN * RS];
   __shared__ __attribute__((aligned(16))) T Bs[2][BM * RS];
-  __shared__ float red[4][BN];
+  __shared__ float red[NWM][BN];
 
   // XCD-aware order: the channel blocks of one image run on one XCD, so its 320-channel map is fetched from
   // HBM once into that XCD's L2 instead of once per XCD (blocks are dealt round-robin over the 8 XCDs).
@@ -39,12 +50,6 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
   const T* Xb = X + (size_t)b * HW * K;
   const int KS = KSC > 0 ? KSC : Kp >> 5;
 
-  f32x4 bias4[NT];
-#pragma unroll
-  for (int a = 0; a < NT; ++a) {
-    const float4 t = *reinterpret_cast<const float4*>(bias + n0 + (wn * NT + a) * 16 + 4 * kg);
-    bias4[a] = f32x4{t.x, t.y, t.z, t.w};
-  }
   f32x4 sum[NT];
 #pragma unroll
   for (int a = 0; a < NT; ++a) sum[a] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -56,19 +61,19 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
   x8 xr[2][XP], wr[2][WP];
   for (int m0 = 0; m0 < HW; m0 += BM) {
     auto xok = [&](int i, int ks) {
-      const int p = tid + 512 * i, row = p >> 2, g = p & 3;
-      return m0 + row < HW && ks * 32 + 8 * g < K;
+      const int p = tid + NTHR * i, row = p >> 2, g = p & 3;
+      return row < BM && m0 + row < HW && ks * 32 + 8 * g < K;
     };
     auto gload = [&](int ks, auto stc) {
       constexpr int st = decltype(stc)::value;
 #pragma unroll
       for (int i = 0; i < XP; ++i) {
-        const int p = tid + 512 * i, row = p >> 2, g = p & 3, k = ks * 32 + 8 * g;
+        const int p = tid + NTHR * i, row = p >> 2, g = p & 3, k = ks * 32 + 8 * g;
         xr[st][i] = load8<DT>(Xb + (xok(i, ks) ? (size_t)(m0 + row) * K + k : 0));
       }
 #pragma unroll
       for (int i = 0; i < WP; ++i) {
-        const int p = tid + 512 * i, row = p >> 2, g = p & 3;
+        const int p = tid + NTHR * i, row = (p >> 2) < BN ? p >> 2 : 0, g = p & 3;
         wr[st][i] = load8<DT>(Wt + (size_t)(n0 + row) * Kp + ks * 32 + 8 * g);
       }
     };
@@ -76,20 +81,28 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
       constexpr int st = decltype(stc)::value;
 #pragma unroll
       for (int i = 0; i < XP; ++i) {
-        const int p = tid + 512 * i;
-        *reinterpret_cast<x8*>(&Bs[buf][(p >> 2) * RS + 8 * (p & 3)]) = xok(i, ks) ? xr[st][i] : zero8<DT>();
+        const int p = tid + NTHR * i;
+        if (BM * 4 % NTHR == 0 || (p >> 2) < BM)
+          *reinterpret_cast<x8*>(&Bs[buf][(p >> 2) * RS + 8 * (p & 3)]) = xok(i, ks) ? xr[st][i] : zero8<DT>();
       }
 #pragma unroll
       for (int i = 0; i < WP; ++i) {
-        const int p = tid + 512 * i;
-        *reinterpret_cast<x8*>(&As[buf][(p >> 2) * RS + 8 * (p & 3)]) = wr[st][i];
+        const int p = tid + NTHR * i;
+        if (BN * 4 % NTHR == 0 || (p >> 2) < BN)
+          *reinterpret_cast<x8*>(&As[buf][(p >> 2) * RS + 8 * (p & 3)]) = wr[st][i];
       }
     };
-    f32x4 acc[NT][MT];
+    f32x4 acc[NT][MT];   // bias as the MFMA C operand (re-read per pixel chunk: no registers held across chunks)
+    {
+      const float* bt = bias;
+      asm volatile("" : "+s"(bt));
 #pragma unroll
-    for (int a = 0; a < NT; ++a)
+      for (int a = 0; a < NT; ++a) {
+        const float4 t = *reinterpret_cast<const float4*>(bt + n0 + (wn * NT + a) * 16 + 4 * kg);
 #pragma unroll
-      for (int q = 0; q < MT; ++q) acc[a][q] = bias4[a];
+        for (int q = 0; q < MT; ++q) acc[a][q] = f32x4{t.x, t.y, t.z, t.w};
+      }
+    }
     __syncthreads();   // previous chunk's LDS reads done
     gload(0, std::integral_constant<int, 0>());
     if (KS > 1) gload(1, std::integral_constant<int, 1>());
@@ -132,7 +145,7 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
         for (int e = 0; e < 4; ++e) sum[a][e] += pv ? fmaxf(acc[a][q][e], 0.f) : 0.f;
     }
   }
-  // reduce over the 16 pixel lanes, then over the 4 pixel waves
+  // reduce over the 16 pixel lanes, then over the NWM pixel waves
 #pragma unroll
   for (int a = 0; a < NT; ++a)
 #pragma unroll
@@ -146,7 +159,9 @@ __global__ __launch_bounds__(512) void pool_gemm_kernel(const typename DT::T* __
     }
   __syncthreads();
   if (tid < BN && n0 + tid < N) {
-    const float v = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    float v;
+    if constexpr (NWM == 4) v = (red[0][tid] + red[1][tid]) + (red[2][tid] + red[3][tid]);
+    else v = red[0][tid] + red[1][tid];
     pooled[(size_t)b * N + n0 + tid] = v / (float)HW;
   }
 }
@@ -158,7 +173,7 @@ hipError_t launch_pool_gemm(int dtype, const void* x, const void* wt, const floa
   dim3 g(Np / 128, B);
   if (dtype == DT_F16) {
     if (Kp == 320)
-      pool_gemm_kernel<F16, 10><<<g, 512, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
+      pool_gemm_kernel<F16, 10, SPEF_POOL_MT, SPEF_POOL_NWM><<<g, 2 * SPEF_POOL_NWM * 64, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
     else
       pool_gemm_kernel<F16, 0><<<g, 512, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
   } else {
