@@ -20,8 +20,25 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+def _demangle_spef(full: str) -> str:
+    """Mangled symbols the profiler left as-is, e.g. '_ZN4spef15front_vp_kernelILi16ELi16ELi8EEEv...' ->
+    'front_vp_kernel<16,16,8>' (integer and bool template arguments only; anything else is returned unchanged)."""
+    m = re.match(r'_ZN4spef(\d+)', full)
+    if not m:
+        return full
+    ln = int(m.group(1))
+    name = full[m.end():m.end() + ln]
+    rest = full[m.end() + ln:]
+    if not rest.startswith('I'):
+        return name
+    args = re.findall(r'L[ib](\d+)E', rest[1:rest.find('EEE') + 1] if 'EEE' in rest else rest[1:])
+    return f"{name}<{','.join(args)}>"
+
+
 def short_name(full: str) -> str:
     """'void spef::pw_kernel<spef::F16, 6, 2, 1>(...)' -> 'pw_kernel<F16,6,2,1>' (bench.py key form)."""
+    if full.startswith('_Z'):
+        full = _demangle_spef(full)
     n = full.replace('(anonymous namespace)::', '').split('(')[0].replace('void ', '').replace('spef::', '').strip()
     n = re.sub(r'\s+', '', n)
     n = n.replace('stem_kernel<F16,0>', 'stem_kernel<u8>').replace('stem_kernel<F16,1>', 'stem_kernel<f32>')
