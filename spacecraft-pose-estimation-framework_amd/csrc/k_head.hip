@@ -110,20 +110,34 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, const float* __
 }
 
 // ------------------------------------------------------------------------------------------ reductions
-__device__ __forceinline__ float block_max256(float v, float* sh) {
-  v = warp_max(v);
-  __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  return fmaxf(fmaxf(sh[0], sh[1]), fmaxf(sh[2], sh[3]));
+// Workgroup (4 waves) max / sum of one float per thread: within a 16-lane row by DPP (quad swaps, half-row and row
+// mirrors: every lane ends with its row's value, no LDS round trip), the 4 rows by readlane, the 4 waves through
+// LDS with one barrier. sh[4] must not be reused by the caller. A fixed combination order: deterministic.
+template <bool MAX>
+__device__ __forceinline__ float dpp_op(float a, float b) { return MAX ? fmaxf(a, b) : a + b; }
+template <bool MAX, int CTRL>
+__device__ __forceinline__ float dpp_step(float v) {
+  const float o = __builtin_bit_cast(float, __builtin_amdgcn_mov_dpp(__builtin_bit_cast(int, v), CTRL, 0xf, 0xf, false));
+  return dpp_op<MAX>(v, o);
 }
-__device__ __forceinline__ float block_sum256(float v, float* sh) {
-  v = warp_sum(v);
+template <bool MAX>
+__device__ __forceinline__ float block_reduce256(float v, float* sh) {
+  v = dpp_step<MAX, 0xB1>(v);    // quad_perm [1,0,3,2]
+  v = dpp_step<MAX, 0x4E>(v);    // quad_perm [2,3,0,1]
+  v = dpp_step<MAX, 0x141>(v);   // row_half_mirror
+  v = dpp_step<MAX, 0x140>(v);   // row_mirror
+  const int u = __builtin_bit_cast(int, v);
+  const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(u, 0));
+  const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(u, 16));
+  const float r2 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(u, 32));
+  const float r3 = __builtin_bit_cast(float, __builtin_amdgcn_readlane(u, 48));
+  const float w = dpp_op<MAX>(dpp_op<MAX>(r0, r1), dpp_op<MAX>(r2, r3));
+  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = w;
   __syncthreads();
-  if ((threadIdx.x & 63) == 0) sh[threadIdx.x >> 6] = v;
-  __syncthreads();
-  return (sh[0] + sh[1]) + (sh[2] + sh[3]);
+  return dpp_op<MAX>(dpp_op<MAX>(sh[0], sh[1]), dpp_op<MAX>(sh[2], sh[3]));
 }
+__device__ __forceinline__ float block_max256(float v, float* sh) { return block_reduce256<true>(v, sh); }
+__device__ __forceinline__ float block_sum256(float v, float* sh) { return block_reduce256<false>(v, sh); }
 
 // Top eigenvector of the symmetric PSD 4x4 a (fp64, packed upper triangle t) by repeated squaring: each step
 // M <- M^2 multiplies the eigenvalue ratios (l_i / l_1) by themselves, so after k steps M is l_1-dominated to
@@ -193,6 +207,7 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
   __shared__ double shd[10][256];
   __shared__ double shp[10][16];
   const int tid = threadIdx.x, b = blockIdx.x;
+  SPEF_TRACE(0);   // timeline probes (tools/kbench/head_bench.hip trace): nothing in the library build
   const float* x = logits + (size_t)b * n;
   float v[PER];
 #pragma unroll
@@ -200,10 +215,23 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
     const int i = tid + 256 * j;
     v[j] = i < n ? x[i] : -INFINITY;
   }
+  // the bin quaternions are loaded with the logits (PER <= 8: 64 VGPRs), not after the softmax: in the network the
+  // forward has evicted them, and that second dependent HBM round trip was 40 % of the kernel (head_bench trace)
+  constexpr bool PF = PER <= 8;
+  double4 qv[PF ? PER : 1];
+  if constexpr (PF) {
+#pragma unroll
+    for (int j = 0; j < PER; ++j) {
+      const int i = tid + 256 * j;
+      qv[j] = *reinterpret_cast<const double4*>(qb + 4 * (i < n ? i : 0));
+    }
+  }
   float m = v[0];
 #pragma unroll
   for (int j = 1; j < PER; ++j) m = fmaxf(m, v[j]);
+  SPEF_TRACE(1);
   m = block_max256(m, shf[0]);
+  SPEF_TRACE(2);
   float s = 0.0f;
 #pragma unroll
   for (int j = 0; j < PER; ++j) {
@@ -211,6 +239,7 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
     s += v[j];
   }
   s = block_sum256(s, shf[1]);
+  SPEF_TRACE(3);
   double mom[10];
 #pragma unroll
   for (int k = 0; k < 10; ++k) mom[k] = 0.0;
@@ -221,15 +250,19 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
       const float p = v[j] / s;
       if (soft) soft[(size_t)b * n + i] = p;
       const double pd = (double)p;
-      const double4 q = *reinterpret_cast<const double4*>(qb + 4 * i);
+      double4 q;
+      if constexpr (PF) q = qv[j];
+      else q = *reinterpret_cast<const double4*>(qb + 4 * i);
       mom[0] += (q.x * q.x) * pd; mom[1] += (q.x * q.y) * pd; mom[2] += (q.x * q.z) * pd; mom[3] += (q.x * q.w) * pd;
       mom[4] += (q.y * q.y) * pd; mom[5] += (q.y * q.z) * pd; mom[6] += (q.y * q.w) * pd;
       mom[7] += (q.z * q.z) * pd; mom[8] += (q.z * q.w) * pd; mom[9] += (q.w * q.w) * pd;
     }
   }
+  SPEF_TRACE(4);
 #pragma unroll
   for (int k = 0; k < 10; ++k) shd[k][tid] = mom[k];
   __syncthreads();
+  SPEF_TRACE(5);
   if (tid < 160) {
     const int k = tid >> 4, j = tid & 15;
     double a = 0.0;
@@ -238,6 +271,7 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
     shp[k][j] = a;
   }
   __syncthreads();
+  SPEF_TRACE(6);
   if (tid >= 16) return;
   double t[10];
   if (tid < 10) {
@@ -262,25 +296,27 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
     return;
   }
   double q[4];
+  SPEF_TRACE(7);
   sym4_top_eigvec(t, q);
   for (int k = 0; k < 4; ++k) quat[4 * b + k] = (float)q[k];
+  SPEF_TRACE(8);
 }
 
 // ------------------------------------------------------------------------------------------ decode pos
 __global__ __launch_bounds__(256) void decode_pos_kernel(const float* __restrict__ logits, int n,
                                                          const double* __restrict__ grid, float* __restrict__ soft,
                                                          float* __restrict__ pos, int* __restrict__ status) {
-  __shared__ float shf[4];
+  __shared__ float shf[2][4];
   __shared__ double shd[4][3];
   __shared__ float shp[4];
   const int b = blockIdx.x;
   const float* x = logits + (size_t)b * n;
   float m = -INFINITY;
   for (int i = threadIdx.x; i < n; i += 256) m = fmaxf(m, x[i]);
-  m = block_max256(m, shf);
+  m = block_max256(m, shf[0]);
   float s = 0.0f;
   for (int i = threadIdx.x; i < n; i += 256) s += expf(x[i] - m);
-  s = block_sum256(s, shf);
+  s = block_sum256(s, shf[1]);
   double acc[3] = {0.0, 0.0, 0.0};
   float ps = 0.0f;
   for (int i = threadIdx.x; i < n; i += 256) {

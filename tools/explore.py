@@ -42,7 +42,13 @@ def run(eng, fr, ori, pos, opts, steps=10, label=''):
 def main():
     B, S = int(os.environ.get('B', 64)), int(os.environ.get('S', 512))
     sd = synthetic_state_dict(mobilenet_v2(), seed=1001)
-    eng = Engine(Bl.pack(sd, dtype='fp16'), 'cuda:0')
+    if os.environ.get('DT') == 'int8':   # the C5 path: calibrated int8 blob (bench.py run_int8)
+        from spef_amd.blob_q8 import pack_int8
+        from spef_amd.data.synthetic import synth_frames
+        from spef_amd.quant import calibrate
+        eng = Engine(pack_int8(sd, calibrate(sd, synth_frames(4, 128, 128, 900))), 'cuda:0')
+    else:
+        eng = Engine(Bl.pack(sd, dtype='fp16'), 'cuda:0')
     rng = np.random.Generator(np.random.PCG64(0))
     fr = torch.from_numpy(rng.integers(0, 256, (B, S, S, 3), dtype=np.uint8)).cuda()
     ori = torch.empty((B, 1728), device='cuda')

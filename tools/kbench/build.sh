@@ -8,4 +8,6 @@ F="-O3 -std=c++17 --offload-arch=gfx950 -fno-honor-nans -fno-slp-vectorize -mllv
 /opt/rocm/bin/hipcc $F tools/kbench/blk_trace.hip -o tools/kbench/blk_trace &
 /opt/rocm/bin/hipcc $F -DSPEF_KBENCH_TIMING_ONLY tools/kbench/blk_trace.hip -o tools/kbench/blk_bench &
 wait
-/opt/rocm/bin/hipcc ${F/-fno-honor-nans /} tools/kbench/head_bench.hip -o tools/kbench/head_bench
+/opt/rocm/bin/hipcc ${F/-fno-honor-nans /} tools/kbench/head_bench.hip -o tools/kbench/head_bench &
+/opt/rocm/bin/hipcc ${F/-fno-honor-nans /} -DSPEF_KTRACE tools/kbench/head_bench.hip -o tools/kbench/head_trace &
+wait

@@ -2,6 +2,7 @@
 // the orientation decode (softmax + Markley average) over B images. Not part of the library.
 //
 //   tools/kbench/build.sh; ./tools/kbench/head_bench [B=64] [iters=200]
+//   ./tools/kbench/head_trace [B=64]: the same, plus the decode_ori SPEF_TRACE timeline of one launch
 #include "k_head.hip"
 
 #include <cmath>
@@ -69,9 +70,62 @@ int main(int argc, char** argv) {
   CK(hipMemset(status, 0, B * 4));
   hipStream_t s;
   CK(hipStreamCreate(&s));
+  const size_t kFlush = (size_t)512 << 20;   // > the 256 MB MALL: evicts every cache level
+  void* flush;
+  CK(hipMalloc(&flush, kFlush));
+#ifdef SPEF_KTRACE
+  // the probe buffer is set before the first launch of the traced kernel (a null spef_ktrace faults)
+  unsigned long long* tr;
+  const size_t nt = (size_t)B * 16 * SPEF_TRACE_SLOTS;
+  CK(hipMalloc(&tr, nt * 8));
+  CK(hipMemset(tr, 0, nt * 8));
+  CK(hipMemcpyToSymbol(HIP_SYMBOL(spef::spef_ktrace), &tr, sizeof(tr)));
+#endif
   const double t_fc = time_us(s, iters, [&] { CK(launch_fc(x, w, bias, o0, n0, o1, n1, B, K, s)); });
   const double t_dec =
       time_us(s, iters, [&] { CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, s)); });
+#ifdef SPEF_KTRACE
+  {   // one traced launch after an L2 flush (as in the network, where the forward evicts the bins): per workgroup
+      // (wave 0), the s_memtime deltas between consecutive probes
+    constexpr int NS = 9;
+    CK(hipMemsetAsync(flush, 1, kFlush, s));
+    CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, s));
+    CK(hipStreamSynchronize(s));
+    std::vector<unsigned long long> h(nt);
+    CK(hipMemcpy(h.data(), tr, nt * 8, hipMemcpyDeviceToHost));
+    double acc[NS] = {0}, mx[NS] = {0};
+    for (int b = 0; b < B; ++b) {
+      const unsigned long long* w0 = &h[(size_t)b * 16 * SPEF_TRACE_SLOTS];
+      for (int k = 1; k < NS; ++k) {
+        const double d = (double)(w0[k] - w0[k - 1]);
+        acc[k] += d / B;
+        mx[k] = d > mx[k] ? d : mx[k];
+      }
+    }
+    const char* nm[NS] = {"", "load+local max", "max reduce", "exp+sum reduce", "moments", "LDS write+barrier",
+                          "16x16 reduce+barrier", "10-lane reduce", "eigvec"};
+    printf("decode_ori timeline (s_memtime ticks, wave 0; mean / max over %d workgroups):\n", B);
+    for (int k = 1; k < NS; ++k) printf("  %-22s %8.0f %8.0f\n", nm[k], acc[k], mx[k]);
+  }
+#endif
+  {   // cold: every decode after an L2/MALL flush, events around the decode only
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    double tot = 0;
+    const int n = 20;
+    for (int i = 0; i < n; ++i) {
+      CK(hipMemsetAsync(flush, i & 0xff, kFlush, s));
+      CK(hipEventRecord(e0, s));
+      CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, s));
+      CK(hipEventRecord(e1, s));
+      CK(hipEventSynchronize(e1));
+      float ms;
+      CK(hipEventElapsedTime(&ms, e0, e1));
+      tot += ms;
+    }
+    printf("decode_ori_kernel after a cache flush: %.2f us (events around one launch, mean of %d)\n", tot / n * 1e3, n);
+  }
   std::vector<float> hq4((size_t)B * 4);
   CK(hipMemcpy(hq4.data(), quat, hq4.size() * 4, hipMemcpyDeviceToHost));
   printf("B=%d: fc_kernel %.2f us (%.1f GB/s of weights+inputs), decode_ori_kernel %.2f us; quat[0] = %.5f %.5f %.5f %.5f\n",
