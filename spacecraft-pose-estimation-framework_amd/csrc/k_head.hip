@@ -144,16 +144,28 @@ __device__ __forceinline__ float block_sum256(float v, float* sh) { return block
 // (l_2 / l_1)^(2^k); M is rescaled by a power of two each step (exact, no division) and the loop stops when M is
 // rank one to fp64 precision (tr(M^2) = tr(M)^2), at most 40 steps. The eigenvector is M's column of largest
 // diagonal entry, polished by two power steps with a. Replaces np.linalg.eig (classification_utils.py:137-141):
-// ~7 squarings (<= 11 on every golden/random/near-uniform case, equal to numpy's eigenvector in float32), a short
-// dependent chain of independent FMAs where cyclic Jacobi spent ~20 us of fp64 divides and square roots on one lane.
+// <= 8 squarings after the Gershgorin shift below (<= 11 without it on every golden/random/near-uniform case; equal to
+// numpy's eigenvector in float32), a short dependent chain of independent FMAs where cyclic Jacobi spent ~20 us of
+// fp64 divides and square roots on one lane.
 __device__ void sym4_top_eigvec(const double t[10], double out[4]) {
   // packed upper triangle: 0:00 1:01 2:02 3:03 4:11 5:12 6:13 7:22 8:23 9:33
   double m[10];
   {
-    int e;
-    frexp((t[0] + t[4]) + (t[7] + t[9]), &e);
+    // shift by (just under) the Gershgorin lower bound g <= l_4 of a: the eigenvectors stay, every shifted
+    // eigenvalue stays >= 0 and the ratio (l_2 - g) / (l_1 - g) < l_2 / l_1 -- near-flat softmaxes (a ~ I/4, the
+    // slow case) converge in ~7 squarings instead of ~10; peaked ones have g <= 0 and keep sigma = 0
+    const double g0 = t[0] - (fabs(t[1]) + fabs(t[2]) + fabs(t[3]));
+    const double g1 = t[4] - (fabs(t[1]) + fabs(t[5]) + fabs(t[6]));
+    const double g2 = t[7] - (fabs(t[2]) + fabs(t[5]) + fabs(t[8]));
+    const double g3 = t[9] - (fabs(t[3]) + fabs(t[6]) + fabs(t[8]));
+    const double sg = fmax(0.0, fmin(fmin(g0, g1), fmin(g2, g3))) * (1.0 - 0x1p-10);
 #pragma unroll
-    for (int k = 0; k < 10; ++k) m[k] = ldexp(t[k], -e);
+    for (int k = 0; k < 10; ++k) m[k] = t[k];
+    m[0] -= sg; m[4] -= sg; m[7] -= sg; m[9] -= sg;
+    int e;
+    frexp((m[0] + m[4]) + (m[7] + m[9]), &e);
+#pragma unroll
+    for (int k = 0; k < 10; ++k) m[k] = ldexp(m[k], -e);
   }
   for (int it = 0; it < 40; ++it) {
     const double m00 = m[0], m01 = m[1], m02 = m[2], m03 = m[3], m11 = m[4], m12 = m[5], m13 = m[6], m22 = m[7],
