@@ -136,6 +136,13 @@ __device__ __forceinline__ float block_reduce256(float v, float* sh) {
   __syncthreads();
   return dpp_op<MAX>(dpp_op<MAX>(sh[0], sh[1]), dpp_op<MAX>(sh[2], sh[3]));
 }
+template <int CTRL>
+__device__ __forceinline__ double dpp_add_d(double v) {   // v + (v of the DPP source lane), fp64 as two dword moves
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xf, 0xf, false);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xf, 0xf, false);
+  return v + __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ float block_max256(float v, float* sh) { return block_reduce256<true>(v, sh); }
 __device__ __forceinline__ float block_sum256(float v, float* sh) { return block_reduce256<false>(v, sh); }
 
@@ -210,7 +217,8 @@ __device__ void sym4_top_eigvec(const double t[10], double out[4]) {
 // ------------------------------------------------------------------------------------------ decode ori
 // One 256-thread workgroup per image; the image's logits stay in registers (PER per thread, n <= 256 PER) from one
 // global read. Softmax in float32 as SPEUtils.last_activ; the ten fp64 moments of a = sum_i p_i q_i q_i^T are
-// reduced through LDS (each of 160 threads sums 16 interleaved partials, ten threads sum those: a fixed order).
+// reduced through LDS (each of 160 threads sums 16 interleaved partials, each 16-lane row sums those by DPP: a fixed
+// order).
 template <int PER>
 __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict__ logits, int n,
                                                          const double* __restrict__ qb, float* __restrict__ soft,
@@ -275,31 +283,25 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
   for (int k = 0; k < 10; ++k) shd[k][tid] = mom[k];
   __syncthreads();
   SPEF_TRACE(5);
-  if (tid < 160) {
+  if (tid < 160) {   // 16-lane row k sums moment k: 16 partials per lane, then the row by DPP
     const int k = tid >> 4, j = tid & 15;
     double a = 0.0;
 #pragma unroll
     for (int r = 0; r < 16; ++r) a += shd[k][j + 16 * r];
-    shp[k][j] = a;
+    a = dpp_add_d<0xB1>(a);    // quad_perm [1,0,3,2]
+    a = dpp_add_d<0x4E>(a);    // quad_perm [2,3,0,1]
+    a = dpp_add_d<0x141>(a);   // row_half_mirror
+    a = dpp_add_d<0x140>(a);   // row_mirror
+    if (j == 0) shp[k][0] = a;
   }
   __syncthreads();
   SPEF_TRACE(6);
-  if (tid >= 16) return;
-  double t[10];
-  if (tid < 10) {
-    double a = 0.0;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) a += shp[tid][r];
-    shd[tid][0] = a;
-  }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-  __builtin_amdgcn_wave_barrier();
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
   if (tid != 0) return;
+  double t[10];
   bool nan = false;
 #pragma unroll
   for (int k = 0; k < 10; ++k) {
-    t[k] = shd[k][0];
+    t[k] = shp[k][0];
     nan |= isnan(t[k]);
   }
   if (nan) {  // classification_utils.py:134-135
