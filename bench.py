@@ -274,14 +274,14 @@ def main():
     ap.add_argument('--cpu-batch', type=int, default=64)
     ap.add_argument('--traffic', default=None,
                     help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic (default: '
-                         'profiles/r02b_pmc_traffic.json, r01_int8_pmc_traffic.json for --dtype int8)')
+                         'profiles/r02c_pmc_traffic.json, r01_int8_pmc_traffic.json for --dtype int8)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU + gloo: the distributed control flow (weight distribution, timing, max over ranks, '
                          'JSON) without device work')
     args = ap.parse_args()
     if args.traffic is None:   # the newest committed FETCH/WRITE summary of this path
-        names = ['r01_int8_pmc_traffic.json'] if args.dtype == 'int8' else ['r02b_pmc_traffic.json',
-                                                                             'r02_pmc_traffic.json']
+        names = (['r01_int8_pmc_traffic.json'] if args.dtype == 'int8' else
+                 ['r02c_pmc_traffic.json', 'r02b_pmc_traffic.json', 'r02_pmc_traffic.json'])
         paths = [os.path.join(ROOT, 'profiles', n) for n in names]
         args.traffic = next((p for p in paths if os.path.exists(p)), paths[-1])
 
