@@ -129,6 +129,29 @@ def test_decode_orientation_planted(engine, golden):
         assert err.max() < 1e-3, (T, err.max())
 
 
+@pytest.mark.parametrize('scale', [0.0, 1e-4, 1e-2])
+def test_decode_orientation_flat_softmax(engine, scale):
+    """Flat and near-flat softmaxes (the random-weight bench regime and the degenerate limit): the moment matrix is
+    close to I/4, where the decode's repeated squaring is slowest and its Gershgorin shift (k_head.hip) matters.
+    The eigenvector there is ill-conditioned, so instead of comparing against numpy's choice the test checks the
+    property the decode must satisfy: a finite unit quaternion whose Rayleigh quotient is the top eigenvalue of
+    a = sum_i p_i q_i q_i^T (classification_utils.py:137-141)."""
+    h, _ = D.orientation_histogram(12, False)
+    engine.set_decode_tables(h, None)
+    rng = np.random.Generator(np.random.PCG64(11))
+    lg = (scale * rng.standard_normal((8, h.shape[0]))).astype(np.float32)
+    out = engine.decode(1, 0, torch.from_numpy(lg).cuda(), torch.zeros((8, 3), device='cuda'))
+    q = out['ori'].cpu().numpy().astype(np.float64)
+    assert np.isfinite(q).all() and not out['status'].cpu().numpy().any()
+    np.testing.assert_allclose(np.linalg.norm(q, axis=1), 1.0, atol=1e-6)
+    p = D.softmax_f32(lg).astype(np.float64)
+    hb = np.asarray(h, np.float64)
+    for b in range(8):
+        a = (hb * p[b][:, None]).T @ hb
+        lam = np.linalg.eigvalsh(a)
+        assert q[b] @ a @ q[b] >= lam[-1] - 1e-6 * (lam[-1] - lam[0] + 1e-12) - 1e-7, (scale, b)
+
+
 def test_decode_position_classification(engine, golden):
     g = golden('decode_pos.npz')
     engine.set_decode_tables(None, g['grid'])
