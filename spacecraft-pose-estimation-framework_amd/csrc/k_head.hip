@@ -219,15 +219,19 @@ __device__ void sym4_top_eigvec(const double t[10], double out[4]) {
 // global read. Softmax in float32 as SPEUtils.last_activ; the ten fp64 moments of a = sum_i p_i q_i q_i^T are
 // reduced through LDS (each of 160 threads sums 16 interleaved partials, each 16-lane row sums those by DPP: a fixed
 // order).
+// It also writes the image's whole status word (the decode's first kernel: no memset launch) and, in position
+// regression mode, copies the 3 raw position outputs (no copy launch): pos_src == nullptr skips the copy.
 template <int PER>
 __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict__ logits, int n,
                                                          const double* __restrict__ qb, float* __restrict__ soft,
-                                                         float* __restrict__ quat, int* __restrict__ status) {
+                                                         float* __restrict__ quat, int* __restrict__ status,
+                                                         const float* __restrict__ pos_src, float* __restrict__ pos) {
   __shared__ float shf[2][4];
   __shared__ double shd[10][256];
   __shared__ double shp[10][16];
   const int tid = threadIdx.x, b = blockIdx.x;
   SPEF_TRACE(0);   // timeline probes (tools/kbench/head_bench.hip trace): nothing in the library build
+  if (pos_src && tid < 3) pos[3 * b + tid] = pos_src[3 * b + tid];
   const float* x = logits + (size_t)b * n;
   float v[PER];
 #pragma unroll
@@ -304,8 +308,8 @@ __global__ __launch_bounds__(256) void decode_ori_kernel(const float* __restrict
     t[k] = shp[k][0];
     nan |= isnan(t[k]);
   }
+  status[b] = nan ? 1 : 0;
   if (nan) {  // classification_utils.py:134-135
-    status[b] |= 1;
     for (int k = 0; k < 4; ++k) quat[4 * b + k] = NAN;
     return;
   }
@@ -359,9 +363,14 @@ __global__ __launch_bounds__(256) void decode_pos_kernel(const float* __restrict
   }
 }
 
-__global__ void normalize_ori_kernel(const float* __restrict__ raw, int B, float* __restrict__ quat) {
+__global__ void normalize_ori_kernel(const float* __restrict__ raw, int B, float* __restrict__ quat,
+                                     int* __restrict__ status, const float* __restrict__ pos_src,
+                                     float* __restrict__ pos) {
   const int b = blockIdx.x * 256 + threadIdx.x;
   if (b >= B) return;
+  status[b] = 0;   // as decode_ori_kernel: the decode's first kernel owns the status word and the position copy
+  if (pos_src)
+    for (int k = 0; k < 3; ++k) pos[3 * b + k] = pos_src[3 * b + k];
   const float4 q = *reinterpret_cast<const float4*>(raw + 4 * b);
   const float n = sqrtf(q.x * q.x + q.y * q.y + q.z * q.z + q.w * q.w);
   *reinterpret_cast<float4*>(quat + 4 * b) = make_float4(q.x / n, q.y / n, q.z / n, q.w / n);
@@ -393,18 +402,19 @@ hipError_t launch_fc_splitk(const float* x, const float* w, const float* bias, f
 }
 
 hipError_t launch_decode_ori(const float* logits, int B, int n_bins, const double* q_bins, float* soft, float* quat,
-                             int* status, hipStream_t s) {
+                             int* status, const float* pos_src, float* pos, hipStream_t s) {
   if (n_bins <= 256 * 8)
-    decode_ori_kernel<8><<<B, 256, 0, s>>>(logits, n_bins, q_bins, soft, quat, status);
+    decode_ori_kernel<8><<<B, 256, 0, s>>>(logits, n_bins, q_bins, soft, quat, status, pos_src, pos);
   else if (n_bins <= 256 * 32)
-    decode_ori_kernel<32><<<B, 256, 0, s>>>(logits, n_bins, q_bins, soft, quat, status);
+    decode_ori_kernel<32><<<B, 256, 0, s>>>(logits, n_bins, q_bins, soft, quat, status, pos_src, pos);
   else
     return hipErrorInvalidValue;   // more than 8192 orientation bins (20^3 = 8000 is the largest cubic grid)
   return hipGetLastError();
 }
 
-hipError_t launch_normalize_ori(const float* raw, int B, float* quat, hipStream_t s) {
-  normalize_ori_kernel<<<(B + 255) / 256, 256, 0, s>>>(raw, B, quat);
+hipError_t launch_normalize_ori(const float* raw, int B, float* quat, int* status, const float* pos_src, float* pos,
+                                hipStream_t s) {
+  normalize_ori_kernel<<<(B + 255) / 256, 256, 0, s>>>(raw, B, quat, status, pos_src, pos);
   return hipGetLastError();
 }
 

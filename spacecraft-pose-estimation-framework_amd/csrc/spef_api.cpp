@@ -1097,28 +1097,29 @@ int spef_decode(spef_ctx* c, int ori_mode, int pos_mode, const float* ori_raw, i
     return fail(SPEF_ERR_ARG, "position logits are " + std::to_string(n_pos) + " wide, the grid has " +
                                   std::to_string(c->n_pos_bins) + " bins");
   if (pos_mode == SPEF_REGRESSION && n_pos != 3) return fail(SPEF_ERR_ARG, "position regression needs 3 outputs");
+  if (ori_mode != SPEF_CLASSIFICATION && ori_mode != SPEF_REGRESSION)
+    return fail(SPEF_ERR_ARG, "ori_mode must be regression or classification");
+  if (pos_mode != SPEF_CLASSIFICATION && pos_mode != SPEF_REGRESSION)
+    return fail(SPEF_ERR_ARG, "pos_mode must be regression or classification");
+  if (ori_mode == SPEF_CLASSIFICATION && !c->d_ori_bins)
+    return fail(SPEF_ERR_STATE, "orientation bins not set (spef_set_decode_tables)");
+  if (pos_mode == SPEF_CLASSIFICATION && !c->d_pos_grid)
+    return fail(SPEF_ERR_STATE, "position grid not set (spef_set_decode_tables)");
   Dev d(c->device);
   hipStream_t s = (hipStream_t)stream;
-  HIP_TRY(hipMemsetAsync(status, 0, sizeof(int) * B, s));
+  // the orientation kernel runs first: it writes every status word and, in position regression mode, copies the
+  // raw position (no memset / copy launches); the position decode then ORs its bits in, in stream order
+  const float* pos_src = (pos_mode == SPEF_REGRESSION && pos != pos_raw) ? pos_raw : nullptr;
   if (ori_mode == SPEF_CLASSIFICATION) {
-    if (!c->d_ori_bins) return fail(SPEF_ERR_STATE, "orientation bins not set (spef_set_decode_tables)");
     HIP_TRY(prof_launch(c, s, "decode_ori_kernel", (double)B * c->n_ori_bins * (ori_soft ? 8 : 4) + 32.0 * c->n_ori_bins,
                         (double)B * c->n_ori_bins * 30, [&] {
-      return launch_decode_ori(ori_raw, B, c->n_ori_bins, c->d_ori_bins, ori_soft, quat, status, s);
+      return launch_decode_ori(ori_raw, B, c->n_ori_bins, c->d_ori_bins, ori_soft, quat, status, pos_src, pos, s);
     }));
-  } else if (ori_mode == SPEF_REGRESSION) {
-    HIP_TRY(launch_normalize_ori(ori_raw, B, quat, s));
   } else {
-    return fail(SPEF_ERR_ARG, "ori_mode must be regression or classification");
+    HIP_TRY(launch_normalize_ori(ori_raw, B, quat, status, pos_src, pos, s));
   }
-  if (pos_mode == SPEF_CLASSIFICATION) {
-    if (!c->d_pos_grid) return fail(SPEF_ERR_STATE, "position grid not set (spef_set_decode_tables)");
+  if (pos_mode == SPEF_CLASSIFICATION)
     HIP_TRY(launch_decode_pos(pos_raw, B, c->n_pos_bins, c->d_pos_grid, pos_soft, pos, status, s));
-  } else if (pos_mode == SPEF_REGRESSION) {
-    if (pos != pos_raw) HIP_TRY(hipMemcpyAsync(pos, pos_raw, sizeof(float) * 3 * B, hipMemcpyDeviceToDevice, s));
-  } else {
-    return fail(SPEF_ERR_ARG, "pos_mode must be regression or classification");
-  }
   return SPEF_OK;
 }
 

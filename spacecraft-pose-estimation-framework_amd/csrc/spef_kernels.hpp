@@ -89,9 +89,11 @@ hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStrea
 
 // Decode (src/spe/spe_utils.py:56-101): ori softmax + Markley average; pos softmax + soft-argmax.
 // status[b] |= 1 (NaN orientation moments), 2 (pos zero sum), 4 (NaN position).
+// The orientation kernels write status[b] (=, not |=) and copy pos_src -> pos when pos_src is not null.
 hipError_t launch_decode_ori(const float* logits, int B, int n_bins, const double* q_bins, float* soft,
-                             float* quat, int* status, hipStream_t s);
-hipError_t launch_normalize_ori(const float* raw, int B, float* quat, hipStream_t s);
+                             float* quat, int* status, const float* pos_src, float* pos, hipStream_t s);
+hipError_t launch_normalize_ori(const float* raw, int B, float* quat, int* status, const float* pos_src, float* pos,
+                                hipStream_t s);
 hipError_t launch_decode_pos(const float* logits, int B, int n_bins, const double* grid, float* soft,
                              float* pos, int* status, hipStream_t s);
 

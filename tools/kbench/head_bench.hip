@@ -83,13 +83,13 @@ int main(int argc, char** argv) {
 #endif
   const double t_fc = time_us(s, iters, [&] { CK(launch_fc(x, w, bias, o0, n0, o1, n1, B, K, s)); });
   const double t_dec =
-      time_us(s, iters, [&] { CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, s)); });
+      time_us(s, iters, [&] { CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, nullptr, nullptr, s)); });
 #ifdef SPEF_KTRACE
   {   // one traced launch after an L2 flush (as in the network, where the forward evicts the bins): per workgroup
       // (wave 0), the s_memtime deltas between consecutive probes
     constexpr int NS = 9;
     CK(hipMemsetAsync(flush, 1, kFlush, s));
-    CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, s));
+    CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, nullptr, nullptr, s));
     CK(hipStreamSynchronize(s));
     std::vector<unsigned long long> h(nt);
     CK(hipMemcpy(h.data(), tr, nt * 8, hipMemcpyDeviceToHost));
@@ -117,7 +117,7 @@ int main(int argc, char** argv) {
     for (int i = 0; i < n; ++i) {
       CK(hipMemsetAsync(flush, i & 0xff, kFlush, s));
       CK(hipEventRecord(e0, s));
-      CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, s));
+      CK(launch_decode_ori(o0, B, n0, bins, soft, quat, status, nullptr, nullptr, s));
       CK(hipEventRecord(e1, s));
       CK(hipEventSynchronize(e1));
       float ms;
