@@ -28,10 +28,18 @@ struct RQ16 {
 
 // The packer guarantees S >= 32 for fused blocks (blob_q8.py), so (acc * M + B) >> S is the high word of the
 // 64-bit v_mad_i64_i32 result shifted by S - 32: three VALU ops with the clamp (v_med3_i32).
+// clamp to [lo, hi] (lo <= hi) as one v_med3_i32: the compiler only forms med3 from min(max()) with constant bounds,
+// and the quantizer tops here are kernel arguments (two VALU ops per requantised value otherwise)
+__device__ __forceinline__ int med3i(int x, int lo, int hi) {
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+  return r;
+}
+
 __device__ __forceinline__ int rq_apply(int acc, const RQ16& r, int lo, int hi) {
   const int64_t t = (int64_t)acc * r.M + r.B;
   const int v = (int)(t >> 32) >> (r.S - 32);
-  return min(max(v, lo), hi);   // v_med3_i32
+  return med3i(v, lo, hi);
 }
 
 // A requant record held in registers for a whole chunk, with the shift already reduced to S - 32. SH32 (blob flag 4:
@@ -60,10 +68,10 @@ constexpr uint32_t kF16Bias2 = 0x64006400u;   // two fp16 1024.0
 template <bool SH32>
 __device__ __forceinline__ uint32_t expand_pair(const RQR<SH32>& r0, int a0, const RQR<SH32>& r1, int a1, int eh) {
   if constexpr (SH32) {   // the offset carries + 0x6400: clamp to [0x6400, 0x6400 + eh], two low halves -> one v_perm_b32
-    const int v0 = min(max(r0.hi(a0), 0x6400), 0x6400 + eh), v1 = min(max(r1.hi(a1), 0x6400), 0x6400 + eh);
+    const int v0 = med3i(r0.hi(a0), 0x6400, 0x6400 + eh), v1 = med3i(r1.hi(a1), 0x6400, 0x6400 + eh);
     return __builtin_amdgcn_perm((uint32_t)v1, (uint32_t)v0, 0x05040100u);
   } else {
-    const int v0 = min(max(r0.hi(a0), 0), eh), v1 = min(max(r1.hi(a1), 0), eh);
+    const int v0 = med3i(r0.hi(a0), 0, eh), v1 = med3i(r1.hi(a1), 0, eh);
     return ((uint32_t)v1 << 16) | (uint32_t)v0 | kF16Bias2;
   }
 }
@@ -314,7 +322,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
         if constexpr (SH32) {
           int q[8];
 #pragma unroll
-          for (int e = 0; e < 8; ++e) q[e] = min(max(rd[e].hi((int)a8[e]), -128), dh - 128);
+          for (int e = 0; e < 8; ++e) q[e] = med3i(rd[e].hi((int)a8[e]), -128, dh - 128);
           const uint32_t p01 = __builtin_amdgcn_perm((uint32_t)q[1], (uint32_t)q[0], 0x0c0c0400u);
           const uint32_t p23 = __builtin_amdgcn_perm((uint32_t)q[3], (uint32_t)q[2], 0x0c0c0400u);
           const uint32_t p45 = __builtin_amdgcn_perm((uint32_t)q[5], (uint32_t)q[4], 0x0c0c0400u);
@@ -326,7 +334,7 @@ __global__ __launch_bounds__(NW * 64) void q_irb_kernel(
           hi = 0;
 #pragma unroll
           for (int e = 0; e < 8; ++e) {
-            const uint32_t q = (uint32_t)min(max(rd[e].hi((int)a8[e]), 0), dh);
+            const uint32_t q = (uint32_t)med3i(rd[e].hi((int)a8[e]), 0, dh);
             if (e < 4) lo |= q << (8 * e);
             else hi |= q << (8 * (e - 4));
           }
