@@ -31,6 +31,13 @@ __device__ __forceinline__ int requant(int acc, int64_t M, int64_t B, int S, int
   return (int)(v < lo ? lo : (v > hi ? hi : v));
 }
 
+// clamp to [lo, hi] (lo <= hi) as one v_med3_i32 (the compiler forms med3 only for constant bounds)
+__device__ __forceinline__ int q_med3(int x, int lo, int hi) {
+  int r;
+  asm("v_med3_i32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(lo), "v"(hi));
+  return r;
+}
+
 // ------------------------------------------------------------------------------------------------ stem
 // Input QuantIdentity + QConvBnAct 3->32 3x3/s2 (mobilenet_v2.py:177-182).
 // A workgroup owns a 4 x 64 output tile. Its 9 x 129 input
@@ -40,6 +47,7 @@ __device__ __forceinline__ int requant(int acc, int64_t M, int64_t B, int S, int
 // per thread instead of 27 per pixel. Requant: the high word of one v_mad_i64_i32 shifted by S - 32 when every channel's
 // S >= 32 and |M| < 2^31 (workgroup-uniform check), the 64-bit form otherwise.
 constexpr int kStemTH = 4, kStemTW = 64, kStemIH = 2 * kStemTH + 1, kStemIW = 2 * kStemTW + 1;
+
 template <bool F32IN>
 __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict__ in, const int8_t* __restrict__ lut,
                                                           float s_img, int in_lo, int in_hi,
@@ -204,7 +212,7 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
         int v;
         if (fast) {
           v = (int)(((int64_t)acc * (int)Mr[e] + Br[e]) >> 32) >> (Sr[e] - 32);
-          v = min(max(v, 0), rq.hi);
+          v = q_med3(v, 0, rq.hi);
         } else {
           v = requant(acc, Mr[e], Br[e], Sr[e], 0, rq.hi);
         }
