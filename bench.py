@@ -218,6 +218,12 @@ def kernel_table(prof, steps):
             for k, v in sorted(prof.items(), key=lambda kv: -kv[1][1])}
 
 
+def newest_profile(names):
+    """The first of the committed profiles/ summaries (newest first) that exists; the last name otherwise."""
+    paths = [os.path.join(ROOT, 'profiles', n) for n in names]
+    return next((p for p in paths if os.path.exists(p)), paths[-1])
+
+
 def run_int8(args, sd, dev, frames, ref):
     """C5 sub-record: the INT8 (Brevitas-mirroring) path at the same workload, same timing protocol (N=1)."""
     import torch
@@ -244,8 +250,8 @@ def run_int8(args, sd, dev, frames, ref):
     prof = eng.profile_end()
     rec = {'workload': f'C5: INT8 (Brevitas-mirroring, PTQ-calibrated scales) full net + decode, {S}x{S}, batch {B}',
            'value': round(B * args.steps / el, 2), 'unit': 'images/sec', 'ms_per_step': round(el / args.steps * 1e3, 4),
-           'dtype': 'int8', 'roofline_kernel': roofline(prof, args.steps, B, os.path.join(
-               ROOT, 'profiles', 'r01_int8_pmc_traffic.json'))}
+           'dtype': 'int8', 'roofline_kernel': roofline(prof, args.steps, B, newest_profile(
+               ['r02_int8_pmc_traffic.json', 'r01_int8_pmc_traffic.json']))}
     rec['roofline_kernel']['peak'] = 2 * MFMA_PEAK_TFLOPS
     rec['roofline_kernel']['unit'] = 'TOP/s'
     rec['roofline_kernel']['frac'] = round(rec['roofline_kernel']['achieved'] / (2 * MFMA_PEAK_TFLOPS), 4)
@@ -274,16 +280,15 @@ def main():
     ap.add_argument('--cpu-batch', type=int, default=64)
     ap.add_argument('--traffic', default=None,
                     help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic (default: '
-                         'profiles/r02c_pmc_traffic.json, r01_int8_pmc_traffic.json for --dtype int8)')
+                         'profiles/r02d_pmc_traffic.json, r02_int8_pmc_traffic.json for --dtype int8)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU + gloo: the distributed control flow (weight distribution, timing, max over ranks, '
                          'JSON) without device work')
     args = ap.parse_args()
     if args.traffic is None:   # the newest committed FETCH/WRITE summary of this path
-        names = (['r01_int8_pmc_traffic.json'] if args.dtype == 'int8' else
-                 ['r02c_pmc_traffic.json', 'r02b_pmc_traffic.json', 'r02_pmc_traffic.json'])
-        paths = [os.path.join(ROOT, 'profiles', n) for n in names]
-        args.traffic = next((p for p in paths if os.path.exists(p)), paths[-1])
+        args.traffic = newest_profile(
+            ['r02_int8_pmc_traffic.json', 'r01_int8_pmc_traffic.json'] if args.dtype == 'int8' else
+            ['r02d_pmc_traffic.json', 'r02c_pmc_traffic.json', 'r02b_pmc_traffic.json', 'r02_pmc_traffic.json'])
 
     import torch
     import torch.distributed as dist
