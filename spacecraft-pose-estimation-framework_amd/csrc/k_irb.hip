@@ -23,12 +23,14 @@
 
 namespace spef {
 
-// Vertical-pair depthwise (VP, fp16 stride-1 blocks 3, 5, 6): the hidden slab holds, per position (row pair pr,
+// Vertical-pair depthwise (VP, fp16 stride-1 blocks 3, 5, 6, 8-13): the hidden slab holds, per position (row pair pr,
 // column), one dword per channel = (row 2pr, row 2pr+1) -- the depthwise takes two taps of a kernel column with one
 // v_dot2_f32_f16 and the third with one v_fma_mix. The unfused dw_kernel uses the same order for these blocks
 // (irb_dw_pairs), so both schedules stay bit-identical. (Stride 2 measured slower: a 3-row window straddles two
 // pairs, so every output row reads 1.5x the slab bytes, and the odd input-tile height wastes half a pair row.)
-constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) { return f16 && expand && hid <= 192 && stride == 1; }
+// Blocks 8-13 (hid 384, 576) run the same pair order in the role-split kernel (k_irw.hip); their slab-kernel variants
+// follow it so every schedule of those blocks stays bit-identical.
+constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) { return f16 && expand && hid <= 576 && stride == 1; }
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
           bool STW, int DWB = 4, bool VP = false>

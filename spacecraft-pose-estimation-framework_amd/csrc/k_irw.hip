@@ -22,7 +22,14 @@
 
 namespace spef {
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, int NE, int ND, int WCO, int DWB>
+// Vertical-pair depthwise (fp16, stride 1, 16-wide tiles; blocks 8-13): the hidden slab holds, per (row pair, column)
+// position, one dword per channel = (row 2m, row 2m+1), in four 8-channel regions (k_irb.hip's VP layout); a kernel
+// column's taps ky 0,1 (or 1,2) are one v_dot2_f32_f16 and the third one v_fma_mix: 6 instead of 9 VALU per 3x3
+// tap set. The depthwise weights are staged once as (w[0][kx], w[1][kx]) / (w[1][kx], w[2][kx]) pairs. The unfused
+// dw_kernel (irb_dw_pairs) evaluates the same instructions in the same order: bit-identical.
+constexpr bool irw_vp(bool f16, int s, int th, int tw) { return f16 && s == 1 && tw == 16 && th % 2 == 0; }
+
+template <int CIN, int HID, int COUT, int S, int TH, int TW, int NE, int ND, int WCO, int DWB, bool VP = false>
 struct IrwGeom {
   static constexpr int NW = NE + ND;
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
@@ -33,9 +40,13 @@ struct IrwGeom {
   static constexpr int WKP = (CIN + 31) / 32 * 32;   // blob row length of the expand weights
   static constexpr int ES = 48;                   // 16-B granules per row = 2 mod 4: conflict-free b128 reads
   static constexpr int HIDP_ = (HID + 31) / 32 * 32;
-  static constexpr int bytes_for(int xs) {
-    return (PINP * xs + 2 * PINP * ES) * 2 + 9 * HIDP_ * DWB + 2 * HIDP_ * 4;
-  }
+  // VP slab: row pairs x columns, 16 positions per expand unit (two MFMA pixel tiles: even and odd row)
+  static constexpr int PR = (IH + 1) / 2, NQ = PR * IW, NU = (NQ + 15) / 16, NQP = NU * 16;
+  static constexpr int RS = NQP * 32 + 16;        // bytes per channel-group region (regions 16 B apart mod 256 B)
+  static constexpr int EPU = (NU + NE - 1) / NE;  // expand units per expand wave
+  static constexpr int ES_BYTES = VP ? 4 * RS : PINP * ES * 2;   // one hidden slab buffer
+  static constexpr int WD_BYTES = VP ? 6 * HIDP_ * 4 : 9 * HIDP_ * DWB;
+  static constexpr int bytes_for(int xs) { return PINP * xs * 2 + 2 * ES_BYTES + WD_BYTES + 2 * HIDP_ * 4; }
   static constexpr int XS = bytes_for(CINP + 16) <= 163840 ? CINP + 16 : CINP + 8;   // input row stride
   static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
   static constexpr int NCT = (COUT + 15) / 16;
@@ -48,7 +59,8 @@ struct IrwGeom {
   static constexpr int LDS_BYTES = bytes_for(XS);
   static_assert(CIN % 8 == 0 && HID % 16 == 0 && COUT % 8 == 0, "channel counts");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
-  static_assert(EPT <= 32, "validity mask is 32 bits");
+  static_assert(EPT <= 32 && 2 * EPU <= 32, "validity mask is 32 bits");
+  static_assert(!VP || PAIR, "VP depthwise runs two output rows per step");
   static_assert(2 * NCH + 8 <= SPEF_TRACE_SLOTS, "trace slots");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
@@ -60,16 +72,19 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     const float* __restrict__ bp, typename DT::T* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x,
     int tiles_y, uint32_t nwg) {
   using DW = typename DT::DW;
-  using G = IrwGeom<CIN, HID, COUT, S, TH, TW, NE, ND, WCO, (int)sizeof(DW)>;
+  constexpr bool VP = irw_vp(std::is_same<DT, F16>::value, S, TH, TW);
+  using G = IrwGeom<CIN, HID, COUT, S, TH, TW, NE, ND, WCO, (int)sizeof(DW), VP>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
   using x4 = typename DT::x4;
   constexpr int NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   T* Xs = reinterpret_cast<T*>(smem);                          // [PINP][XS] input tile (+halo)
-  T* Es0 = Xs + G::PINP * G::XS;                               // [2][PINP][ES] hidden chunk slabs
-  DW* Wds = reinterpret_cast<DW*>(Es0 + 2 * G::PINP * G::ES);  // [9][HIDP] depthwise weights (0 past HID)
-  float* Be = reinterpret_cast<float*>(Wds + 9 * G::HIDP);     // [HIDP] expand bias
+  T* Es0 = Xs + G::PINP * G::XS;                               // [2] hidden chunk slabs ([PINP][ES] or VP regions)
+  char* Wdb = reinterpret_cast<char*>(Es0) + 2 * G::ES_BYTES;
+  DW* Wds = reinterpret_cast<DW*>(Wdb);                        // [9][HIDP] depthwise weights (0 past HID)
+  uint32_t* Wdp = reinterpret_cast<uint32_t*>(Wdb);            // VP: [kx][(w0,w1) | (w1,w2)][HIDP] weight pairs
+  float* Be = reinterpret_cast<float*>(Wdb + G::WD_BYTES);     // [HIDP] expand bias
   float* Bd = Be + G::HIDP;                                    // [HIDP] depthwise bias
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -89,11 +104,25 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     constexpr int NXP = G::PINP * GPR;
     constexpr int EPP = 16 / (int)sizeof(DW);
     constexpr int DPR = G::HIDP / EPP;                 // depthwise pieces per tap
-    constexpr int NDP = 9 * DPR;
+    constexpr int NDP = VP ? 0 : 9 * DPR;
     constexpr int NBP = G::HIDP / 4;
     constexpr int NTOT = NXP + NDP + 2 * NBP;
     constexpr int NIT = (NTOT + NW * 64 - 1) / (NW * 64);
     const T* Xb = X + (size_t)b * H * W * CIN;
+    // VP weight pairs: piece u = (kx, j, 4 channels) from two 8-B pieces of taps (j, kx) and (j + 1, kx)
+    constexpr int NVP = VP ? 6 * G::HIDP / 4 : 0;
+    constexpr int NIV = (NVP + NW * 64 - 1) / (NW * 64);
+    uint2 wa[NIV > 0 ? NIV : 1], wb[NIV > 0 ? NIV : 1];
+#pragma unroll
+    for (int i = 0; i < NIV; ++i) {
+      const int u = tid + NW * 64 * i;
+      const int g = u % (G::HIDP / 4), kj = u / (G::HIDP / 4), kx = kj >> 1, j = kj & 1;
+      const bool ok = u < NVP && 4 * g < HID;
+      const int off = ok ? (j * 3 + kx) * HID + 4 * g : 0;
+      wa[i] = *reinterpret_cast<const uint2*>(Wd + off);
+      wb[i] = *reinterpret_cast<const uint2*>(Wd + (ok ? off + 3 * HID : 0));
+      if (!ok) wa[i] = wb[i] = make_uint2(0, 0);
+    }
     uint4 v[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
@@ -131,6 +160,16 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       }
       if (dst) *reinterpret_cast<uint4*>(dst) = v[i];
     }
+#pragma unroll
+    for (int i = 0; i < NIV; ++i) {   // (lo = tap j, hi = tap j + 1 of each channel)
+      const int u = tid + NW * 64 * i;
+      if (u < NVP) {
+        const uint2 a = wa[i], c = wb[i];
+        *reinterpret_cast<uint4*>(Wdp + 4 * u) =
+            make_uint4((a.x & 0xffffu) | (c.x << 16), (a.x >> 16) | (c.x & 0xffff0000u), (a.y & 0xffffu) | (c.y << 16),
+                       (a.y >> 16) | (c.y & 0xffff0000u));
+      }
+    }
   }
   SPEF_TRACE(1);
 
@@ -158,7 +197,83 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     }
   };
   // expand of chunk c into slab Es[c & 1] by this expand wave
+  auto expand_vp = [&](int c) {
+    // unit u = 16 pair positions q; lane r16 computes the even- and odd-row pixel of its position (two MFMA pixel
+    // tiles) and stores each channel's pair as one dword (channels 4kg.. -> region kg/2, 16+4kg.. -> region 2+kg/2)
+    char* Ew = reinterpret_cast<char*>(Es0) + (c & 1) * G::ES_BYTES;
+    const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
+    const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
+    constexpr int NBX = G::K16 ? 1 : G::KS;
+    using BX = typename std::conditional<G::K16, x4, x8>::type;
+    constexpr bool VBATCH = G::EPU * 2 * NBX * (G::K16 ? 2 : 4) <= 48;
+    BX vbx[G::EPU][2][NBX];
+    auto read_vbx = [&](int jj) {
+      const int q = (ew + NE * jj) * 16 + r16;
+      const int qc = q < G::NQ ? q : G::NQ - 1;
+      const int pr = qc / G::IW, col = qc - pr * G::IW;
+      const int p0 = 2 * pr * G::IW + col;
+      const int p1 = (G::IH % 2 == 0 || 2 * pr + 1 < G::IH) ? p0 + G::IW : p0;
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const T* xr = Xs + (h ? p1 : p0) * G::XS;
+        if constexpr (G::K16) {
+          vbx[jj][h][0] = *reinterpret_cast<const x4*>(xr + 4 * kg);
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < G::KS; ++ks) vbx[jj][h][ks] = *reinterpret_cast<const x8*>(xr + 8 * kg + 32 * ks);
+        }
+      }
+    };
+#pragma unroll
+    for (int jj = 0; jj < G::EPU; ++jj) {
+      if (!VBATCH || ew + NE * jj >= G::NU) break;
+      read_vbx(jj);
+    }
+#pragma unroll
+    for (int jj = 0; jj < G::EPU; ++jj) {
+      const int u = ew + NE * jj;
+      if (u >= G::NU) break;
+      if (!VBATCH) read_vbx(jj);
+      f32x4 e[2][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        e[h][0] = f32x4{eb0.x, eb0.y, eb0.z, eb0.w};
+        e[h][1] = f32x4{eb1.x, eb1.y, eb1.z, eb1.w};
+        if constexpr (G::K16) {
+          e[h][0] = DT::mfma16(eq0, vbx[jj][h][0], e[h][0]);
+          e[h][1] = DT::mfma16(eq1, vbx[jj][h][0], e[h][1]);
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < G::KS; ++ks) {
+            e[h][0] = DT::mfma(ea0[ks], vbx[jj][h][ks], e[h][0]);
+            e[h][1] = DT::mfma(ea1[ks], vbx[jj][h][ks], e[h][1]);
+          }
+        }
+      }
+      uint4 d[2];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        d[t] = make_uint4(relu_pk2(e[0][t][0], e[1][t][0]), relu_pk2(e[0][t][1], e[1][t][1]),
+                          relu_pk2(e[0][t][2], e[1][t][2]), relu_pk2(e[0][t][3], e[1][t][3]));
+      if (!interior) {   // zero the halves of pixels outside the image (the depthwise padding)
+        const uint32_t m = (((pvmask >> (2 * jj)) & 1u) ? 0x0000ffffu : 0u) |
+                           (((pvmask >> (2 * jj)) & 2u) ? 0xffff0000u : 0u);
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          d[t].x &= m; d[t].y &= m; d[t].z &= m; d[t].w &= m;
+        }
+      }
+      typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+      char* er = Ew + (u * 16 + r16) * 32 + (kg & 1) * 16;
+      *reinterpret_cast<u32x4*>(er + (kg >> 1) * G::RS) = u32x4{d[0].x, d[0].y, d[0].z, d[0].w};
+      *reinterpret_cast<u32x4*>(er + (2 + (kg >> 1)) * G::RS) = u32x4{d[1].x, d[1].y, d[1].z, d[1].w};
+    }
+  };
   auto expand = [&](int c) {
+    if constexpr (VP) {
+      expand_vp(c);
+      return;
+    }
     T* Ew = Es0 + (c & 1) * G::PINP * G::ES;
     const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
     const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
@@ -231,7 +346,19 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   // The two roles run separate loops with the same barrier count (2 + NCH), so each role's registers (the
   // project accumulators, the expand fragments) are allocated independently.
   if (is_expand) {
-    if (!interior)   // only edge tiles mask (workgroup-uniform branch)
+    if (VP && !interior) {   // VP: bits 2j / 2j+1 = even / odd row pixel of unit j
+#pragma unroll
+      for (int jj = 0; jj < G::EPU; ++jj) {
+        const int q = (ew + NE * jj) * 16 + r16;
+        if (q < G::NQ) {
+          const int pr = q / G::IW, col = q - pr * G::IW;
+          const int iy = iy0 + 2 * pr, ix = ix0 + col;
+          const bool cx = ix >= 0 && ix < W;
+          if (cx && iy >= 0 && iy < H) pvmask |= 1u << (2 * jj);
+          if (cx && 2 * pr + 1 < G::IH && iy + 1 >= 0 && iy + 1 < H) pvmask |= 2u << (2 * jj);
+        }
+      }
+    } else if (!interior)   // only edge tiles mask (workgroup-uniform branch)
 #pragma unroll
     for (int jj = 0; jj < G::EPT; ++jj) {
       const int p = (ew + NE * jj) * 16 + r16;
@@ -297,6 +424,51 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
         db[0] = u0.x; db[1] = u0.y; db[2] = u0.z; db[3] = u0.w;
         db[4] = u1.x; db[5] = u1.y; db[6] = u1.z; db[7] = u1.w;
       }
+      if constexpr (VP) {
+        // per kernel column kx: row oy (even) dot2(ky 0,1) then fma(ky 2); row oy + 1 fma(ky 0) then dot2(ky 1,2)
+        // -- dw_kernel<.., VP>'s order. This lane's channels 8kg.. live in region kg (32 B per position).
+        auto rd8 = [&](const void* p, uint32_t v[8]) {
+          const uint4 a = *reinterpret_cast<const uint4*>(p), b = *(reinterpret_cast<const uint4*>(p) + 1);
+          v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+        };
+        const char* er = reinterpret_cast<const char*>(Es0) + (c & 1) * G::ES_BYTES + kg * G::RS;
+        uint32_t w01[3][8], w12[3][8];   // the chunk's weight pairs, read once for all of this wave's pixel tiles
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          rd8(Wdp + (2 * kx) * G::HIDP + 32 * c + 8 * kg, w01[kx]);
+          rd8(Wdp + (2 * kx + 1) * G::HIDP + 32 * c + 8 * kg, w12[kx]);
+        }
+#pragma unroll
+        for (int qi = 0; qi < G::QPW; qi += 2) {   // output rows oy (even) and oy + 1: pairs m = oy / 2 and m + 1
+          x8 bf0, bf1;
+          {
+            float a0[8], a1[8];
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a0[e] = a1[e] = db[e];
+            const char* pb = er + ((oyq[qi] >> 1) * G::IW + oxq[qi]) * 32;
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) {
+              uint32_t pc[8], pn[8];
+              rd8(pb + kx * 32, pc);
+              rd8(pb + (G::IW + kx) * 32, pn);
+#pragma unroll
+              for (int e = 0; e < 8; ++e) {
+                a1[e] = fmaf(h_hi(pc[e]), h_lo(w01[kx][e]), a1[e]);
+                a0[e] = dot2h(pc[e], w01[kx][e], a0[e]);
+                a0[e] = fmaf(h_lo(pn[e]), h_hi(w12[kx][e]), a0[e]);
+                a1[e] = dot2h(pn[e], w12[kx][e], a1[e]);
+              }
+            }
+            bf0 = relu_cvt8<DT>(a0);
+            bf1 = relu_cvt8<DT>(a1);
+          }
+#pragma unroll
+          for (int t = 0; t < G::NCTW; ++t) {
+            acc[qi][t] = DT::mfma(pa[t], bf0, acc[qi][t]);
+            acc[qi + 1][t] = DT::mfma(pa[t], bf1, acc[qi + 1][t]);
+          }
+        }
+      } else {
       // the chunk's 9 depthwise weight vectors, read once for all of this wave's pixel tiles
       DW8<DT> wt[9];
       if (hv) {
@@ -361,6 +533,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
           for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
         }
       }
+      }
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) pa[t] = pn[t];
       SPEF_TRACE(6 + 2 * c);
@@ -422,7 +595,8 @@ static hipError_t irw_go(const void* x, const void* we, const float* be, const v
                          const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s) {
   using DW = typename DT::DW;
   using T = typename DT::T;
-  using G = IrwGeom<CIN, HID, COUT, S, TH, TW, NE, ND, WCO, (int)sizeof(DW)>;
+  using G = IrwGeom<CIN, HID, COUT, S, TH, TW, NE, ND, WCO, (int)sizeof(DW),
+                    irw_vp(std::is_same<DT, F16>::value, S, TH, TW)>;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
