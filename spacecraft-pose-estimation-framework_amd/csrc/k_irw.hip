@@ -22,6 +22,14 @@
 
 namespace spef {
 
+// Per-chunk barrier of the role loops. SPEF_KBENCH_NO_CHUNK_BARRIER (tools/kbench timing ablation only, wrong results)
+// removes it to measure what the chunk hand-off costs.
+#ifdef SPEF_KBENCH_NO_CHUNK_BARRIER
+#define SPEF_IRW_CHUNK_SYNC() ((void)0)
+#else
+#define SPEF_IRW_CHUNK_SYNC() __syncthreads()
+#endif
+
 // Vertical-pair depthwise (fp16, stride 1, 16-wide tiles; blocks 8-13): the hidden slab holds, per (row pair, column)
 // position, one dword per channel = (row 2m, row 2m+1), in four 8-channel regions (k_irb.hip's VP layout); a kernel
 // column's taps ky 0,1 (or 1,2) are one v_dot2_f32_f16 and the third one v_fma_mix: 6 instead of 9 VALU per 3x3
@@ -384,7 +392,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
         load_ea(c + 2);
       }
       SPEF_TRACE(6 + 2 * c);
-      __syncthreads();          // Es[(c+1) & 1] complete; Es[c & 1] free for chunk c+2
+      SPEF_IRW_CHUNK_SYNC();    // Es[(c+1) & 1] complete; Es[c & 1] free for chunk c+2
       SPEF_TRACE(7 + 2 * c);
     }
   } else {
@@ -537,7 +545,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) pa[t] = pn[t];
       SPEF_TRACE(6 + 2 * c);
-      __syncthreads();
+      SPEF_IRW_CHUNK_SYNC();
       SPEF_TRACE(7 + 2 * c);
     }
   }
