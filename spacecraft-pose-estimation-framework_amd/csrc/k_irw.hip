@@ -280,56 +280,56 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   auto expand = [&](int c) {
     if constexpr (VP) {
       expand_vp(c);
-      return;
-    }
-    T* Ew = Es0 + (c & 1) * G::PINP * G::ES;
-    const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
-    const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
-    // all of this wave's B fragments first, then MFMAs + epilogues (the compiler cannot hoist an Xs read above the
-    // previous tile's slab store: same LDS array), within a register budget for the expand role
-    constexpr int NBX = G::K16 ? 1 : G::KS;
-    constexpr bool BATCH = G::EPT * NBX * (G::K16 ? 2 : 4) <= 48;
-    typename std::conditional<G::K16, x4, x8>::type bxs[G::EPT][NBX];
-    auto read_bx = [&](int jj) {
-      const int pt = ew + NE * jj;
-      if constexpr (G::K16) {
-        bxs[jj][0] = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
-      } else {
+    } else {
+      T* Ew = Es0 + (c & 1) * G::PINP * G::ES;
+      const float4 eb0 = *reinterpret_cast<const float4*>(Be + 32 * c + 4 * kg);
+      const float4 eb1 = *reinterpret_cast<const float4*>(Be + 32 * c + 16 + 4 * kg);
+      // all of this wave's B fragments first, then MFMAs + epilogues (the compiler cannot hoist an Xs read above the
+      // previous tile's slab store: same LDS array), within a register budget for the expand role
+      constexpr int NBX = G::K16 ? 1 : G::KS;
+      constexpr bool BATCH = G::EPT * NBX * (G::K16 ? 2 : 4) <= 48;
+      typename std::conditional<G::K16, x4, x8>::type bxs[G::EPT][NBX];
+      auto read_bx = [&](int jj) {
+        const int pt = ew + NE * jj;
+        if constexpr (G::K16) {
+          bxs[jj][0] = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
+        } else {
 #pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks)
-          bxs[jj][ks] = *reinterpret_cast<const x8*>(Xs + (pt * 16 + r16) * G::XS + 8 * kg + 32 * ks);
-      }
-    };
-#pragma unroll
-    for (int jj = 0; jj < G::EPT; ++jj) {
-      if (!BATCH || ew + NE * jj >= G::PIN16) break;
-      read_bx(jj);
-    }
-#pragma unroll
-    for (int jj = 0; jj < G::EPT; ++jj) {
-      const int pt = ew + NE * jj;
-      if (pt >= G::PIN16) break;
-      if (!BATCH) read_bx(jj);
-      f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
-      if constexpr (G::K16) {
-        e0 = DT::mfma16(eq0, bxs[jj][0], e0);
-        e1 = DT::mfma16(eq1, bxs[jj][0], e1);
-      } else {
-#pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-          e0 = DT::mfma(ea0[ks], bxs[jj][ks], e0);
-          e1 = DT::mfma(ea1[ks], bxs[jj][ks], e1);
+          for (int ks = 0; ks < G::KS; ++ks)
+            bxs[jj][ks] = *reinterpret_cast<const x8*>(Xs + (pt * 16 + r16) * G::XS + 8 * kg + 32 * ks);
         }
+      };
+#pragma unroll
+      for (int jj = 0; jj < G::EPT; ++jj) {
+        if (!BATCH || ew + NE * jj >= G::PIN16) break;
+        read_bx(jj);
       }
-      x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);
-      uint2 u0 = *reinterpret_cast<uint2*>(&o0), u1 = *reinterpret_cast<uint2*>(&o1);
-      if (!interior) {   // the depthwise zero padding: hidden values of pixels outside the image are 0
-        const uint32_t m0 = ((pvmask >> jj) & 1u) ? 0xffffffffu : 0u;
-        u0.x &= m0; u0.y &= m0; u1.x &= m0; u1.y &= m0;
+#pragma unroll
+      for (int jj = 0; jj < G::EPT; ++jj) {
+        const int pt = ew + NE * jj;
+        if (pt >= G::PIN16) break;
+        if (!BATCH) read_bx(jj);
+        f32x4 e0 = {eb0.x, eb0.y, eb0.z, eb0.w}, e1 = {eb1.x, eb1.y, eb1.z, eb1.w};   // bias as MFMA C
+        if constexpr (G::K16) {
+          e0 = DT::mfma16(eq0, bxs[jj][0], e0);
+          e1 = DT::mfma16(eq1, bxs[jj][0], e1);
+        } else {
+#pragma unroll
+          for (int ks = 0; ks < G::KS; ++ks) {
+            e0 = DT::mfma(ea0[ks], bxs[jj][ks], e0);
+            e1 = DT::mfma(ea1[ks], bxs[jj][ks], e1);
+          }
+        }
+        x4 o0 = relu_cvt4<DT>(e0), o1 = relu_cvt4<DT>(e1);
+        uint2 u0 = *reinterpret_cast<uint2*>(&o0), u1 = *reinterpret_cast<uint2*>(&o1);
+        if (!interior) {   // the depthwise zero padding: hidden values of pixels outside the image are 0
+          const uint32_t m0 = ((pvmask >> jj) & 1u) ? 0xffffffffu : 0u;
+          u0.x &= m0; u0.y &= m0; u1.x &= m0; u1.y &= m0;
+        }
+        T* er = Ew + (pt * 16 + r16) * G::ES + 4 * kg;
+        *reinterpret_cast<uint2*>(er) = u0;
+        *reinterpret_cast<uint2*>(er + 16) = u1;
       }
-      T* er = Ew + (pt * 16 + r16) * G::ES + 4 * kg;
-      *reinterpret_cast<uint2*>(er) = u0;
-      *reinterpret_cast<uint2*>(er + 16) = u1;
     }
   };
 
@@ -579,14 +579,17 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
 }
 
 // (variant, cin, hidden, cout, stride, TH x TW tile, residual, expand waves, depthwise waves, cout groups).
-// Variant 0 is the default; others are alternatives for tuning sweeps (SPEF_OPT_IRB_VARIANT).
+// Variant 0 is the default; others are alternatives for tuning sweeps (SPEF_OPT_IRB_VARIANT). With the pair depthwise,
+// 4 depthwise waves of two pair steps each (weight pairs read once for both) beat 8 waves of one step on blocks 12-13
+// (interleaved A/B: 88.8 -> 82.2 us per step) and tie on blocks 8-10; block 11 keeps 4. (4 expand + 2 depthwise waves
+// spill.)
 #define SPEF_IRW_TABLE(X)                                                   \
-  X(0, 64, 384, 64, 1, 16, 16, true, 4, 8, 1)      /* blocks 8-10  */       \
-  X(1, 64, 384, 64, 1, 16, 16, true, 4, 4, 1)                               \
+  X(0, 64, 384, 64, 1, 16, 16, true, 4, 4, 1)      /* blocks 8-10  */       \
+  X(1, 64, 384, 64, 1, 16, 16, true, 4, 8, 1)                               \
   X(0, 64, 384, 96, 1, 16, 16, false, 4, 4, 1)     /* block 11     */       \
   X(1, 64, 384, 96, 1, 16, 16, false, 4, 8, 1)                              \
-  X(0, 96, 576, 96, 1, 16, 16, true, 4, 8, 1)      /* blocks 12-13 */       \
-  X(1, 96, 576, 96, 1, 16, 16, true, 4, 4, 1)                               \
+  X(0, 96, 576, 96, 1, 16, 16, true, 4, 4, 1)      /* blocks 12-13 */       \
+  X(1, 96, 576, 96, 1, 16, 16, true, 4, 8, 1)                               \
   X(0, 96, 576, 160, 2, 8, 8, false, 4, 4, 2)      /* block 14     */       \
   X(1, 96, 576, 160, 2, 8, 8, false, 4, 8, 2)                               \
   X(0, 160, 960, 160, 1, 8, 8, true, 4, 4, 2)      /* blocks 15-16 */       \
