@@ -755,8 +755,9 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   X(0, 32, 32, 16, 1, 16, 16, false, false, 8, 1, true, false)    /* block 1      */ \
   X(0, 16, 96, 24, 2, 4, 16, true, false, 4, 1, false, false)     /* block 2      */ \
   X(2, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false)                        \
-  X(0, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false)     /* block 3      */ \
+  X(0, 24, 144, 24, 1, 16, 16, true, true, 4, 1, false, false)    /* block 3      */ \
   X(1, 24, 144, 24, 1, 8, 16, true, true, 8, 1, false, false)                        \
+  X(2, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false)                        \
   X(0, 24, 144, 32, 2, 8, 8, true, false, 4, 1, false, false)     /* block 4      */ \
   X(2, 24, 144, 32, 2, 8, 16, true, false, 8, 1, false, false)                       \
   X(0, 32, 192, 32, 1, 8, 16, true, true, 4, 1, false, false)     /* blocks 5-6   */ \
@@ -817,14 +818,14 @@ static bool irb_has(int variant, int cin, int hid, int cout, int stride, bool ex
 template <typename DT>
 // timing ablations of the variant-0 configurations (tools/explore.py ABL=1): variant 100 + 10 * ABL
 #define SPEF_IRB_ABL(X)                                                                                      \
-  X(1, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) X(2, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) \
-  X(3, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) X(4, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false) \
+  X(1, 24, 144, 24, 1, 16, 16, true, true, 4, 1, false, false) X(2, 24, 144, 24, 1, 16, 16, true, true, 4, 1, false, false) \
+  X(3, 24, 144, 24, 1, 16, 16, true, true, 4, 1, false, false) X(4, 24, 144, 24, 1, 16, 16, true, true, 4, 1, false, false) \
   X(1, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(2, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
   X(3, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(4, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
   X(1, 16, 96, 24, 2, 4, 16, true, false, 4, 1, false, false) X(2, 16, 96, 24, 2, 4, 16, true, false, 4, 1, false, false) \
   X(3, 16, 96, 24, 2, 4, 16, true, false, 4, 1, false, false) X(4, 16, 96, 24, 2, 4, 16, true, false, 4, 1, false, false) \
   X(5, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(6, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) \
-  X(7, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(5, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false)
+  X(7, 96, 576, 96, 1, 16, 16, true, true, 8, 1, false, true) X(5, 24, 144, 24, 1, 16, 16, true, true, 4, 1, false, false)
 
 static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stride, bool expand, bool res,
                                const void* x, const void* we, const float* be, const void* wd, const float* bd,
