@@ -280,7 +280,7 @@ def main():
     ap.add_argument('--cpu-batch', type=int, default=64)
     ap.add_argument('--traffic', default=None,
                     help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic (default: '
-                         'profiles/r02f_pmc_traffic.json, r02_int8_pmc_traffic.json for --dtype int8)')
+                         'profiles/r02g_pmc_traffic.json, r02_int8_pmc_traffic.json for --dtype int8)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU + gloo: the distributed control flow (weight distribution, timing, max over ranks, '
                          'JSON) without device work')
@@ -288,7 +288,7 @@ def main():
     if args.traffic is None:   # the newest committed FETCH/WRITE summary of this path
         args.traffic = newest_profile(
             ['r02_int8_pmc_traffic.json', 'r01_int8_pmc_traffic.json'] if args.dtype == 'int8' else
-            ['r02f_pmc_traffic.json', 'r02e_pmc_traffic.json', 'r02d_pmc_traffic.json', 'r02c_pmc_traffic.json', 'r02b_pmc_traffic.json', 'r02_pmc_traffic.json'])
+            ['r02g_pmc_traffic.json', 'r02f_pmc_traffic.json', 'r02e_pmc_traffic.json', 'r02d_pmc_traffic.json', 'r02c_pmc_traffic.json', 'r02b_pmc_traffic.json', 'r02_pmc_traffic.json'])
 
     import torch
     import torch.distributed as dist
