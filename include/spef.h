@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define SPEF_ABI_VERSION 2
+#define SPEF_ABI_VERSION 3
 #define SPEF_COMM_ID_BYTES 128   /* size of the RCCL unique id (ncclUniqueId) */
 
 enum spef_status {
@@ -31,7 +31,8 @@ enum spef_status {
   SPEF_ERR_HIP = 2,      /* HIP runtime error                                                        */
   SPEF_ERR_BLOB = 3,     /* malformed / incompatible weight blob                                      */
   SPEF_ERR_STATE = 4,    /* weights or decode tables not loaded, workspace too small                  */
-  SPEF_ERR_NUMERIC = 5   /* NaN / zero-sum in decode (ValueError, classification_utils.py:134,253,262) */
+  SPEF_ERR_NUMERIC = 5,  /* NaN / zero-sum in decode (ValueError, classification_utils.py:134,253,262) */
+  SPEF_ERR_COMM = 6      /* RCCL error or timeout: the communicator was aborted (ncclCommAbort)       */
 };
 
 /* input layouts of spef_forward */
@@ -59,7 +60,8 @@ int spef_destroy(spef_ctx* ctx);
  * (or stays empty), so a failed reload never leaves a half-loaded context. */
 int spef_load_weights(spef_ctx* ctx, const void* host_blob, size_t bytes);
 int spef_load_weights_device(spef_ctx* ctx, const void* dev_blob, size_t bytes);
-/* Query the loaded model: head (0 URSONet, 1 keypoints), output widths, storage dtype (1 fp16, 2 bf16). */
+/* Query the loaded model: head (0 URSONet, 1 keypoints), output widths, storage dtype (1 fp16, 2 bf16, 3 int8,
+ * 4 fp32 = the reference's own arithmetic: exact-fp32 MFMA, one kernel per conv). */
 int spef_model_info(const spef_ctx* ctx, int* head, int* n_out0, int* n_out1, int* dtype, int* n_ops);
 
 /* Allocate activation workspace for batches up to B of H x W frames. Must precede spef_forward for that
@@ -145,12 +147,21 @@ int spef_validate_blob(const void* host_blob, size_t bytes, int* dtype, int* hea
 /* Weight broadcast over RCCL (xGMI) -- SURVEY.md §8b/§8e: rank `root` sends the blob its context holds, every
  * other rank's context receives and loads it (header, op table and data section, device to device; no host
  * round trip). Collective: every rank of `comm` calls it with the same root. Replaces each rank reading
- * parameters.pt itself (modeling/model.py:261-266). `comm` is an RCCL communicator (ncclComm_t) -- the host's
- * own, or one made with spef_comm_init from an id that rank 0 produced with spef_comm_unique_id and the host
- * shipped to the other ranks (any side channel: torch.distributed, MPI, a file). On failure a receiving context
- * keeps the model it had. */
+ * parameters.pt itself (modeling/model.py:261-266).
+ * Failure handling (the reference's analogue is the socket timeouts of spe_nvidia.py:82-103):
+ *  - the ranks agree (all-reduce MAX of a status word) after the header broadcast and again after the receivers
+ *    have staged the blob; no rank enters a data collective unless all are ready, no receiver commits the new
+ *    model unless all staged it, and every rank returns the same status, naming the failing rank;
+ *  - every wait is bounded by the communicator's timeout; an RCCL error or a timeout aborts the communicator
+ *    (ncclCommAbort) and returns SPEF_ERR_COMM -- the handle is then dead (spef_comm_destroy only forgets it).
+ * On any failure a receiving context keeps the model it had.
+ * `comm` is an RCCL communicator (ncclComm_t): one made with spef_comm_init (nonblocking, ncclConfig_t.blocking
+ * = 0, bounded by `timeout_ms`; <= 0 = 120 s) from an id that rank 0 drew with spef_comm_unique_id and the host
+ * shipped to the other ranks (any side channel: torch.distributed, MPI, a file), or the host's own (120 s).
+ * spef_comm_abort aborts a communicator from the host (e.g. when the launcher learns a peer died). */
 int spef_comm_unique_id(void* id_out, size_t cap);
-int spef_comm_init(int device, int nranks, int rank, const void* id, void** comm_out);
+int spef_comm_init(int device, int nranks, int rank, const void* id, int timeout_ms, void** comm_out);
+int spef_comm_abort(void* comm);
 int spef_comm_destroy(void* comm);
 int spef_bcast_weights(spef_ctx* ctx, void* comm, int root);
 

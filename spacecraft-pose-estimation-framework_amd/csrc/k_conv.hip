@@ -304,7 +304,12 @@ static inline unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + p
 hipError_t launch_stem(int dtype, int in_layout, const void* in, const float* w, const float* bias, void* y, int B,
                        int H, int W, int OH, int OW, hipStream_t s) {
   const unsigned g = blocks_for((int64_t)B * OH * OW * 4, 256);
-  if (dtype == DT_F16) {
+  if (dtype == DT_F32) {
+    if (in_layout == IN_U8_NHWC)
+      stem_kernel<F32, IN_U8_NHWC><<<g, 256, 0, s>>>(in, w, bias, (float*)y, B, H, W, OH, OW);
+    else
+      stem_kernel<F32, IN_F32_NCHW><<<g, 256, 0, s>>>(in, w, bias, (float*)y, B, H, W, OH, OW);
+  } else if (dtype == DT_F16) {
     if (in_layout == IN_U8_NHWC)
       stem_kernel<F16, IN_U8_NHWC><<<g, 256, 0, s>>>(in, w, bias, (_Float16*)y, B, H, W, OH, OW);
     else
@@ -373,6 +378,11 @@ hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias
       dw_kernel<F16, 1, true><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
     else
       dw_kernel<F16, 2, true><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
+  } else if (dtype == DT_F32) {
+    if (stride == 1)
+      dw_kernel<F32, 1><<<g, 256, 0, s>>>((const float*)x, (const float*)w9, bias, (float*)y, B, H, W, C, OH, OW);
+    else
+      dw_kernel<F32, 2><<<g, 256, 0, s>>>((const float*)x, (const float*)w9, bias, (float*)y, B, H, W, C, OH, OW);
   } else if (dtype == DT_F16) {
     if (stride == 1)
       dw_kernel<F16, 1><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
@@ -400,6 +410,7 @@ hipError_t launch_pw_pool(int dtype, const void* x, const void* wt, const float*
 }
 
 hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStream_t s) {
+  if (dtype == DT_F32) return hipMemcpyAsync(y, x, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s);
   const unsigned g = blocks_for(n, 256);
   if (dtype == DT_F16)
     to_f32_kernel<F16><<<g, 256, 0, s>>>((const _Float16*)x, y, n);

@@ -14,6 +14,10 @@
 
 #include <algorithm>
 #include <array>
+#include <chrono>
+#include <map>
+#include <mutex>
+#include <thread>
 
 #include <string>
 #include <vector>
@@ -68,6 +72,7 @@ struct spef_ctx {
   int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
   int irb_variant = 0;       // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps)
   int wavespec = 2;          // SPEF_OPT_WAVESPEC: 2 = pipelined (k_irp.hip), 1 = wave-specialised (k_irw.hip)
+  int test_fail_bcast = 0;   // SPEF_OPT_TEST_FAIL_BCAST (spef_tuning.hpp): failure injection in spef_bcast_weights
   // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
   std::vector<double> q8_sw, q8_bias;
   std::vector<int32_t> q8_wsum;
@@ -137,12 +142,14 @@ hipError_t prof_launch(spef_ctx* c, hipStream_t s, const char* key, double bytes
 
 hipError_t pw_any(spef_ctx* c, int dt, int epi, const void* x, const void* wt, const float* bias, const void* r,
                   void* y, int64_t M, int K, int N, hipStream_t s) {
+  if (dt == DT_F32) return launch_gemm_f32(epi, x, wt, bias, r, y, M, K, N, s);
   return c->gemm ? launch_gemm_pw(dt, epi, x, wt, bias, r, y, M, K, N, s)
                  : launch_pw(dt, epi, x, wt, bias, r, y, M, K, N, s);
 }
 
 const char* pw_key(int dt, int epi, int N);
 const char* pw_any_key(spef_ctx* c, int dt, int epi, int N) {
+  if (dt == DT_F32) return gemm_f32_key(N);
   return c->gemm ? gemm_key(dt, epi, N) : pw_key(dt, epi, N);
 }
 
@@ -181,7 +188,9 @@ static inline int q8_pool_shift(const spef_ctx* c, int hw) {
   return sh > 0 ? sh : 0;
 }
 
-size_t elem_size(const spef_ctx* c) { return c->hdr.dtype == DT_I8 ? 1 : 2; }  // int8 | fp16 / bf16 activations
+size_t elem_size(const spef_ctx* c) {   // int8 | fp16 / bf16 | fp32 activations
+  return c->hdr.dtype == DT_I8 ? 1 : c->hdr.dtype == DT_F32 ? 4 : 2;
+}
 
 // algorithmic HBM bytes of one pointwise launch: read X, write Y (+ read residual), weights + bias once
 double pw_bytes(int64_t M, uint32_t K, uint32_t N, bool res) {
@@ -228,6 +237,8 @@ int check_ready(spef_ctx* c, int B, int H, int W) {
 int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W, hipStream_t s, int mode,
                  int stop, void** out_buf, int* oc, int* oh, int* ow, float* feat_f32 = nullptr) {
   const int dt = (int)c->hdr.dtype;
+  const bool f32 = dt == DT_F32;   // fp32 schedule: one kernel per conv (k_f32.hip), no fused kernels
+  const double es = f32 ? 4.0 : 2.0;   // activation bytes per element (profiler byte counts)
   void* cur = nullptr;
   int h = H, w = W, ch = 3;
   int op_index = 0;
@@ -250,7 +261,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
     if (op.kind == OP_STEM) {
       const int OH = conv_out(h, 2), OW = conv_out(w, 2);
       const OpDesc* nx = (&op + 1 < c->ops.data() + c->ops.size()) ? &op + 1 : nullptr;
-      const bool front = c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx && nx->kind == OP_IRB &&
+      const bool front = !f32 && c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx && nx->kind == OP_IRB &&
                          nx->cin == 32 && nx->hidden == 32 && nx->cout == 16 && nx->expand == 1 && nx->stride == 1 &&
                          op.cout == 32 && op.x0 != kAbsent;
       if (front) {
@@ -273,7 +284,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const double px = (double)B * OH * OW;
       const double in_b = (double)B * h * w * 3 * (layout == IN_U8_NHWC ? 1 : 4);
       HIP_TRY(prof_launch(c, s, layout == IN_U8_NHWC ? "stem_kernel<u8>" : "stem_kernel<f32>",
-                          in_b + px * 32 * 2, px * 2 * 27 * 32, [&] {
+                          in_b + px * 32 * es, px * 2 * 27 * 32, [&] {
         return launch_stem(dt, layout, input, ptr<float>(c, op.w0), ptr<float>(c, op.b0), y, B, h, w, OH, OW, s);
       }));
       cur = y;
@@ -286,7 +297,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const bool res = op.flags & 1u;
       const bool expand = op.expand != 1;
       void* x = cur;
-      if (c->fuse && (int64_t)h * w >= c->fuse_min_hw && irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res)) {
+      if (!f32 && c->fuse && (int64_t)h * w >= c->fuse_min_hw && irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res)) {
         void* y = pick({x});
         const int64_t M2 = (int64_t)B * OH * OW;
         const double flops = 2.0 * M * op.cin * op.hidden * (expand ? 1 : 0) + 18.0 * M2 * op.hidden +
@@ -322,7 +333,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         void* h1 = x;
         if (expand) {
           h1 = pick({x});
-          HIP_TRY(prof_launch(c, s, pw_any_key(c, dt, EPI_RELU, op.hidden), pw_bytes(M, op.cin, op.hidden, false),
+          HIP_TRY(prof_launch(c, s, pw_any_key(c, dt, EPI_RELU, op.hidden), pw_bytes(M, op.cin, op.hidden, false) * es / 2,
                               2.0 * M * op.cin * op.hidden, [&] {
             return pw_any(c, dt, EPI_RELU, x, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, h1, M,
                              (int)op.cin, (int)op.hidden, s);
@@ -333,14 +344,14 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const bool dw_pairs = irb_dw_pairs(dt, (int)op.hidden, expand, (int)op.stride);
         HIP_TRY(prof_launch(c, s, op.stride == 1 ? (dw_pairs ? "dw_kernel<1,pairs>" : "dw_kernel<1>")
                                                  : (dw_pairs ? "dw_kernel<2,pairs>" : "dw_kernel<2>"),
-                            ((double)B * h * w + opx) * op.hidden * 2 + 40.0 * op.hidden, opx * op.hidden * 18.0, [&] {
+                            ((double)B * h * w + opx) * op.hidden * es + 40.0 * op.hidden, opx * op.hidden * 18.0, [&] {
           return launch_dw(dt, h1, ptr<void>(c, op.w1), ptr<float>(c, op.b1), h2, B, h, w, (int)op.hidden,
                            (int)op.stride, OH, OW, dw_pairs, s);
         }));
         void* y = res ? pick({x, h2}) : pick({h2});
         const int64_t M2 = (int64_t)B * OH * OW;
         HIP_TRY(prof_launch(c, s, pw_any_key(c, dt, res ? EPI_RES : EPI_NONE, op.cout),
-                            pw_bytes(M2, op.hidden, op.cout, res), 2.0 * M2 * op.hidden * op.cout, [&] {
+                            pw_bytes(M2, op.hidden, op.cout, res) * es / 2, 2.0 * M2 * op.hidden * op.cout, [&] {
           return pw_any(c, dt, res ? EPI_RES : EPI_NONE, h2, ptr<void>(c, op.w2), ptr<float>(c, op.b2),
                            res ? x : nullptr, y, M2, (int)op.hidden, (int)op.cout, s);
         }));
@@ -350,7 +361,29 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         ch = (int)op.cout;
       }
     } else if (op.kind == OP_LAST) {
-      if (mode == 0) {
+      if (f32 && (mode == 0 || (mode == 2 && !feat_f32))) {   // fp32 map into a workspace buffer, then the mean
+        void* y = pick({cur});
+        const double M3 = (double)B * h * w;
+        HIP_TRY(prof_launch(c, s, gemm_f32_key(op.cout), M3 * (op.cin + op.cout) * 4 + (double)op.cout * (op.cin + 1) * 4,
+                            2.0 * M3 * op.cin * op.cout, [&] {
+          return launch_gemm_f32(EPI_RELU, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, y,
+                                 (int64_t)B * h * w, (int)op.cin, (int)op.cout, s);
+        }));
+        cur = y;
+        ch = (int)op.cout;
+        if (mode == 0)
+          HIP_TRY(prof_launch(c, s, "mean_hw_kernel", M3 * op.cout * 4 + (double)B * op.cout * 4, M3 * op.cout, [&] {
+            return launch_mean_hw((const float*)cur, c->pooled, B, h * w, (int)op.cout, s);
+          }));
+      } else if (f32 && mode == 2) {
+        HIP_TRY(prof_launch(c, s, gemm_f32_key(op.cout), (double)B * h * w * (op.cin + op.cout) * 4,
+                            2.0 * B * h * w * op.cin * op.cout, [&] {
+          return launch_gemm_f32(EPI_RELU, cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), nullptr, feat_f32,
+                                 (int64_t)B * h * w, (int)op.cin, (int)op.cout, s);
+        }));
+        cur = feat_f32;
+        ch = (int)op.cout;
+      } else if (mode == 0) {
         const double M3 = (double)B * h * w;
         const bool tiled = c->gemm && ((op.cout + 15) & ~15u) % 128 == 0;
         HIP_TRY(prof_launch(c, s, tiled ? "pool_gemm_kernel" : "pw_pool_kernel<4>",
@@ -637,7 +670,7 @@ static void op_extents(const OpDesc& op, uint32_t dtype, uint64_t ext[9]) {
   auto r16 = [](uint64_t n) { return (n + 15) & ~15ull; };
   auto r32 = [](uint64_t n) { return (n + 31) & ~31ull; };
   auto r64 = [](uint64_t n) { return (n + 63) & ~63ull; };
-  const uint64_t a = 2;                                   // fp16 / bf16 activation storage
+  const uint64_t a = dtype == DT_F32 ? 4 : 2;             // fp16 / bf16 | fp32 weight storage
   const uint64_t rq = 20;                                 // int64 M + int64 B + int32 S per channel
   for (int i = 0; i < 9; ++i) ext[i] = 0;
   const uint64_t ci = op.cin, co = op.cout, h = op.hidden;
@@ -675,10 +708,14 @@ static int parse_blob(const uint8_t* head_bytes, size_t meta_bytes, size_t bytes
   memcpy(&h, head_bytes, sizeof(h));
   if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_BLOB, "bad blob magic");
   if (h.version != kBlobVersion) return fail(SPEF_ERR_BLOB, "unsupported blob version");
-  if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8) return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
+  if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8 && h.dtype != DT_F32)
+    return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
   if (h.n_ops == 0 || h.n_ops > 4096) return fail(SPEF_ERR_BLOB, "bad op count");
+  // every term bounded on its own before any sum (a crafted ops_off near 2^64 must not wrap ops_end)
+  if (h.ops_off < sizeof(BlobHeader) || h.ops_off > bytes || (uint64_t)h.n_ops * sizeof(OpDesc) > bytes - h.ops_off)
+    return fail(SPEF_ERR_BLOB, "blob truncated");
   const uint64_t ops_end = h.ops_off + (uint64_t)h.n_ops * sizeof(OpDesc);
-  if (h.ops_off < sizeof(BlobHeader) || ops_end > h.data_off || h.data_off > bytes ||
+  if (ops_end > h.data_off || h.data_off > bytes ||
       h.data_bytes > bytes - h.data_off || ops_end > meta_bytes)
     return fail(SPEF_ERR_BLOB, "blob truncated");
   if (h.feat_c != 1280) return fail(SPEF_ERR_BLOB, "feature width must be 1280 (mobilenet_v2.py:232)");
@@ -704,8 +741,8 @@ static int parse_blob(const uint8_t* head_bytes, size_t meta_bytes, size_t bytes
     if (qop != (h.dtype == DT_I8)) return fail(SPEF_ERR_BLOB, "op kind does not match the blob dtype");
     if (op.kind == OP_QSTEM && op.cout != 32) return fail(SPEF_ERR_BLOB, "int8 stem needs 32 outputs");
     for (int k = 0; k < 4; ++k)
-      if (op.qbits[k] == 1 || op.qbits[k] > 8 || (op.qbits[k] && !qop))
-        return fail(SPEF_ERR_BLOB, "quantizer bit widths must be 2..8 (int8 ops only)");
+      if (op.qbits[k] == 1 || op.qbits[k] == 2 || op.qbits[k] > 8 || (op.qbits[k] && !qop))
+        return fail(SPEF_ERR_BLOB, "quantizer bit widths must be 3..8 (int8 ops only; quant.check_bit_width)");
     if (op.kind == OP_FC || op.kind == OP_QFC) {
       ++n_head;
       if (h.head != HEAD_URSONET || op.cin != h.feat_c || op.cout != h.n_out0 + h.n_out1)
@@ -723,9 +760,28 @@ static int parse_blob(const uint8_t* head_bytes, size_t meta_bytes, size_t bytes
   return SPEF_OK;
 }
 
-// Load the blob at `blob` (host or device memory). Transactional: everything is parsed and copied into new
-// storage first; the context's model is replaced only when all of it succeeded.
-static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_device) {
+// A blob parsed and copied into fresh device storage, not yet owned by any context (the first half of a
+// transactional load: a failure anywhere leaves the context's current model untouched).
+struct Staged {
+  BlobHeader h{};
+  std::vector<OpDesc> ops;
+  uint8_t* dd = nullptr;
+  std::vector<std::array<int64_t, 3>> q8_res;
+  std::vector<double> q8_sw, q8_bias;
+  std::vector<int32_t> q8_wsum;
+  double q8_sl = 0.0;
+  float q8_s_img = 0.f;
+  int q8_last_bits = 8, q8_pool_bits = 8, q8_fc_bias_bits = 8;
+  Staged() = default;
+  Staged(const Staged&) = delete;
+  Staged& operator=(const Staged&) = delete;
+  ~Staged() {
+    if (dd) hipFree(dd);
+  }
+};
+
+// Stage the blob at `blob` (host or device memory) into `st`.
+static int stage_blob(spef_ctx* c, const void* blob, size_t bytes, bool on_device, Staged* st) {
   if (!c || !blob) return fail(SPEF_ERR_ARG, "null argument");
   Dev d(c->device);
   std::vector<uint8_t> head;
@@ -743,71 +799,69 @@ static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_devi
     hb = (const uint8_t*)blob;
     meta = bytes;
   }
-  BlobHeader h;
-  std::vector<OpDesc> ops;
-  int rc = parse_blob(hb, meta, bytes, &h, &ops);
+  int rc = parse_blob(hb, meta, bytes, &st->h, &st->ops);
   if (rc) return rc;
-
-  uint8_t* dd = nullptr;
-  std::vector<std::array<int64_t, 3>> q8_res;
-  std::vector<double> q8_sw, q8_bias;
-  std::vector<int32_t> q8_wsum;
-  double q8_sl = 0.0;
-  float q8_s_img = 0.f;
-  int q8_last_bits = 8, q8_pool_bits = 8, q8_fc_bias_bits = 8;
-  auto stage = [&]() -> int {
-    HIP_TRY(hipMalloc(&dd, std::max<uint64_t>(h.data_bytes, 256)));
-    const uint8_t* src = (const uint8_t*)blob + h.data_off;
-    HIP_TRY(hipMemcpy(dd, src, h.data_bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
-    if (h.dtype == DT_I8) {   // small host-side constants of the int8 schedule, fetched once
-      q8_res.assign(ops.size(), {0, 0, 0});
-      for (size_t i = 0; i < ops.size(); ++i) {
-        const OpDesc& op = ops[i];
-        if (op.kind == OP_QSTEM) HIP_TRY(hipMemcpy(&q8_s_img, dd + op.x0, sizeof(float), hipMemcpyDeviceToHost));
-        if (op.kind == OP_QLAST) {
-          q8_last_bits = qbits(op, 0);
-          q8_pool_bits = qbits(op, 1);
-        }
-        if (op.kind == OP_QFC) q8_fc_bias_bits = qbits(op, 0);
-        if (op.kind == OP_QIRB && (op.flags & 1u))
-          HIP_TRY(hipMemcpy(q8_res[i].data(), dd + op.x1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost));
-        if (op.kind == OP_QFC) {
-          const size_t np_ = (op.cout + 15) & ~15u;
-          q8_sw.resize(np_);
-          q8_bias.resize(np_);
-          q8_wsum.resize(np_);
-          HIP_TRY(hipMemcpy(q8_sw.data(), dd + op.b0, np_ * sizeof(double), hipMemcpyDeviceToHost));
-          HIP_TRY(hipMemcpy(q8_bias.data(), dd + op.w1, np_ * sizeof(double), hipMemcpyDeviceToHost));
-          HIP_TRY(hipMemcpy(q8_wsum.data(), dd + op.x0, np_ * sizeof(int32_t), hipMemcpyDeviceToHost));
-          HIP_TRY(hipMemcpy(&q8_sl, dd + op.x1, sizeof(double), hipMemcpyDeviceToHost));
-        }
+  const BlobHeader& h = st->h;
+  const std::vector<OpDesc>& ops = st->ops;
+  HIP_TRY(hipMalloc(&st->dd, std::max<uint64_t>(h.data_bytes, 256)));
+  uint8_t* dd = st->dd;
+  const uint8_t* src = (const uint8_t*)blob + h.data_off;
+  HIP_TRY(hipMemcpy(dd, src, h.data_bytes, on_device ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+  if (h.dtype == DT_I8) {   // small host-side constants of the int8 schedule, fetched once
+    st->q8_res.assign(ops.size(), {0, 0, 0});
+    for (size_t i = 0; i < ops.size(); ++i) {
+      const OpDesc& op = ops[i];
+      if (op.kind == OP_QSTEM) HIP_TRY(hipMemcpy(&st->q8_s_img, dd + op.x0, sizeof(float), hipMemcpyDeviceToHost));
+      if (op.kind == OP_QLAST) {
+        st->q8_last_bits = qbits(op, 0);
+        st->q8_pool_bits = qbits(op, 1);
+      }
+      if (op.kind == OP_QFC) st->q8_fc_bias_bits = qbits(op, 0);
+      if (op.kind == OP_QIRB && (op.flags & 1u))
+        HIP_TRY(hipMemcpy(st->q8_res[i].data(), dd + op.x1, 3 * sizeof(int64_t), hipMemcpyDeviceToHost));
+      if (op.kind == OP_QFC) {
+        const size_t np_ = (op.cout + 15) & ~15u;
+        st->q8_sw.resize(np_);
+        st->q8_bias.resize(np_);
+        st->q8_wsum.resize(np_);
+        HIP_TRY(hipMemcpy(st->q8_sw.data(), dd + op.b0, np_ * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(st->q8_bias.data(), dd + op.w1, np_ * sizeof(double), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(st->q8_wsum.data(), dd + op.x0, np_ * sizeof(int32_t), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&st->q8_sl, dd + op.x1, sizeof(double), hipMemcpyDeviceToHost));
       }
     }
-    return SPEF_OK;
-  };
-  rc = stage();
-  if (rc) {
-    if (dd) hipFree(dd);
-    return rc;
   }
-  // commit
+  return SPEF_OK;
+}
+
+// Second half: the context takes the staged model (cannot fail).
+static void commit_staged(spef_ctx* c, Staged* st) {
+  Dev d(c->device);
   free_workspace(c);
   if (c->d_data) hipFree(c->d_data);
-  c->d_data = dd;
-  c->data_bytes = h.data_bytes;
-  c->hdr = h;
-  c->ops = std::move(ops);
-  c->q8_res = std::move(q8_res);
-  c->q8_sw = std::move(q8_sw);
-  c->q8_bias = std::move(q8_bias);
-  c->q8_wsum = std::move(q8_wsum);
-  c->q8_sl = q8_sl;
-  c->q8_s_img = q8_s_img;
-  c->q8_last_bits = q8_last_bits;
-  c->q8_pool_bits = q8_pool_bits;
-  c->q8_fc_bias_bits = q8_fc_bias_bits;
+  c->d_data = st->dd;
+  st->dd = nullptr;
+  c->data_bytes = st->h.data_bytes;
+  c->hdr = st->h;
+  c->ops = std::move(st->ops);
+  c->q8_res = std::move(st->q8_res);
+  c->q8_sw = std::move(st->q8_sw);
+  c->q8_bias = std::move(st->q8_bias);
+  c->q8_wsum = std::move(st->q8_wsum);
+  c->q8_sl = st->q8_sl;
+  c->q8_s_img = st->q8_s_img;
+  c->q8_last_bits = st->q8_last_bits;
+  c->q8_pool_bits = st->q8_pool_bits;
+  c->q8_fc_bias_bits = st->q8_fc_bias_bits;
   c->q8_fc_hw = 0;
   c->loaded = true;
+}
+
+static int load_common(spef_ctx* c, const void* blob, size_t bytes, bool on_device) {
+  Staged st;
+  const int rc = stage_blob(c, blob, bytes, on_device, &st);
+  if (rc) return rc;
+  commit_staged(c, &st);
   return SPEF_OK;
 }
 
@@ -834,6 +888,64 @@ int spef_validate_blob(const void* blob, size_t bytes, int* dtype, int* head, in
     if (r_ != ncclSuccess) return fail(SPEF_ERR_HIP, std::string(#expr) + ": " + ncclGetErrorString(r_));  \
   } while (0)
 
+// Communicators made by spef_comm_init: nonblocking (ncclConfig_t.blocking = 0) with a per-communicator timeout, so
+// every wait below is bounded and a dead peer ends in ncclCommAbort instead of a hang. A communicator
+// the host made itself is unknown here and gets kDefaultCommTimeoutMs.
+namespace {
+const int kDefaultCommTimeoutMs = 120000;
+struct CommInfo {
+  int timeout_ms;
+  bool aborted;
+};
+std::mutex g_comm_mu;
+std::map<void*, CommInfo> g_comms;
+
+int comm_timeout(void* comm) {
+  std::lock_guard<std::mutex> g(g_comm_mu);
+  auto it = g_comms.find(comm);
+  return it == g_comms.end() ? kDefaultCommTimeoutMs : it->second.timeout_ms;
+}
+
+using Clock = std::chrono::steady_clock;
+
+// Abort the communicator (unblocks every kernel of it on this rank; the handle is dead afterwards) and fail.
+int comm_abort_fail(ncclComm_t comm, const std::string& msg) {
+  ncclCommAbort(comm);
+  {
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    auto it = g_comms.find((void*)comm);
+    if (it != g_comms.end()) it->second.aborted = true;
+    else g_comms[(void*)comm] = {kDefaultCommTimeoutMs, true};
+  }
+  return fail(SPEF_ERR_COMM, msg + " -- communicator aborted (ncclCommAbort)");
+}
+
+// Wait until a nonblocking RCCL call has left ncclInProgress; abort on error or at the deadline.
+int comm_settle(ncclComm_t comm, ncclResult_t r, Clock::time_point deadline, const char* what) {
+  while (r == ncclInProgress) {
+    if (Clock::now() > deadline) return comm_abort_fail(comm, std::string(what) + ": timed out");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+    if (ncclCommGetAsyncError(comm, &r) != ncclSuccess) r = ncclSystemError;
+  }
+  if (r != ncclSuccess) return comm_abort_fail(comm, std::string(what) + ": " + ncclGetErrorString(r));
+  return SPEF_OK;
+}
+
+// Wait for the stream's collectives to finish, polling the communicator's async error; abort at the deadline.
+int comm_wait_stream(ncclComm_t comm, hipStream_t s, Clock::time_point deadline, const char* what, int inject) {
+  for (;;) {
+    const hipError_t e = inject ? hipErrorNotReady : hipStreamQuery(s);
+    if (e == hipSuccess) return SPEF_OK;
+    if (e != hipErrorNotReady) return comm_abort_fail(comm, std::string(what) + ": " + hipGetErrorString(e));
+    ncclResult_t ae = ncclSuccess;
+    if (ncclCommGetAsyncError(comm, &ae) != ncclSuccess || (ae != ncclSuccess && ae != ncclInProgress))
+      return comm_abort_fail(comm, std::string(what) + ": " + ncclGetErrorString(ae));
+    if (Clock::now() > deadline) return comm_abort_fail(comm, std::string(what) + ": timed out");
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+}  // namespace
+
 int spef_comm_unique_id(void* id_out, size_t cap) {
   if (!id_out || cap < sizeof(ncclUniqueId)) return fail(SPEF_ERR_ARG, "id buffer smaller than SPEF_COMM_ID_BYTES");
   static_assert(sizeof(ncclUniqueId) == SPEF_COMM_ID_BYTES, "SPEF_COMM_ID_BYTES != sizeof(ncclUniqueId)");
@@ -843,75 +955,196 @@ int spef_comm_unique_id(void* id_out, size_t cap) {
   return SPEF_OK;
 }
 
-int spef_comm_init(int device, int nranks, int rank, const void* id, void** comm_out) {
+int spef_comm_init(int device, int nranks, int rank, const void* id, int timeout_ms, void** comm_out) {
   if (!id || !comm_out || nranks < 1 || rank < 0 || rank >= nranks) return fail(SPEF_ERR_ARG, "bad communicator arguments");
+  if (timeout_ms <= 0) timeout_ms = kDefaultCommTimeoutMs;
   Dev d(device);
   HIP_TRY(hipSetDevice(device));
   ncclUniqueId uid;
   memcpy(&uid, id, sizeof(uid));
   ncclComm_t comm = nullptr;
-  NCCL_TRY(ncclCommInitRank(&comm, nranks, uid, rank));
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = 0;
+  const ncclResult_t r = ncclCommInitRankConfig(&comm, nranks, uid, rank, &cfg);
+  if (r != ncclSuccess && r != ncclInProgress) return fail(SPEF_ERR_COMM, std::string("ncclCommInitRankConfig: ") + ncclGetErrorString(r));
+  {
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    g_comms[(void*)comm] = {timeout_ms, false};
+  }
+  const int rc = comm_settle(comm, r, Clock::now() + std::chrono::milliseconds(timeout_ms), "communicator init");
+  if (rc) {   // aborted: the handle is gone
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    g_comms.erase((void*)comm);
+    return rc;
+  }
   *comm_out = comm;
+  return SPEF_OK;
+}
+
+int spef_comm_abort(void* comm) {
+  if (!comm) return SPEF_OK;
+  {
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    auto it = g_comms.find(comm);
+    if (it != g_comms.end() && it->second.aborted) return SPEF_OK;
+  }
+  comm_abort_fail((ncclComm_t)comm, "spef_comm_abort");
   return SPEF_OK;
 }
 
 int spef_comm_destroy(void* comm) {
   if (!comm) return SPEF_OK;
-  NCCL_TRY(ncclCommDestroy((ncclComm_t)comm));
+  bool aborted = false;
+  {
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    auto it = g_comms.find(comm);
+    if (it != g_comms.end()) {
+      aborted = it->second.aborted;
+      g_comms.erase(it);
+    }
+  }
+  if (aborted) return SPEF_OK;   // ncclCommAbort already released it
+  ncclComm_t cm = (ncclComm_t)comm;
+  const Clock::time_point dl = Clock::now() + std::chrono::milliseconds(kDefaultCommTimeoutMs);
+  ncclResult_t r = ncclCommFinalize(cm);   // nonblocking communicators finalize asynchronously
+  if (r == ncclInProgress) {
+    while (r == ncclInProgress && Clock::now() < dl) {
+      std::this_thread::sleep_for(std::chrono::microseconds(50));
+      if (ncclCommGetAsyncError(cm, &r) != ncclSuccess) r = ncclSystemError;
+    }
+  }
+  if (r != ncclSuccess) {
+    ncclCommAbort(cm);
+    return fail(SPEF_ERR_COMM, std::string("ncclCommFinalize: ") + ncclGetErrorString(r) + " -- aborted");
+  }
+  NCCL_TRY(ncclCommDestroy(cm));
   return SPEF_OK;
 }
 
+// Collective weight broadcast with agreement: no rank enters a data collective unless every rank reported a good
+// local state, and every rank returns the same verdict. Steps: header broadcast -> local checks + allocation ->
+// all-reduce(MAX) of the status words -> op table + data broadcasts -> receivers stage (parse, copy, validate) ->
+// second all-reduce(MAX) -> receivers commit. Any RCCL error or a wait past the communicator's timeout aborts the
+// communicator (ncclCommAbort) and returns SPEF_ERR_COMM; a failing rank is named in spef_last_error on every rank.
+// Status word: 0 = ok, else (error code << 16) | (failing rank + 1); MAX picks one failing rank deterministically.
 int spef_bcast_weights(spef_ctx* c, void* comm_, int root) {
   if (!c || !comm_) return fail(SPEF_ERR_ARG, "null argument");
   ncclComm_t comm = (ncclComm_t)comm_;
+  {
+    std::lock_guard<std::mutex> g(g_comm_mu);
+    auto it = g_comms.find(comm_);
+    if (it != g_comms.end() && it->second.aborted) return fail(SPEF_ERR_COMM, "communicator was aborted");
+  }
   int rank = 0, n = 0;
   NCCL_TRY(ncclCommUserRank(comm, &rank));
   NCCL_TRY(ncclCommCount(comm, &n));
   if (root < 0 || root >= n) return fail(SPEF_ERR_ARG, "root out of range");
   Dev d(c->device);
+  const Clock::time_point deadline = Clock::now() + std::chrono::milliseconds(comm_timeout(comm_));
+  const int inject = c->test_fail_bcast;   // spef_tuning.hpp SPEF_OPT_TEST_FAIL_BCAST
   struct Tmp {   // scratch freed on every exit path
     hipStream_t s = nullptr;
-    uint8_t* buf = nullptr;
-    ~Tmp() {
+    uint8_t* hdr = nullptr;
+    uint8_t* img = nullptr;
+    int32_t* st = nullptr;
+    ~Tmp() {   // (after an abort the communicator's kernels have been told to exit)
       if (s) hipStreamDestroy(s);
-      if (buf) hipFree(buf);
+      if (hdr) hipFree(hdr);
+      if (img) hipFree(img);
+      if (st) hipFree(st);
     }
   } t;
   HIP_TRY(hipStreamCreateWithFlags(&t.s, hipStreamNonBlocking));
-  // 1. header (a root without weights sends an all-zero header, so every rank fails the same way below)
+  HIP_TRY(hipMalloc(&t.hdr, sizeof(BlobHeader)));
+  HIP_TRY(hipMalloc(&t.st, sizeof(int32_t)));
+  int rc;
+#define COMM_CALL(expr, what)                                                        \
+  do {                                                                               \
+    if ((rc = comm_settle(comm, (expr), deadline, what)) != SPEF_OK) return rc;      \
+  } while (0)
+#define COMM_WAIT(what, inj)                                                         \
+  do {                                                                               \
+    if ((rc = comm_wait_stream(comm, t.s, deadline, what, inj)) != SPEF_OK) return rc; \
+  } while (0)
+  // agree on a local status word; returns the MAX over ranks (or an error: communicator aborted)
+  std::string local_msg;
+  auto agree = [&](int local_code, int32_t* agreed, int inj) -> int {
+    const int32_t w = local_code ? (int32_t)((local_code << 16) | (rank + 1)) : 0;
+    HIP_TRY(hipMemcpyAsync(t.st, &w, sizeof(w), hipMemcpyHostToDevice, t.s));
+    COMM_CALL(ncclAllReduce(t.st, t.st, 1, ncclInt32, ncclMax, comm, t.s), "status all-reduce");
+    COMM_WAIT("status all-reduce", inj);
+    HIP_TRY(hipMemcpy(agreed, t.st, sizeof(int32_t), hipMemcpyDeviceToHost));
+    return SPEF_OK;
+  };
+  auto verdict = [&](int32_t agreed) -> int {
+    const int code = agreed >> 16, bad = (agreed & 0xffff) - 1;
+    if (bad == rank) return fail(code, local_msg + " (rank " + std::to_string(rank) + ", weight broadcast)");
+    return fail(code, "weight broadcast failed on rank " + std::to_string(bad) + " (error " + std::to_string(code) +
+                          "); every rank returns it and keeps its previous model");
+  };
+
+  // 1. header (a root without weights sends an all-zero header; the receivers' checks then fail together)
   BlobHeader h{};
   if (rank == root && c->loaded) h = c->hdr;
-  const size_t meta = (rank == root && c->loaded) ? (size_t)h.data_off : 0;
-  uint8_t* dh = nullptr;
-  HIP_TRY(hipMalloc(&dh, sizeof(h)));
-  t.buf = dh;
-  HIP_TRY(hipMemcpy(dh, &h, sizeof(h), hipMemcpyHostToDevice));
-  NCCL_TRY(ncclBroadcast(dh, dh, sizeof(h), ncclUint8, root, comm, t.s));
-  HIP_TRY(hipStreamSynchronize(t.s));
-  HIP_TRY(hipMemcpy(&h, dh, sizeof(h), hipMemcpyDeviceToHost));
-  if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_STATE, "broadcast root has no weights loaded");
-  if (h.data_off > (1ull << 30) || h.data_bytes > (1ull << 36)) return fail(SPEF_ERR_BLOB, "broadcast header out of range");
-  // 2. op table + data section into a full blob image (the receivers load it like spef_load_weights_device)
-  const size_t total = (size_t)h.data_off + (size_t)h.data_bytes;
-  hipFree(t.buf);
-  t.buf = nullptr;
-  HIP_TRY(hipMalloc(&t.buf, std::max<size_t>(total, 256)));
-  uint8_t* img = t.buf;
-  HIP_TRY(hipMemcpy(img, &h, sizeof(h), hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(t.hdr, &h, sizeof(h), hipMemcpyHostToDevice));
+  COMM_CALL(ncclBroadcast(t.hdr, t.hdr, sizeof(h), ncclUint8, root, comm, t.s), "header broadcast");
+  COMM_WAIT("header broadcast", inject == 3);
+  HIP_TRY(hipMemcpy(&h, t.hdr, sizeof(h), hipMemcpyDeviceToHost));
+
+  // 2. local checks and allocation, then agreement before any bulk collective
+  int local = SPEF_OK;
   const size_t ops_bytes = (size_t)h.n_ops * sizeof(OpDesc);
-  if (h.ops_off + ops_bytes > h.data_off) return fail(SPEF_ERR_BLOB, "broadcast op table overlaps the data section");
-  if (rank == root) {
-    (void)meta;
-    HIP_TRY(hipMemcpy(img + h.ops_off, c->ops.data(), ops_bytes, hipMemcpyHostToDevice));
-    NCCL_TRY(ncclBroadcast(img + h.ops_off, img + h.ops_off, ops_bytes, ncclUint8, root, comm, t.s));
-    NCCL_TRY(ncclBroadcast(c->d_data, c->d_data, h.data_bytes, ncclUint8, root, comm, t.s));
-    HIP_TRY(hipStreamSynchronize(t.s));
-    return SPEF_OK;   // the root keeps its loaded model
+  if (memcmp(h.magic, kBlobMagic, 8) != 0) {
+    local = fail(SPEF_ERR_STATE, "broadcast root has no weights loaded");
+  } else if (h.data_off > (1ull << 30) || h.data_bytes > (1ull << 36) || h.ops_off > h.data_off ||
+             ops_bytes > h.data_off - h.ops_off) {
+    local = fail(SPEF_ERR_BLOB, "broadcast header out of range");
+  } else if (inject == 1) {
+    local = fail(SPEF_ERR_HIP, "injected failure before the data broadcast (SPEF_OPT_TEST_FAIL_BCAST=1)");
+  } else if (rank != root) {
+    const size_t total = (size_t)h.data_off + (size_t)h.data_bytes;
+    const hipError_t e = hipMalloc(&t.img, std::max<size_t>(total, 256));
+    if (e != hipSuccess) {
+      t.img = nullptr;
+      local = fail(SPEF_ERR_HIP, std::string("hipMalloc of the broadcast image: ") + hipGetErrorString(e));
+    }
   }
-  NCCL_TRY(ncclBroadcast(img + h.ops_off, img + h.ops_off, ops_bytes, ncclUint8, root, comm, t.s));
-  NCCL_TRY(ncclBroadcast(img + h.data_off, img + h.data_off, h.data_bytes, ncclUint8, root, comm, t.s));
-  HIP_TRY(hipStreamSynchronize(t.s));
-  return load_common(c, img, total, true);
+  if (local) local_msg = g_err;
+  int32_t agreed = 0;
+  if ((rc = agree(local, &agreed, 0)) != SPEF_OK) return rc;
+  if (agreed) return verdict(agreed);
+
+  // 3. op table + data section (receivers: into a full blob image they then stage like spef_load_weights_device)
+  if (rank == root) {
+    HIP_TRY(hipMalloc(&t.img, std::max<size_t>(ops_bytes, 256)));
+    HIP_TRY(hipMemcpy(t.img, c->ops.data(), ops_bytes, hipMemcpyHostToDevice));
+    COMM_CALL(ncclGroupStart(), "group start");
+    COMM_CALL(ncclBroadcast(t.img, t.img, ops_bytes, ncclUint8, root, comm, t.s), "op-table broadcast");
+    COMM_CALL(ncclBroadcast(c->d_data, c->d_data, h.data_bytes, ncclUint8, root, comm, t.s), "data broadcast");
+    COMM_CALL(ncclGroupEnd(), "group end");
+  } else {
+    HIP_TRY(hipMemcpy(t.img, &h, sizeof(h), hipMemcpyHostToDevice));
+    COMM_CALL(ncclGroupStart(), "group start");
+    COMM_CALL(ncclBroadcast(t.img + h.ops_off, t.img + h.ops_off, ops_bytes, ncclUint8, root, comm, t.s),
+              "op-table broadcast");
+    COMM_CALL(ncclBroadcast(t.img + h.data_off, t.img + h.data_off, h.data_bytes, ncclUint8, root, comm, t.s),
+              "data broadcast");
+    COMM_CALL(ncclGroupEnd(), "group end");
+  }
+  COMM_WAIT("data broadcast", 0);
+
+  // 4. receivers stage (full validation + device copy); all ranks agree before anyone commits
+  Staged st;
+  local = SPEF_OK;
+  if (inject == 2) local = fail(SPEF_ERR_BLOB, "injected failure after the data broadcast (SPEF_OPT_TEST_FAIL_BCAST=2)");
+  else if (rank != root) local = stage_blob(c, t.img, (size_t)h.data_off + (size_t)h.data_bytes, true, &st);
+  local_msg = local ? g_err : std::string();
+  if ((rc = agree(local, &agreed, 0)) != SPEF_OK) return rc;
+  if (agreed) return verdict(agreed);
+  if (rank != root) commit_staged(c, &st);   // the root keeps its loaded model
+  return SPEF_OK;
+#undef COMM_CALL
+#undef COMM_WAIT
 }
 
 int spef_model_info(const spef_ctx* c, int* head, int* n_out0, int* n_out1, int* dtype, int* n_ops) {
@@ -1349,6 +1582,11 @@ int spef_set_option(spef_ctx* c, int option, int value) {
   }
   if (option == SPEF_OPT_IRB_VARIANT) {
     c->irb_variant = value;
+    return SPEF_OK;
+  }
+  if (option == SPEF_OPT_TEST_FAIL_BCAST) {
+    if (value < 0 || value > 3) return fail(SPEF_ERR_ARG, "SPEF_OPT_TEST_FAIL_BCAST: 0..3");
+    c->test_fail_bcast = value;
     return SPEF_OK;
   }
   if (option == SPEF_OPT_PW_GEMM) {

@@ -24,12 +24,13 @@
 //   OP_QLAST w0 int8 [Np][Kp64], b0 RQ
 //   OP_QFC   w0 int8 [Np][1280] (ori rows then pos), b0 fp64 [Np] weight scales, w1 fp64 [Np] float bias,
 //            x0 int32 [Np] 128 * sum_k q_w, x1 fp64 [1] last-conv activation scale
-// qbits (bit_width.json of the reference's QMobileNetV2 / QURSONetHead, model.py:16-45; 0 means 8; 2..8 allowed):
+// qbits (bit_width.json of the reference's QMobileNetV2 / QURSONetHead, model.py:16-45; 0 means 8; 3..8 allowed):
 //   OP_QSTEM [0] first_conv activation (unsigned), [1] image (signed, f32 NCHW input path; the u8 LUT has it built in)
 //   OP_QIRB  [0] expand activation, [1] depthwise activation (unsigned), [2] shared_act (signed output quantizer)
 //   OP_QLAST [0] last_conv activation (unsigned), [1] pooling (TruncTo8bit output: shift = [0] + ceil(log2 HW) - [1])
 //   OP_QFC   [0] fully_connected bias width (signed)
-// act = the activation storage type (fp16 or bf16); Kp = K rounded up to 32, Np = N rounded up to 16, padding 0.
+// act = the activation storage type (fp16, bf16 or fp32 -- dtype 4, whose depthwise weights are fp32 as in bf16
+// blobs and whose stem x0 is fp32 hi + zero lo); Kp = K rounded up to 32, Np = N rounded up to 16, padding 0.
 // BatchNorm (eps 1e-5) is folded: w' = w*g/sqrt(v+eps), b' = beta - mean*g/sqrt(v+eps).
 #pragma once
 #include <stdint.h>
@@ -37,7 +38,7 @@
 namespace spef {
 
 static const char kBlobMagic[8] = {'S', 'P', 'E', 'F', 'M', 'I', '3', '5'};
-static const uint32_t kBlobVersion = 1;
+static const uint32_t kBlobVersion = 2;   // 2: fp16 stem operand (x0) in the front_vp_kernel row-triple k order
 static const uint64_t kAbsent = ~0ull;
 
 enum OpKind : uint32_t {

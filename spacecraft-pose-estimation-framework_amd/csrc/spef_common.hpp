@@ -44,6 +44,15 @@ struct BF16 {
   }
 };
 
+// fp32 storage (blob dtype 4, k_f32.hip): stem and depthwise kernels only (the 1x1 convs use gemm_f32_kernel)
+typedef float f32x8 __attribute__((ext_vector_type(8)));
+struct F32 {
+  using T = float;
+  using DW = float;
+  using x8 = f32x8;
+  using x4 = f32x4;
+};
+
 template <typename DT>
 __device__ __forceinline__ typename DT::x8 load8(const typename DT::T* p) {
   return *reinterpret_cast<const typename DT::x8*>(p);

@@ -6,7 +6,7 @@
 
 namespace spef {
 
-enum Dtype : int { DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3 };
+enum Dtype : int { DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3, DT_F32 = 4 };
 enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RELU_F32 = 3 /* ReLU, fp32 output */ };
 enum InLayout : int { IN_U8_NHWC = 0, IN_F32_NCHW = 1 };
 
@@ -67,6 +67,14 @@ hipError_t launch_irw(int variant, int dtype, int cin, int hid, int cout, int st
 // weights split hi + lo in the activation dtype, [2][32][32] (blob OP_STEM x0).
 hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* bs, const void* wd, const float* bd,
                         const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
+
+// fp32 schedule (k_f32.hip, blob dtype 4): 1x1 conv on the exact fp32 MFMA, same contract as launch_pw with fp32
+// activations and weights ([Np][Kp] fp32); EPI_RELU_F32 = EPI_RELU. K % 4 == 0, N % 4 == 0.
+hipError_t launch_gemm_f32(int epi, const void* x, const void* wt, const float* bias, const void* r, void* y,
+                           int64_t M, int K, int N, hipStream_t s);
+const char* gemm_f32_key(int N);
+// URSONetHead mean([2,3]) over an fp32 NHWC map: pooled [B][C].
+hipError_t launch_mean_hw(const float* x, float* pooled, int B, int HW, int C, hipStream_t s);
 
 // Split-K fp32 head GEMM for very long K: part = workspace [splits][B][round_up(n,16)] floats.
 hipError_t launch_fc_splitk(const float* x, const float* w, const float* bias, float* out, int n, int B, int K,

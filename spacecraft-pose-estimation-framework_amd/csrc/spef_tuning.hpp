@@ -4,10 +4,14 @@
 //                         GEMM + depthwise + GEMM).
 //   SPEF_OPT_PW_GEMM    : LDS-tiled MFMA GEMM (1, default) or register-direct kernel (0) for unfused 1x1 convs.
 //   SPEF_OPT_IRB_VARIANT: fused-block tile variant (0 = tuned default).
+//   SPEF_OPT_TEST_FAIL_BCAST: failure injection for spef_bcast_weights tests: 1 = this rank fails its local check
+//                         before the data broadcast, 2 = fails staging after it, 3 = the header wait never completes
+//                         (exercises the timeout -> ncclCommAbort path without a hung peer). 0 = off.
 #pragma once
 
 enum spef_tuning_option {
   SPEF_OPT_FUSE_MIN_HW = 2,
   SPEF_OPT_PW_GEMM = 3,
-  SPEF_OPT_IRB_VARIANT = 4
+  SPEF_OPT_IRB_VARIANT = 4,
+  SPEF_OPT_TEST_FAIL_BCAST = 5
 };

@@ -9,13 +9,13 @@ import os
 
 from . import _build
 
-OK, ERR_ARG, ERR_HIP, ERR_BLOB, ERR_STATE, ERR_NUMERIC = range(6)
+OK, ERR_ARG, ERR_HIP, ERR_BLOB, ERR_STATE, ERR_NUMERIC, ERR_COMM = range(7)
 IN_U8_NHWC, IN_F32_NCHW = 0, 1
 REGRESSION, CLASSIFICATION, KEYPOINTS = 0, 1, 2
-ABI_VERSION = 2
+ABI_VERSION = 3
 COMM_ID_BYTES = 128
 OPT_FUSE_BLOCKS, OPT_WAVESPEC = 1, 6                          # public schedule options (include/spef.h)
-OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT = 2, 3, 4       # internal tuning knobs (csrc/spef_tuning.hpp)
+OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT, OPT_TEST_FAIL_BCAST = 2, 3, 4, 5   # internal (csrc/spef_tuning.hpp)
 
 # name -> (restype, argtypes); keep in sync with include/spef.h (tests/test_abi.py checks the header)
 _vp, _i, _sz = C.c_void_p, C.c_int, C.c_size_t
@@ -37,7 +37,8 @@ SIGNATURES = {
     'spef_decode': (_i, [_vp, _i, _i, _vp, _i, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp, _vp]),
     'spef_validate_blob': (_i, [_vp, _sz, _ip, _ip, _ip, _ip]),
     'spef_comm_unique_id': (_i, [_vp, _sz]),
-    'spef_comm_init': (_i, [_i, _i, _i, _vp, C.POINTER(_vp)]),
+    'spef_comm_init': (_i, [_i, _i, _i, _vp, _i, C.POINTER(_vp)]),
+    'spef_comm_abort': (_i, [_vp]),
     'spef_comm_destroy': (_i, [_vp]),
     'spef_bcast_weights': (_i, [_vp, _vp, _i]),
     'spef_set_option': (_i, [_vp, _i, _i]),
@@ -63,6 +64,10 @@ def load(path: str | None = None) -> C.CDLL:
     global _LIB
     if _LIB is not None:
         return _LIB
+    # torch first: its bundled libamdhip64 (SONAME libamdhip64.so.7) then satisfies this library's dependency, so
+    # the process holds ONE HIP runtime. Loaded the other way round, torch's libraries pull in their own copy next
+    # to /opt/rocm's (they name the unversioned file) and the two runtimes' teardown double-frees at exit.
+    import torch  # noqa: F401
     override = path or os.environ.get('SPEF_LIB')    # SPEF_LIB: A/B timing of two builds (tools/ab.py)
     path = override or _build.lib_path()
     if not os.path.exists(path):

@@ -21,8 +21,8 @@ import numpy as np
 from .arch import Arch, BN_EPS, ConvSpec, LAST_CHANNELS, arch_from_state_dict, mobilenet_v2
 
 MAGIC = b'SPEFMI35'
-VERSION = 1
-DTYPES = {'fp16': 1, 'bf16': 2}
+VERSION = 2   # 2: fp16 stem MFMA operand in the front_vp_kernel row-triple k order (csrc/spef_blob.hpp)
+DTYPES = {'fp16': 1, 'bf16': 2, 'fp32': 4}   # fp32: the reference's own arithmetic (k_f32.hip schedule)
 DT_I8 = 3
 OP_STEM, OP_IRB, OP_LAST, OP_FC, OP_FCKP = 1, 2, 3, 4, 5
 OP_QSTEM, OP_QIRB, OP_QLAST, OP_QFC = 11, 12, 13, 14
@@ -54,6 +54,8 @@ def _to_act(a: np.ndarray, dtype: str) -> bytes:
     a = np.ascontiguousarray(a, dtype=np.float32)
     if dtype == 'fp16':
         return a.astype(np.float16).tobytes()
+    if dtype == 'fp32':
+        return a.tobytes()
     # bf16: round-to-nearest-even on the fp32 bits (finite weights only)
     u = a.view(np.uint32).astype(np.uint64)
     r = ((u + 0x7FFF + ((u >> 16) & 1)) >> 16).astype(np.uint16)
@@ -65,6 +67,8 @@ def _round_act(a: np.ndarray, dtype: str) -> np.ndarray:
     a = np.ascontiguousarray(a, dtype=np.float32)
     if dtype == 'fp16':
         return a.astype(np.float16).astype(np.float32)
+    if dtype == 'fp32':
+        return a
     return np.frombuffer(_to_act(a, 'bf16'), np.uint16).astype(np.uint32).__lshift__(16).view(np.float32).reshape(a.shape)
 
 

@@ -58,9 +58,11 @@ class RcclComm:
 
     Rank 0 draws the 128-byte unique id (``spef_comm_unique_id``); the id travels to the other ranks over the
     already-initialised torch.distributed group (``broadcast_object_list``: any backend), the way a C host would ship
-    it over MPI or a file. ``int(comm)`` is the ncclComm_t handle."""
+    it over MPI or a file. ``int(comm)`` is the ncclComm_t handle. The communicator is nonblocking and every wait on
+    it is bounded by ``timeout_ms``: a dead peer makes ``spef_bcast_weights`` abort it (``SpefError`` code
+    ``ERR_COMM``) instead of hanging."""
 
-    def __init__(self, device: torch.device):
+    def __init__(self, device: torch.device, timeout_ms: int = 120_000):
         import ctypes as C
         from . import _lib as L
         self.lib = L.load()
@@ -74,11 +76,16 @@ class RcclComm:
             dist.broadcast_object_list(idbuf, src=0)
         rid = C.create_string_buffer(bytes(idbuf[0]), L.COMM_ID_BYTES)
         h = C.c_void_p()
-        L.check(self.lib.spef_comm_init(torch.device(device).index or 0, ws, rank, rid, C.byref(h)))
+        L.check(self.lib.spef_comm_init(torch.device(device).index or 0, ws, rank, rid, int(timeout_ms), C.byref(h)))
         self.handle = h.value
 
     def __int__(self) -> int:
         return int(self.handle)
+
+    def abort(self) -> None:
+        """ncclCommAbort (e.g. when the launcher learns that a peer died); the handle is dead afterwards."""
+        if self.handle:
+            self.lib.spef_comm_abort(self.handle)
 
     def close(self) -> None:
         if self.handle:

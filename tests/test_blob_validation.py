@@ -76,3 +76,36 @@ def test_head_width_mismatch_rejected(fp16_blob):
     struct.pack_into('<I', b, 24, 1232)                          # header n_out0 != FC rows - 3
     rc, _, msg = _validate(bytes(b))
     assert rc == L.ERR_BLOB and 'head' in msg, msg
+
+
+def test_ops_offset_overflow_rejected(fp16_blob):
+    """ops_off near 2^64 must not wrap ops_off + n_ops * 128 into range (the memcpy would read before the buffer)."""
+    b = bytearray(fp16_blob)
+    struct.pack_into('<Q', b, 48, 0xFFFFFFFFFFFFFFC0)             # header ops_off (after 8s + 10 uint32)
+    rc, _, msg = _validate(bytes(b))
+    assert rc == L.ERR_BLOB and 'truncated' in msg, msg
+
+
+def test_old_blob_version_rejected(fp16_blob):
+    """Version 1 blobs hold the fp16 stem operand in the old k order: they must fail to load, not run wrongly."""
+    assert struct.unpack_from('<I', fp16_blob, 8)[0] == Bl.VERSION == 2
+    b = bytearray(fp16_blob)
+    struct.pack_into('<I', b, 8, 1)
+    rc, _, msg = _validate(bytes(b))
+    assert rc == L.ERR_BLOB and 'version' in msg, msg
+
+
+@pytest.mark.parametrize('bits', [1, 2, 9])
+def test_int8_qbits_outside_3_to_8_rejected(bits):
+    """The C validator and quant.check_bit_width agree: widths 1-2 (Brevitas binary / ternary quantizers,
+    quantizers.py:85-88) change the arithmetic, so only 0 (= 8) or 3..8 are accepted."""
+    from spef_amd.blob_q8 import pack_int8
+    from spef_amd.data.synthetic import synth_frames
+    from spef_amd.quant import calibrate
+    sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=3)
+    good = pack_int8(sd, calibrate(sd, synth_frames(2, 64, 64, 900)))
+    info = Bl.describe(good)
+    b = bytearray(good)
+    struct.pack_into('<B', b, info['ops_off'] + 1 * 128 + 104, bits)   # op 1 (first QIRB): qbits[0]
+    rc, _, msg = _validate(bytes(b))
+    assert rc == L.ERR_BLOB and 'bit widths' in msg, msg

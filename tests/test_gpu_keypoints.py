@@ -13,12 +13,30 @@ from spef_amd.weights import synthetic_state_dict
 pytestmark = pytest.mark.gpu
 
 
+KP_TOL = 1e-3        # north_star: raw head outputs within 1e-3 of the float32 reference (fp32 keypoint blobs)
+KP_TOL_FP16 = 2e-3   # the fp16 fast variant: the unpooled 122,880-wide head sees fp16 storage noise
+
+
 @pytest.fixture(scope='module')
-def kp_engine():
+def kp_sd():
+    return synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=0.002)
+
+
+@pytest.fixture(scope='module')
+def kp_engine(kp_sd):
+    """The keypoint parity variant: fp32 blob (k_f32.hip schedule, exact-fp32 MFMA) -- build_mi355x's default for
+    keypoint experiments."""
     from spef_amd.engine import Engine
-    sd = synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=0.002)
-    e = Engine(Bl.pack(sd, mobilenet_v2('keypoints'), dtype='fp16'), 'cuda:0')
-    yield e, sd
+    e = Engine(Bl.pack(kp_sd, mobilenet_v2('keypoints'), dtype='fp32'), 'cuda:0')
+    yield e, kp_sd
+    e.close()
+
+
+@pytest.fixture(scope='module')
+def kp_engine16(kp_sd):
+    from spef_amd.engine import Engine
+    e = Engine(Bl.pack(kp_sd, mobilenet_v2('keypoints'), dtype='fp16'), 'cuda:0')
+    yield e, kp_sd
     e.close()
 
 
@@ -108,34 +126,46 @@ def test_sigmoid_then_epnp(kp_engine, golden):
 
 
 def test_keypoint_head_forward(kp_engine):
-    """KeypointRegressionHead (flatten NCHW -> Linear 122880 -> 24) at 240x384 vs the oracle.
-
-    Tolerance 2e-3 abs (not the pooled heads' 1e-3): every layer's activations are rounded to fp16 for the MFMA
-    operands (~2.4e-4 relative per layer, 52 layers) and this head sums 122,880 unpooled features, so none of
-    that rounding noise is averaged away; measured max 1.17e-3 on outputs of magnitude ~0.8. The last conv
-    writes fp32 (EPI_RELU_F32) so the head adds no rounding of its own. See DESIGN.md "Precision"."""
+    """KeypointRegressionHead (flatten NCHW -> Linear 122880 -> 24) at 240x384 vs the oracle, fp32 blob: within the
+    north-star 1e-3 (measured ~1e-6: the same fp32 products, only the summation order differs)."""
     eng, sd = kp_engine
     rng = np.random.Generator(np.random.PCG64(5))
     fr = rng.integers(0, 256, (3, 240, 384, 3), dtype=np.uint8)
     raw, _ = eng.forward(torch.from_numpy(fr).cuda())
     ref = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd, head='keypoints')
-    assert np.abs(raw.cpu().numpy() - ref.numpy()).max() < 2e-3
+    assert np.abs(raw.cpu().numpy() - ref.numpy()).max() < KP_TOL
 
 
 def test_keypoint_head_vs_reference_fixture(kp_engine, golden):
     """Raw outputs and keypoint-mode sigmoid against the reference's own ModelWrapper(MobileNetV2,
-    KeypointRegressionHead) (tests/golden/kp_head_240x384_b2.npz, generated by importing the reference).
-    Bound 2e-3 on raw outputs of magnitude ~0.7: see test_keypoint_head_forward and DESIGN.md section 5 for the
-    measured fp16 error budget of this unpooled 122,880-wide head."""
+    KeypointRegressionHead) (tests/golden/kp_head_240x384_b2.npz, generated by importing the reference), fp32 blob:
+    within the north-star 1e-3."""
     from spef_amd.weights import state_dict_digest
     eng, sd = kp_engine
     g = golden('kp_head_240x384_b2.npz')
     assert state_dict_digest(sd) == str(g['digest'])
     raw, _ = eng.forward(torch.from_numpy(g['frames']).cuda())
     raw = raw.cpu().numpy()
-    assert np.abs(raw - g['raw']).max() < 2e-3
+    assert np.abs(raw - g['raw']).max() < KP_TOL
     out = eng.decode_keypoints(torch.from_numpy(raw).cuda(), apply_sigmoid=True)
-    assert np.abs(out['keypoints'].cpu().numpy() - g['sigmoid']).max() < 5e-4     # sigmoid' <= 1/4
+    assert np.abs(out['keypoints'].cpu().numpy() - g['sigmoid']).max() < KP_TOL / 4     # sigmoid' <= 1/4
+
+
+def test_keypoint_head_fp16_fast_variant(kp_engine16, golden):
+    """fp16 keypoint blob (fused kernels, the URSONet speed path): stated bound 2e-3 on raw outputs of magnitude
+    ~0.8 (measured 1.17e-3). The URSONet heads average fp16 storage rounding over 256 pixels before their FC; this
+    head reads all 122,880 values individually. tools/kp_error_budget.py splits the budget by rounding class: no class
+    dominates (weights 9.0e-4, block outputs 8.3e-4, hidden 5.0e-4, depthwise out 4.4e-4 alone), so fp32 storage, not a
+    targeted fix, is what reaches 1e-3 -- the fp32 blob above."""
+    eng, sd = kp_engine16
+    g = golden('kp_head_240x384_b2.npz')
+    raw, _ = eng.forward(torch.from_numpy(g['frames']).cuda())
+    assert np.abs(raw.cpu().numpy() - g['raw']).max() < KP_TOL_FP16
+    rng = np.random.Generator(np.random.PCG64(5))
+    fr = rng.integers(0, 256, (3, 240, 384, 3), dtype=np.uint8)
+    raw, _ = eng.forward(torch.from_numpy(fr).cuda())
+    ref = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd, head='keypoints')
+    assert np.abs(raw.cpu().numpy() - ref.numpy()).max() < KP_TOL_FP16
 
 
 def test_predict_keypoint_mode(kp_engine, golden):
@@ -156,7 +186,7 @@ def test_predict_keypoint_mode(kp_engine, golden):
     pose, lat = spe.predict(x)
     assert set(pose) == {'keypoints', 'ori', 'pos'} and lat > 0
     ref = D.sigmoid_f32(M.forward(x, sd, head='keypoints').numpy())
-    assert np.abs(pose['keypoints'] - ref).max() < 5e-4   # sigmoid' <= 1/4 of the 2e-3 logit tolerance
+    assert np.abs(pose['keypoints'] - ref).max() < KP_TOL / 4   # sigmoid' <= 1/4
     chk = eng.decode_keypoints(torch.from_numpy(pose['keypoints']).cuda(), apply_sigmoid=False)
     np.testing.assert_array_equal(chk['ori'].cpu().numpy(), pose['ori'])
     np.testing.assert_array_equal(chk['pos'].cpu().numpy(), pose['pos'])

@@ -17,7 +17,7 @@ from spef_amd.weights import synthetic_state_dict
 pytestmark = pytest.mark.gpu
 
 LOGIT_TOL = 1e-3          # north_star: outputs within 1e-3 of the FP32 reference
-LOGIT_TOL_BF16 = 4e-3     # bf16 storage variant (SURVEY §7 hard part 3 measured 1.1e-3 on a harsher net)
+LOGIT_TOL_BF16 = 6e-3     # bf16 storage variant: 2x the 3.1e-3 measured over 32 x 1731 logits at C2 (test_gpu_c2_precision)
 
 
 @pytest.fixture(scope='module')
@@ -253,3 +253,25 @@ def test_role_split_blocks_bit_identical_to_slab(engine, b, h, w):
                     op, mode, np.abs(outs[0].astype(np.float32) - outs[mode].astype(np.float32)).max())
     finally:
         engine.set_option(L.OPT_WAVESPEC, 2)
+
+
+def test_fp32_variant_vs_reference_golden(sd, golden):
+    """fp32 blob (k_f32.hip: exact-fp32 MFMA, one kernel per conv): the reference's own arithmetic, so the head
+    outputs agree with the reference's fixtures to fp32 summation-order noise."""
+    from spef_amd.engine import Engine
+    e = Engine(Bl.pack(sd, dtype='fp32'), 'cuda:0')
+    try:
+        for name in ('fwd_64x64_b2.npz', 'fwd_240x384_b1.npz', 'fwd_512x512_b1.npz'):
+            g = golden(name)
+            for x in (torch.from_numpy(g['frames']).cuda(), M.u8_nhwc_to_nchw_f32(g['frames']).contiguous().cuda()):
+                ori, pos = e.forward(x)
+                d = max(np.abs(ori.cpu().numpy() - g['ori']).max(), np.abs(pos.cpu().numpy() - g['pos']).max())
+                assert d < 1e-4, (name, d)
+        fr = _frames(2, 96, 128, 5)
+        x = M.u8_nhwc_to_nchw_f32(fr)
+        for op in (0, 1, 2, 7, 17):
+            ref = M.backbone(x, sd, upto=op).permute(0, 2, 3, 1).numpy()
+            got = e.probe(torch.from_numpy(fr).cuda(), op).cpu().numpy()
+            assert np.abs(got - ref).max() / np.abs(ref).max() < 1e-5, op
+    finally:
+        e.close()

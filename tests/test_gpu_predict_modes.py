@@ -171,3 +171,45 @@ def test_rccl_weight_broadcast_single_rank(blob16):
         a.close()
         empty.close()
         comm.close()
+
+
+def test_rccl_weight_broadcast_injected_failures(blob16):
+    """Deadlock-free spef_bcast_weights: a rank that fails its local check before the data broadcast
+    (SPEF_OPT_TEST_FAIL_BCAST=1) or its staging after it (=2) makes the collective return that error -- naming the
+    failing rank -- instead of leaving the other ranks blocked in a broadcast, the context keeps its model and the
+    communicator stays usable; a wait that never completes (=3) ends at the communicator's timeout in
+    ncclCommAbort (ERR_COMM), after which the handle refuses further collectives and closes cleanly."""
+    import time
+    from spef_amd.engine import Engine
+    from spef_amd.shard import RcclComm
+    dev = torch.device('cuda:0')
+    fr = torch.from_numpy(np.random.default_rng(3).integers(0, 256, (2, 64, 96, 3), dtype=np.uint8)).cuda()
+    a = Engine(blob16, dev)
+    comm = RcclComm(dev, timeout_ms=1500)
+    try:
+        o0, p0 = a.forward(fr)
+        a.set_option(L.OPT_TEST_FAIL_BCAST, 1)
+        with pytest.raises(L.SpefError, match='rank 0') as e1:
+            a.bcast_weights(comm, 0)
+        assert e1.value.code == L.ERR_HIP
+        a.set_option(L.OPT_TEST_FAIL_BCAST, 2)
+        with pytest.raises(L.SpefError, match='rank 0') as e2:
+            a.bcast_weights(comm, 0)
+        assert e2.value.code == L.ERR_BLOB
+        a.set_option(L.OPT_TEST_FAIL_BCAST, 0)
+        a.bcast_weights(comm, 0)                          # the communicator survived both failures
+        o1, p1 = a.forward(fr)
+        assert torch.equal(o0, o1) and torch.equal(p0, p1)
+        a.set_option(L.OPT_TEST_FAIL_BCAST, 3)
+        t0 = time.perf_counter()
+        with pytest.raises(L.SpefError, match='timed out') as e3:
+            a.bcast_weights(comm, 0)
+        assert e3.value.code == L.ERR_COMM and time.perf_counter() - t0 < 30
+        a.set_option(L.OPT_TEST_FAIL_BCAST, 0)
+        with pytest.raises(L.SpefError, match='aborted'):
+            a.bcast_weights(comm, 0)
+        o2, p2 = a.forward(fr)                            # the model is untouched by the aborted collective
+        assert torch.equal(o0, o2) and torch.equal(p0, p2)
+    finally:
+        comm.close()
+        a.close()
