@@ -33,6 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, 'spacecraft-pose-estimation-framework_amd'
 sys.path.insert(0, ROOT)
 
 from spef_amd.data.synthetic import synth_frames  # noqa: E402  (SPEED-style frames)
+from spef_amd.measure import ClockProbe, measure_peaks  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 MFMA_PEAK_TFLOPS = 2500.0      # dense fp16/bf16 MFMA, no sparsity (int8: 2x)
@@ -42,6 +43,9 @@ INT8_TOLERANCE = ('int8 contract: bit-exact vs the integer oracle (oracle/int8_r
                   'reference), not by the kernels: its own bound is logits 0.05, pose 0.25 deg / 30 mm (DESIGN.md '
                   'section 5), not the fp16 1e-3 / 0.1 deg / 1 mm')
 INT8_BOUND = (0.05, 0.030, 0.25)   # logits, position (m), orientation (deg)
+# committed rocprofv3 FETCH_SIZE / WRITE_SIZE summaries, newest first (profiles/)
+FP16_TRAFFIC = ['r03_pmc_traffic.json', 'r02g_pmc_traffic.json']
+INT8_TRAFFIC = ['r03_int8_pmc_traffic.json', 'r02_int8_pmc_traffic.json']
 
 
 def pmc_traffic(kernel_key: str, path: str):
@@ -175,11 +179,16 @@ def device_batches(B, S, first, n_buf, dev):
     return [base] + [torch.roll(base, shifts=(37 * k, 53 * k), dims=(1, 2)).contiguous() for k in range(1, n_buf)]
 
 
-def time_steps(step, n_warm, n_steps, sync, barrier):
+def time_steps(step, n_warm, n_steps, sync, barrier, probe=None):
+    """W warm-up steps, then exactly K timed steps bracketed by barrier + device sync on both sides. ``probe``
+    (measure.ClockProbe) stamps the shader clock just outside the bracket (its kernels are synchronised before t0
+    and launched after t1)."""
     for i in range(n_warm):
         step(i)
     sync()
     barrier()
+    if probe is not None:
+        probe.start()
     sync()
     t0 = time.perf_counter()
     out = None
@@ -188,11 +197,15 @@ def time_steps(step, n_warm, n_steps, sync, barrier):
     sync()
     barrier()
     sync()
-    return time.perf_counter() - t0, out
+    el = time.perf_counter() - t0
+    if probe is not None:
+        probe.stop()
+    return el, out
 
 
-def roofline(prof, steps, B, traffic_path):
-    """Dominant kernel (longest per step): MFMA bound (SURVEY §8d headline) with the HBM figure beside it."""
+def roofline(prof, steps, B, traffic_path, peaks=None, int8=False):
+    """Dominant kernel (longest per step): MFMA bound (SURVEY §8d headline) with the HBM figure beside it; ``frac``
+    against the nominal peak, ``frac_measured`` against the peak measured on this box (measure.measure_peaks)."""
     dom_key = max(prof, key=lambda k: prof[k][1])
     n, ms, byts, fl = prof[dom_key]
     avg_s = ms / n / 1e3
@@ -201,7 +214,7 @@ def roofline(prof, steps, B, traffic_path):
     traffic = pmc_traffic(dom_key, traffic_path)
     if traffic is not None:
         traffic *= B / 64.0     # the PMC passes ran batch 64 (tools/pmc.sh); bytes scale with the batch
-    return {'bound': 'mfma', 'kernel': dom_key, 'achieved': round(ach_tfl, 2), 'peak': MFMA_PEAK_TFLOPS,
+    rec = {'bound': 'mfma', 'kernel': dom_key, 'achieved': round(ach_tfl, 2), 'peak': MFMA_PEAK_TFLOPS,
             'unit': 'TFLOP/s', 'frac': round(ach_tfl / MFMA_PEAK_TFLOPS, 4),
             'traffic': None if traffic is None else round(traffic),
             'traffic_source': os.path.relpath(traffic_path, ROOT) if traffic is not None else None,
@@ -209,6 +222,15 @@ def roofline(prof, steps, B, traffic_path):
             'avg_launch_us': round(avg_s * 1e6, 2), 'launches_per_step': n / steps,
             'hbm': {'achieved': round(ach_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                     'frac': round(ach_gbs / HBM_PEAK_GBS, 4)}}
+    if int8:
+        rec['peak'], rec['unit'] = 2 * MFMA_PEAK_TFLOPS, 'TOP/s'
+        rec['frac'] = round(ach_tfl / rec['peak'], 4)
+    if peaks:
+        pm = peaks['int8_mfma_tops' if int8 else 'fp16_mfma_tflops']
+        rec['peak_measured'], rec['frac_measured'] = pm, round(ach_tfl / pm, 4) if pm else None
+        hm = peaks['hbm_read_gbs']
+        rec['hbm']['peak_measured'], rec['hbm']['frac_measured'] = hm, round(ach_gbs / hm, 4) if hm else None
+    return rec
 
 
 def kernel_table(prof, steps):
@@ -224,7 +246,7 @@ def newest_profile(names):
     return next((p for p in paths if os.path.exists(p)), paths[-1])
 
 
-def run_int8(args, sd, dev, frames, ref):
+def run_int8(args, sd, dev, frames, ref, peaks=None):
     """C5 sub-record: the INT8 (Brevitas-mirroring) path at the same workload, same timing protocol (N=1)."""
     import torch
     from spef_amd import _lib as L
@@ -241,7 +263,8 @@ def run_int8(args, sd, dev, frames, ref):
     def step(i):
         return pipe.submit(frames[i % len(frames)], L.CLASSIFICATION, L.REGRESSION, want_soft=True)
     sync = lambda: (pipe.synchronize(), torch.cuda.synchronize(dev))   # noqa: E731
-    el, _ = time_steps(step, args.warmup, args.steps, sync, lambda: None)
+    probe = ClockProbe(dev)
+    el, _ = time_steps(step, args.warmup, args.steps, sync, lambda: None, probe)
     eng = pipe.engine
     eng.profile_begin()
     for i in range(args.steps):
@@ -250,14 +273,89 @@ def run_int8(args, sd, dev, frames, ref):
     prof = eng.profile_end()
     rec = {'workload': f'C5: INT8 (Brevitas-mirroring, PTQ-calibrated scales) full net + decode, {S}x{S}, batch {B}',
            'value': round(B * args.steps / el, 2), 'unit': 'images/sec', 'ms_per_step': round(el / args.steps * 1e3, 4),
-           'dtype': 'int8', 'roofline_kernel': roofline(prof, args.steps, B, newest_profile(
-               ['r02_int8_pmc_traffic.json', 'r01_int8_pmc_traffic.json']))}
-    rec['roofline_kernel']['peak'] = 2 * MFMA_PEAK_TFLOPS
-    rec['roofline_kernel']['unit'] = 'TOP/s'
-    rec['roofline_kernel']['frac'] = round(rec['roofline_kernel']['achieved'] / (2 * MFMA_PEAK_TFLOPS), 4)
+           'dtype': 'int8', 'sclk_timed_region': probe.mhz(),
+           'roofline_kernel': roofline(prof, args.steps, B, newest_profile(INT8_TRAFFIC), peaks, int8=True)}
     if ref is not None:
         rec['pose_err_vs_fp32'] = pose_error(eng, dev, *ref, tolerance=INT8_TOLERANCE)
     pipe.close()
+    return rec
+
+
+def run_keypoint(args, dev, with_ref: bool):
+    """Keypoint mode of C3: KeypointRegressionHead (only defined at 240x384, keypoints.py:20) +
+    sigmoid + batched EPnP, batch ``args.batch``; the fp32 blob (the parity variant, build_mi355x's keypoint
+    default) and the fp16 fast variant, each with img/s and pose error against the FP32 oracle (forward + EPnP
+    restatement) on the same frames. Plus EPnP alone at 512 problems per launch (problems/s, kernel time from HIP
+    events) on the reference's own projections of valid.json poses (tests/golden/keypoints.npz)."""
+    import numpy as np
+    import torch
+    from spef_amd import blob as Bl
+    from spef_amd.arch import mobilenet_v2
+    from spef_amd.engine import Engine
+    from spef_amd.weights import synthetic_state_dict
+    g = np.load(os.path.join(ROOT, 'tests', 'golden', 'keypoints.npz'))
+    kp3d, K, nu, nv = g['kp3d'], g['K'], float(g['nu']), float(g['nv'])
+    arch = mobilenet_v2('keypoints')
+    sd = synthetic_state_dict(arch, seed=1001, head_std=0.002)
+    B, H, W = args.batch, 240, 384
+    fr = synth_frames(B, H, W, 20_000)
+    xg = torch.from_numpy(fr).to(dev)
+    rec = {'workload': f'C3 keypoint mode: MobileNetV2 + KeypointRegressionHead + sigmoid + batched EPnP, {H}x{W}, '
+                       f'batch {B} (uint8 frames resident in HBM, one stream)'}
+    ref = None
+    if with_ref:
+        from oracle import decode_ref as D
+        from oracle import epnp_ref as E
+        from oracle import model_ref as M
+        raw_ref = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd, head='keypoints').numpy()
+        rq, rt = E.decode_batch(D.sigmoid_f32(raw_ref), kp3d, K)
+        ref = (raw_ref, rq, rt, D)
+    for dtype in ('fp32', 'fp16'):
+        eng = Engine(Bl.pack(sd, arch, dtype=dtype), dev)
+        eng.set_keypoints(kp3d, K, nu, nv)
+        eng.reserve(B, H, W)
+
+        def step(i):
+            raw, _ = eng.forward(xg)
+            return raw, eng.decode_keypoints(raw)
+        sync = lambda: torch.cuda.synchronize(dev)   # noqa: E731
+        el, (raw, out) = time_steps(step, max(2, args.warmup // 2), max(5, args.steps // 4), sync, lambda: None)
+        n = max(5, args.steps // 4)
+        r = {'value': round(B * n / el, 2), 'unit': 'images/sec', 'ms_per_step': round(el / n * 1e3, 4), 'steps': n}
+        if ref is not None:
+            raw_ref, rq, rt, D = ref
+            ang = D.angle_deg_stable(out['ori'].cpu().numpy().astype(np.float64), rq)
+            dt = np.linalg.norm(out['pos'].cpu().numpy().astype(np.float64) - rt, axis=1)
+            r['pose_err_vs_fp32'] = {'raw_max_abs': float(np.abs(raw.cpu().numpy() - raw_ref).max()),
+                                     'ori_max_deg': float(ang.max()), 'ori_median_deg': float(np.median(ang)),
+                                     'pos_max_m': float(dt.max()), 'pos_median_m': float(np.median(dt))}
+            r['pose_err_vs_fp32']['within_tolerance'] = bool(r['pose_err_vs_fp32']['raw_max_abs'] < 1e-3 and
+                                                             ang.max() < 0.1 and dt.max() < 1e-3)
+        rec[dtype] = r
+        if dtype == 'fp32':   # EPnP alone: 512 problems per launch
+            P = 512
+            kp = torch.from_numpy(np.ascontiguousarray(g['kp2d'][:P], np.float32)).to(dev)
+            o = eng.decode_keypoints(kp, apply_sigmoid=False)
+            torch.cuda.synchronize(dev)
+            from spef_amd.quaternion import angle_deg
+            kat_deg = float(np.max(angle_deg(o['ori'].cpu().numpy(), g['q'][:P])))
+            n_l = 100
+            eng.profile_begin()
+            t0 = time.perf_counter()
+            for _ in range(n_l):
+                eng.decode_keypoints(kp, apply_sigmoid=False)
+            torch.cuda.synchronize(dev)
+            wall = time.perf_counter() - t0
+            prof = eng.profile_end()
+            kn, kms = prof['epnp_kernel'][0], prof['epnp_kernel'][1]
+            rec['epnp'] = {'problems_per_launch': P, 'launches': n_l, 'unit': 'problems/sec',
+                           'value': round(P * kn / (kms / 1e3), 1), 'kernel_us_per_launch': round(kms / kn * 1e3, 2),
+                           'value_wall': round(P * n_l / wall, 1),
+                           'kat_max_ori_deg': kat_deg,
+                           'kat_max_pos_m': float(np.linalg.norm(o['pos'].cpu().numpy() - g['t'][:P], axis=1).max()),
+                           'sample': 'noise-free reference projections of the first 512 valid.json poses '
+                                     '(tests/golden/keypoints.npz, KeyPoints.project of the reference)'}
+        eng.close()
     return rec
 
 
@@ -276,19 +374,19 @@ def main():
                     help='distinct device batches the timed steps rotate over (6 x 50 MB > 256 MB Infinity Cache)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-int8', action='store_true', help='skip the C5 (int8) sub-record')
+    ap.add_argument('--no-keypoint', action='store_true', help='skip the keypoint-mode / EPnP sub-record')
+    ap.add_argument('--no-peaks', action='store_true', help='skip the on-box peak microbenchmark')
     ap.add_argument('--cpu-threads', type=int, default=0, help='0 = one socket\'s physical cores (capped by quota)')
     ap.add_argument('--cpu-batch', type=int, default=64)
     ap.add_argument('--traffic', default=None,
-                    help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic (default: '
-                         'profiles/r02g_pmc_traffic.json, r02_int8_pmc_traffic.json for --dtype int8)')
+                    help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic (default: the newest '
+                         'committed profiles/*_pmc_traffic.json of the path)')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU + gloo: the distributed control flow (weight distribution, timing, max over ranks, '
                          'JSON) without device work')
     args = ap.parse_args()
     if args.traffic is None:   # the newest committed FETCH/WRITE summary of this path
-        args.traffic = newest_profile(
-            ['r02_int8_pmc_traffic.json', 'r01_int8_pmc_traffic.json'] if args.dtype == 'int8' else
-            ['r02g_pmc_traffic.json', 'r02f_pmc_traffic.json', 'r02e_pmc_traffic.json', 'r02d_pmc_traffic.json', 'r02c_pmc_traffic.json', 'r02b_pmc_traffic.json', 'r02_pmc_traffic.json'])
+        args.traffic = newest_profile(INT8_TRAFFIC if args.dtype == 'int8' else FP16_TRAFFIC)
 
     import torch
     import torch.distributed as dist
@@ -358,7 +456,14 @@ def main():
             pipe.synchronize()
             torch.cuda.synchronize(dev)
 
-    elapsed, out = time_steps(step, args.warmup, args.steps, sync, barrier)
+    peaks = None
+    probe = None
+    if not args.dry_run:
+        if rank == 0 and not args.no_peaks:
+            peaks = measure_peaks(local)                   # < 1 s, before the warm-up
+        probe = ClockProbe(dev)
+        barrier()
+    elapsed, out = time_steps(step, args.warmup, args.steps, sync, barrier, probe)
     elapsed = max_over_ranks(elapsed, dev)
     assert not out['status'].any().item(), 'decode reported NaN'
 
@@ -396,13 +501,16 @@ def main():
                        'inflight_batches': max(1, args.inflight), 'frame_buffers': max(1, args.frame_buffers)},
             'mfma_utilisation_whole_net': round(fpi * value / world / 1e12 / peak, 5),
         }
+        if peaks:
+            pm = peaks['int8_mfma_tops' if args.dtype == 'int8' else 'fp16_mfma_tflops']
+            rec['mfma_utilisation_whole_net_measured_peak'] = round(fpi * value / world / 1e12 / pm, 5)
+            rec['peak_measured'] = peaks
+        if probe is not None:
+            rec['sclk_timed_region'] = probe.mhz()
         if args.dry_run:
             rec['dry_run'] = True
         else:
-            rec['roofline'] = roofline(prof, args.steps, B, args.traffic)
-            if args.dtype == 'int8':
-                rec['roofline']['peak'], rec['roofline']['unit'] = peak, 'TOP/s'
-                rec['roofline']['frac'] = round(rec['roofline']['achieved'] / peak, 4)
+            rec['roofline'] = roofline(prof, args.steps, B, args.traffic, peaks, int8=args.dtype == 'int8')
             rec['kernels'] = kernel_table(prof, args.steps)
             ref = None
             if world == 1 and not args.no_cpu_baseline:
@@ -410,7 +518,9 @@ def main():
                 rec['pose_err_vs_fp32'] = pose_error(
                     eng, dev, *ref, tolerance='logits 1e-3, pose 0.1 deg / 1 mm (BASELINE.json north_star)')
             if world == 1 and args.dtype != 'int8' and not args.no_int8:
-                rec['c5'] = run_int8(args, sd, dev, frames, ref)
+                rec['c5'] = run_int8(args, sd, dev, frames, ref, peaks)
+            if world == 1 and not args.no_keypoint:
+                rec['keypoint_mode'] = run_keypoint(args, dev, with_ref=not args.no_cpu_baseline)
         print(json.dumps(rec), flush=True)
     if world > 1:
         dist.barrier()

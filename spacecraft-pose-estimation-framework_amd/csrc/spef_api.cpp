@@ -35,6 +35,10 @@ static int fail(int code, const std::string& msg) {
   g_err = msg;
   return code;
 }
+namespace spef {
+int report_error(int code, const std::string& msg) { return fail(code, msg); }
+}  // namespace spef
+
 #define HIP_TRY(expr)                                                                                  \
   do {                                                                                                 \
     hipError_t e_ = (expr);                                                                            \

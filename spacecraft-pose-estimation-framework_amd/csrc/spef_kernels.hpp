@@ -4,7 +4,12 @@
 #include <stddef.h>
 #include <stdint.h>
 
+#include <string>
+
 namespace spef {
+
+// Sets the calling thread's spef_last_error() message and returns `code` (spef_api.cpp).
+int report_error(int code, const std::string& msg);
 
 enum Dtype : int { DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3, DT_F32 = 4 };
 enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RELU_F32 = 3 /* ReLU, fp32 output */ };

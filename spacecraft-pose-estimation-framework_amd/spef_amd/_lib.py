@@ -47,6 +47,8 @@ SIGNATURES = {
     'spef_decode_keypoints': (_i, [_vp, _vp, _i, _i, _vp, _vp, _vp, _vp, _vp]),
     'spef_profile_begin': (_i, [_vp]),
     'spef_profile_end': (_i, [_vp, C.c_char_p, _sz, C.POINTER(_sz)]),
+    'spef_measure_peaks': (_i, [_i, _i, C.POINTER(C.c_double)]),
+    'spef_clock_stamp': (_i, [_vp, _i, _vp]),
 }
 
 

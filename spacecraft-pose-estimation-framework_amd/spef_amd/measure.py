@@ -1,0 +1,59 @@
+"""On-box measurement helpers for bench.py (C ABI spef_measure_peaks / spef_clock_stamp, csrc/k_ubench.hip).
+
+``measure_peaks`` re-measures the roofline peaks on the box the bench runs on; ``ClockProbe``
+brackets a timed region with two in-kernel clock stamps and returns the shader clock held during it (per XCD:
+delta s_memtime -- shader cycles -- over delta s_memrealtime at 100 MHz)."""
+from __future__ import annotations
+
+import ctypes as C
+import statistics
+
+import torch
+
+from . import _lib as L
+
+
+def measure_peaks(device: int = 0, reps: int = 2) -> dict:
+    out = (C.c_double * 6)()
+    L.check(L.load().spef_measure_peaks(int(device), int(reps), out))
+    return {'fp16_mfma_tflops': round(out[0], 1), 'int8_mfma_tops': round(out[1], 1),
+            'hbm_copy_gbs': round(out[2], 1), 'hbm_read_gbs': round(out[3], 1),
+            'sclk_mhz_fp16_loop': round(out[4], 1), 'sclk_mhz_int8_loop': round(out[5], 1),
+            'method': 'csrc/k_ubench.hip: best of %d timed launches after a warm-up; MFMA loops on random operands, '
+                      '8 chains per wave, 2 waves per SIMD; HBM: 1 GiB buffers (copy counts read + write bytes)' % reps}
+
+
+class ClockProbe:
+    """``start()`` / ``stop()`` around a timed region (each enqueues one stamp kernel on the current stream and
+    synchronises); ``mhz()`` -> {'sclk_mhz': median over XCDs, 'per_xcd': [...]} or None when no XCD was stamped
+    in both."""
+
+    def __init__(self, device: torch.device, n_wg: int = 64):
+        self.dev = torch.device(device)
+        self.n = n_wg
+        self.buf = [torch.zeros((n_wg, 3), dtype=torch.int64, device=self.dev) for _ in range(2)]
+
+    def _stamp(self, i: int) -> None:
+        s = torch.cuda.current_stream(self.dev).cuda_stream
+        L.check(L.load().spef_clock_stamp(C.c_void_p(self.buf[i].data_ptr()), self.n, C.c_void_p(s)))
+        torch.cuda.synchronize(self.dev)
+
+    def start(self) -> None:
+        self._stamp(0)
+
+    def stop(self) -> None:
+        self._stamp(1)
+
+    def mhz(self):
+        a, b = (t.cpu().numpy() for t in self.buf)
+        per = {}
+        for xcc in sorted(set(int(v) for v in a[:, 0]) & set(int(v) for v in b[:, 0])):
+            ra, rb = a[a[:, 0] == xcc], b[b[:, 0] == xcc]
+            dt = int(rb[:, 1].min()) - int(ra[:, 1].min())
+            dr = int(rb[:, 2].min()) - int(ra[:, 2].min())
+            if dr > 0 and dt > 0:
+                per[xcc] = dt / dr * 100.0
+        if not per:
+            return None
+        return {'sclk_mhz': round(statistics.median(per.values()), 1),
+                'per_xcd': {str(k): round(v, 1) for k, v in per.items()}}

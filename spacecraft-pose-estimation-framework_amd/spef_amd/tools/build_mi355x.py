@@ -1,12 +1,22 @@
 """Build an experiment for the MI355X target (the analogue of build_nvidia.py / build_tvm.py).
 
-    python -m spef_amd.tools.build_mi355x --experiment experiments/train/<name> [--dtype fp16|bf16|int8]
+    python -m spef_amd.tools.build_mi355x --experiment experiments/train/<name> [--dtype fp16|bf16|int8|fp32]
+        [--eval-variants fp32,fp16,bf16,int8 | none] [--eval-batches N]
     python -m spef_amd.tools.build_mi355x --synthetic --out experiments/build/mi355x/synthetic
 
 Reads ``config.yaml`` + ``model/parameters.pt`` (+ ``model/bit_width.json`` for quantized models) of a
 reference training experiment (eval.py:20-27 layout; the checkpoint is loaded with ``weights_only=True``),
 folds BN and packs the weight blob (fp16/bf16, or int8 with activation scales calibrated on frames), and writes
 ``experiments/build/mi355x/<name>/{model.spef, config.yaml, build.json}``.
+
+Then, like build_nvidia.py:331-343 / build_tvm.py:219-231 (every lowering variant evaluated on the host with the same
+``evaluation()``), each precision variant of the experiment -- fp32 (the reference's arithmetic), fp16, bf16 and
+int8 -- is built in memory and evaluated on the same frames (``eval_host/eval_<variant>.json``), and
+``eval_host/variants.json`` compares every variant's head outputs and poses with the fp32 variant's (the
+spe_finn.py:116-149 statistics, tools/compare.py) and, when the caller passes the reference model
+(``build(..., reference=callable)``: float32 NCHW images -> (ori, pos) raw head outputs), with the reference's.
+Needs a GPU; skipped (with a note in build.json) when none is visible. Keypoint experiments default to the fp32 blob:
+the fp16 keypoint head exceeds the 1e-3 output bound.
 """
 from __future__ import annotations
 
@@ -18,24 +28,85 @@ import sys
 import time
 
 
-def build(sd, cfg, out_dir: str, dtype: str, calib_frames=None, bit_width=None) -> dict:
-    """``bit_width``: the experiment's bit_width.json as quant.BitWidths (int8 only; None = all 8 bits)."""
+def pack_variant(sd, cfg, arch, dtype: str, calib_frames=None, bit_width=None):
+    """-> (blob bytes, int8 quantisation parameters or None)."""
     from .. import blob as Bl
-    from ..arch import arch_from_state_dict
-    os.makedirs(out_dir, exist_ok=True)
-    arch = arch_from_state_dict(sd, residual=cfg.MODEL.BACKBONE.RESIDUAL)
-    t0 = time.time()
     if dtype == 'int8':
         from ..blob_q8 import pack_int8
         from ..quant import calibrate
         assert calib_frames is not None, 'int8 builds calibrate activation scales on frames'
         qp = calibrate(sd, calib_frames, residual=cfg.MODEL.BACKBONE.RESIDUAL, bw=bit_width)
-        blob = pack_int8(sd, qp, arch)
+        return pack_int8(sd, qp, arch), qp
+    return Bl.pack(sd, arch, dtype=dtype), None
+
+
+def evaluate_variants(sd, cfg, arch, out_dir: str, variants, calib_frames=None, bit_width=None, reference=None,
+                      n_batches: int = 2, camera=None) -> dict:
+    """Host evaluation of every precision variant on the same synthetic SPEED-style batches (build_nvidia.py:331-343).
+    Writes eval_host/eval_<variant>.json ({score, error} of evaluation()) and eval_host/variants.json; returns the
+    latter. ``reference``: optional callable, float32 NCHW [0,1] images -> (ori, pos) raw head outputs."""
+    import numpy as np
+    import torch
+    from ..config import to_spe_utils
+    from ..data.synthetic import speed_like_loader
+    from ..spe_mi355x import SPEMi355x
+    from .compare import feature_stats
+    from .evaluation import evaluation
+    dev = torch.device(f'cuda:{cfg.MI355X.DEVICE}')
+    su = to_spe_utils(cfg, camera)
+    size, B = tuple(cfg.DATA.IMG_SIZE), cfg.MI355X.BATCH_SIZE
+    batches = list(speed_like_loader(n_batches, B, size))
+    x0 = batches[0][0]['torch']
+    xf = x0.permute(0, 3, 1, 2).float().div(255.0)        # ToTensor() of the same frames (the reference's input)
+    ed = os.path.join(out_dir, 'eval_host')
+    os.makedirs(ed, exist_ok=True)
+    outs, poses, summary = {}, {}, {'frames': int(B * n_batches), 'img_size': list(size), 'variants': {}}
+    for v in variants:
+        blob, _ = pack_variant(sd, cfg, arch, v, calib_frames, bit_width)
+        spe = SPEMi355x(blob, dev, su)
+        try:
+            score, error = evaluation(spe, {'synthetic': batches}, su, ('synthetic',))
+            with open(os.path.join(ed, f'eval_{v}.json'), 'w') as f:
+                json.dump({'score': score, 'error': error}, f, indent=1)
+            o, p = spe.engine.forward(x0.to(dev))
+            outs[v] = np.concatenate([o.cpu().numpy()] + ([p.cpu().numpy()] if p is not None else []), axis=1)
+            poses[v], _ = spe.predict(x0)
+            summary['variants'][v] = {'esa_score': score['synthetic']['esa'][0], 'blob_bytes': len(blob)}
+        finally:
+            spe.close()
+    ref_out = None
+    if reference is not None:
+        with torch.no_grad():
+            ro, rp = reference(xf)
+        ref_out = np.concatenate([np.asarray(ro, np.float32), np.asarray(rp, np.float32)] if rp is not None and
+                                 np.asarray(rp).size else [np.asarray(ro, np.float32)], axis=1)
+    base = 'fp32' if 'fp32' in outs else None
+    for v in outs:
+        rec = summary['variants'][v]
+        if base and v != base:
+            rec['vs_fp32_variant'] = feature_stats(outs[v], outs[base])
+            qa, qb = poses[v]['ori'].astype(np.float64), poses[base]['ori'].astype(np.float64)
+            d = np.abs(np.sum(qa * qb, axis=1)) / (np.linalg.norm(qa, axis=1) * np.linalg.norm(qb, axis=1))
+            rec['vs_fp32_variant']['ori_max_deg'] = float(np.degrees(2 * np.arccos(np.clip(d, 0, 1))).max())
+            rec['vs_fp32_variant']['pos_max_m'] = float(np.linalg.norm(poses[v]['pos'] - poses[base]['pos'], axis=1).max())
+        if ref_out is not None:
+            rec['vs_reference'] = feature_stats(outs[v], ref_out)
+    with open(os.path.join(ed, 'variants.json'), 'w') as f:
+        json.dump(summary, f, indent=1)
+    return summary
+
+
+def build(sd, cfg, out_dir: str, dtype: str, calib_frames=None, bit_width=None) -> dict:
+    """``bit_width``: the experiment's bit_width.json as quant.BitWidths (int8 only; None = all 8 bits)."""
+    from ..arch import arch_from_state_dict
+    os.makedirs(out_dir, exist_ok=True)
+    arch = arch_from_state_dict(sd, residual=cfg.MODEL.BACKBONE.RESIDUAL)
+    t0 = time.time()
+    blob, qp = pack_variant(sd, cfg, arch, dtype, calib_frames, bit_width)
+    if qp is not None:
         import dataclasses
         with open(os.path.join(out_dir, 'qparams.json'), 'w') as f:
             json.dump(dict(qp, bits=dataclasses.asdict(qp['bits'])), f, indent=1)
-    else:
-        blob = Bl.pack(sd, arch, dtype=dtype)
     with open(os.path.join(out_dir, 'model.spef'), 'wb') as f:
         f.write(blob)
     cfg.MI355X.DTYPE = dtype
@@ -52,8 +123,12 @@ def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument('--experiment', help='reference experiment dir with config.yaml and model/parameters.pt')
     ap.add_argument('--synthetic', action='store_true', help='seeded synthetic weights (no checkpoint offline)')
-    ap.add_argument('--dtype', choices=['fp16', 'bf16', 'int8'])
+    ap.add_argument('--dtype', choices=['fp16', 'bf16', 'int8', 'fp32'])
     ap.add_argument('--out')
+    ap.add_argument('--eval-variants', default='auto',
+                    help="comma list of fp32,fp16,bf16,int8 to evaluate on the host after the build, 'none', or "
+                         "'auto' (all that apply, when a GPU is visible)")
+    ap.add_argument('--eval-batches', type=int, default=2)
     a = ap.parse_args(argv)
     import torch
     from ..config import load_config
@@ -82,10 +157,25 @@ def main(argv=None):
         name = 'synthetic'
     else:
         ap.error('--experiment or --synthetic')
-    dtype = a.dtype or cfg.MI355X.DTYPE
+    keypoints = cfg.MODEL.HEAD.ORI == 'keypoints'
+    dtype = a.dtype or ('fp32' if keypoints and cfg.MI355X.DTYPE == 'fp16' else cfg.MI355X.DTYPE)
     out = a.out or os.path.join('experiments', 'build', 'mi355x', name)
-    calib = synth_frames(cfg.MI355X.CALIB_FRAMES, *cfg.DATA.IMG_SIZE, 900) if dtype == 'int8' else None
-    info = build(sd, cfg, out, dtype, calib, bit_width)
+    calib = synth_frames(cfg.MI355X.CALIB_FRAMES, *cfg.DATA.IMG_SIZE, 900)
+    info = build(sd, cfg, out, dtype, calib if dtype == 'int8' else None, bit_width)
+    if a.eval_variants != 'none':
+        variants = (['fp32', 'fp16', 'bf16'] + ([] if keypoints else ['int8'])) if a.eval_variants == 'auto' else \
+            [v for v in a.eval_variants.split(',') if v]
+        if torch.cuda.is_available():
+            from ..arch import arch_from_state_dict
+            from ..spe.camera import CAMERAS
+            camera = CAMERAS['speed_plus' if 'plus' in cfg.DATA.PATH else 'speed']
+            info['eval_host'] = evaluate_variants(sd, cfg, arch_from_state_dict(sd, residual=cfg.MODEL.BACKBONE.RESIDUAL),
+                                                  out, variants, calib, bit_width, n_batches=a.eval_batches,
+                                                  camera=camera)
+        else:
+            info['eval_host'] = 'skipped: no GPU visible (run the build on the MI355X box to evaluate the variants)'
+        with open(os.path.join(out, 'build.json'), 'w') as f:
+            json.dump(info, f, indent=1)
     print(json.dumps(info))
     return 0
 

@@ -92,3 +92,20 @@ def test_deploy_tool_synthetic(tmp_path):
     lat = json.load(open(os.path.join(out, 'on_board', 'latency_ms.json')))
     sc = json.load(open(os.path.join(out, 'on_board', 'score.json')))
     assert lat['mi355x'][0] > 0 and 'synthetic' in sc['score']
+
+
+@pytest.mark.gpu
+def test_build_tool_evaluates_precision_variants(tmp_path):
+    """build_mi355x evaluates every precision variant on the same frames (build_nvidia.py:331-343): one
+    eval_host/eval_<variant>.json each, and variants.json comparing head outputs and poses with the fp32 variant."""
+    from spef_amd.tools.build_mi355x import main
+    out = str(tmp_path / 'b')
+    assert main(['--synthetic', '--out', out, '--eval-variants', 'fp32,fp16,bf16,int8', '--eval-batches', '1']) == 0
+    v = json.load(open(os.path.join(out, 'eval_host', 'variants.json')))
+    for name in ('fp32', 'fp16', 'bf16', 'int8'):
+        assert os.path.exists(os.path.join(out, 'eval_host', f'eval_{name}.json'))
+        assert name in v['variants']
+    assert v['variants']['fp16']['vs_fp32_variant']['max_abs'] < 1e-3          # north-star logit bound
+    assert v['variants']['bf16']['vs_fp32_variant']['max_abs'] < 6e-3          # test_gpu_c2_precision bound
+    assert v['variants']['fp16']['vs_fp32_variant']['ori_max_deg'] < 0.1
+    assert v['variants']['int8']['vs_fp32_variant']['max_abs'] < 0.05          # INT8_BOUND (bench.py)
