@@ -175,12 +175,12 @@ int spef_profile_end(spef_ctx* ctx, char* buf, size_t cap, size_t* needed);
 /* On-box measurement (bench.py; SURVEY.md §8d "peaks re-measured by the build's own microbenchmark"), no model
  * involved. spef_measure_peaks runs, on `device`, `reps` timed launches (after one warm-up) of each of: a dense
  * v_mfma_f32_16x16x32_f16 loop, a v_mfma_i32_16x16x64_i8 loop (random operands, 8 independent chains per wave,
- * 2 waves per SIMD), a 1 GiB HBM copy and a 1 GiB HBM read, and writes the best rates: out[0] fp16 TFLOP/s,
+ * 4 waves per SIMD), a 1 GiB HBM copy and a 1 GiB HBM read, and writes the best rates: out[0] fp16 TFLOP/s,
  * out[1] int8 TOP/s, out[2] copy GB/s (read + write bytes), out[3] read GB/s, out[4] / out[5] the shader clock in
  * MHz held inside the fp16 / int8 loop (median over workgroups of delta s_memtime / delta s_memrealtime x 100).
- * spef_clock_stamp enqueues n_wg one-wave workgroups on `stream`, each writing (XCD id, s_memtime,
- * s_memrealtime) as three uint64 into the device buffer `out`: two stamps around a timed region give the clock
- * held during it (deltas per XCD). */
+ * spef_clock_stamp enqueues n_wg one-wave workgroups on `stream`, each writing (location, s_memtime,
+ * s_memrealtime) as three uint64 into the device buffer `out` -- location = XCD id << 8 | HW_ID[15:8] (CU, SH,
+ * SE): two stamps around a timed region give the clock held during it (deltas within one CU). */
 int spef_measure_peaks(int device, int reps, double* out);
 int spef_clock_stamp(void* out, int n_wg, void* stream);
 

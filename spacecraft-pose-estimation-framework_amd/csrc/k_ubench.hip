@@ -16,8 +16,13 @@
 
 namespace spef {
 
-// XCC (XCD) id of the executing wave: hwreg XCC_ID (id 20 on gfx940+), bits [3:0].
-__device__ __forceinline__ uint32_t xcc_id() { return __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u; }
+// Location of the executing wave: XCD (hwreg XCC_ID, id 20 on gfx940+, bits [3:0]) in bits [11:8], and HW_ID
+// (id 4) bits [15:8] = CU, SH and SE id in bits [7:0]. s_memtime counters are only comparable within one CU.
+__device__ __forceinline__ uint32_t cu_key() {
+  const uint32_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | 20) & 15u;
+  const uint32_t hw = __builtin_amdgcn_s_getreg((31 << 11) | 4);
+  return (xcc << 8) | ((hw >> 8) & 0xffu);
+}
 
 // 8 independent accumulator chains per wave on random operands (zero operands run at a higher clock than real
 // data, MI355X_MICROARCH.md "DVFS give-back" item 1); lane 0 of each workgroup stamps the clock around the loop.
@@ -67,24 +72,36 @@ __global__ __launch_bounds__(256) void mfma_peak_kernel(const uint32_t* __restri
   }
 }
 
+// Streaming kernels: each thread moves 4 x 16 B per iteration (4 loads in flight), grid-stride over n (n % (4 *
+// grid * 256) == 0 for the 1 GiB buffers used here).
 __global__ __launch_bounds__(256) void hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) dst[i] = src[i];
+  const size_t stride = (size_t)gridDim.x * 256;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
+    const uint4 a = *(src + i), b = *(src + i + stride);
+    const uint4 c = *(src + i + 2 * stride), d = *(src + i + 3 * stride);
+    *(dst + i) = a;
+    *(dst + i + stride) = b;
+    *(dst + i + 2 * stride) = c;
+    *(dst + i + 3 * stride) = d;
+  }
 }
 
 __global__ __launch_bounds__(256) void hbm_read_kernel(const uint4* __restrict__ src, size_t n, uint32_t* __restrict__ sink) {
+  const size_t stride = (size_t)gridDim.x * 256;
   uint32_t x = 0;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
-    const uint4 v = src[i];
-    x ^= v.x ^ v.y ^ v.z ^ v.w;
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
+    const uint4 a = *(src + i), b = *(src + i + stride);
+    const uint4 c = *(src + i + 2 * stride), d = *(src + i + 3 * stride);
+    x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
   }
   if (x == 0x9e3779b9u) sink[0] = x;
 }
 
-// One record per workgroup: (xcc id, s_memtime, s_memrealtime).
+// One record per workgroup: (cu_key, s_memtime, s_memrealtime).
 __global__ void clock_stamp_kernel(unsigned long long* __restrict__ out) {
   if (threadIdx.x == 0) {
     const unsigned long long t = __builtin_amdgcn_s_memtime(), r = __builtin_amdgcn_s_memrealtime();
-    out[blockIdx.x * 3 + 0] = xcc_id();
+    out[blockIdx.x * 3 + 0] = cu_key();
     out[blockIdx.x * 3 + 1] = t;
     out[blockIdx.x * 3 + 2] = r;
   }
@@ -131,8 +148,8 @@ extern "C" int spef_measure_peaks(int device, int reps, double* out) {
   Scratch sc;
   const size_t hbm_bytes = (size_t)1 << 30;   // 1 GiB per buffer: 4x the 256 MB Infinity Cache
   UB_TRY(hipMalloc(&sc.p[0], 4096 * 16));
-  UB_TRY(hipMalloc(&sc.p[1], (size_t)cus * 8 * 256 * sizeof(float)));
-  UB_TRY(hipMalloc(&sc.p[2], (size_t)cus * 8 * 2 * sizeof(unsigned long long)));
+  UB_TRY(hipMalloc(&sc.p[1], (size_t)cus * 4 * 256 * sizeof(float)));
+  UB_TRY(hipMalloc(&sc.p[2], (size_t)cus * 4 * 2 * sizeof(unsigned long long)));
   UB_TRY(hipMalloc(&sc.p[3], hbm_bytes));
   UB_TRY(hipMalloc(&sc.p[4], hbm_bytes));
   UB_TRY(hipEventCreate(&sc.e0));
@@ -150,7 +167,7 @@ extern "C" int spef_measure_peaks(int device, int reps, double* out) {
   }
   UB_TRY(hipMemset(sc.p[3], 1, hbm_bytes));
   UB_TRY(hipMemset(sc.p[4], 0, hbm_bytes));
-  const int wgs = cus * 2;   // 8 waves per CU = 2 per SIMD, 8 independent chains each
+  const int wgs = cus * 4;   // 16 waves per CU = 4 per SIMD, 8 independent chains each
   auto time_launch = [&](auto&& launch, float* ms) -> int {
     UB_TRY(hipEventRecord(sc.e0, nullptr));
     launch();

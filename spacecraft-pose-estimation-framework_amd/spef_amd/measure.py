@@ -1,8 +1,8 @@
 """On-box measurement helpers for bench.py (C ABI spef_measure_peaks / spef_clock_stamp, csrc/k_ubench.hip).
 
 ``measure_peaks`` re-measures the roofline peaks on the box the bench runs on; ``ClockProbe``
-brackets a timed region with two in-kernel clock stamps and returns the shader clock held during it (per XCD:
-delta s_memtime -- shader cycles -- over delta s_memrealtime at 100 MHz)."""
+brackets a timed region with two in-kernel clock stamps and returns the shader clock held during it (per CU stamped
+in both: delta s_memtime -- shader cycles -- over delta s_memrealtime at 100 MHz; median over CUs, and per XCD)."""
 from __future__ import annotations
 
 import ctypes as C
@@ -28,7 +28,7 @@ class ClockProbe:
     synchronises); ``mhz()`` -> {'sclk_mhz': median over XCDs, 'per_xcd': [...]} or None when no XCD was stamped
     in both."""
 
-    def __init__(self, device: torch.device, n_wg: int = 64):
+    def __init__(self, device: torch.device, n_wg: int = 4096):
         self.dev = torch.device(device)
         self.n = n_wg
         self.buf = [torch.zeros((n_wg, 3), dtype=torch.int64, device=self.dev) for _ in range(2)]
@@ -46,14 +46,20 @@ class ClockProbe:
 
     def mhz(self):
         a, b = (t.cpu().numpy() for t in self.buf)
-        per = {}
-        for xcc in sorted(set(int(v) for v in a[:, 0]) & set(int(v) for v in b[:, 0])):
-            ra, rb = a[a[:, 0] == xcc], b[b[:, 0] == xcc]
-            dt = int(rb[:, 1].min()) - int(ra[:, 1].min())
-            dr = int(rb[:, 2].min()) - int(ra[:, 2].min())
+        per_cu = {}
+        for key in sorted(set(int(v) for v in a[:, 0]) & set(int(v) for v in b[:, 0])):
+            ra, rb = a[a[:, 0] == key], b[b[:, 0] == key]
+            # the first wave each stamp put on this CU (smallest realtime), and its own shader-cycle count
+            ia, ib = int(ra[:, 2].argmin()), int(rb[:, 2].argmin())
+            dt = int(rb[ib, 1]) - int(ra[ia, 1])
+            dr = int(rb[ib, 2]) - int(ra[ia, 2])
             if dr > 0 and dt > 0:
-                per[xcc] = dt / dr * 100.0
-        if not per:
+                per_cu[key] = dt / dr * 100.0
+        if not per_cu:
             return None
-        return {'sclk_mhz': round(statistics.median(per.values()), 1),
-                'per_xcd': {str(k): round(v, 1) for k, v in per.items()}}
+        per_xcd = {}
+        for key, v in per_cu.items():
+            per_xcd.setdefault(key >> 8, []).append(v)
+        return {'sclk_mhz': round(statistics.median(per_cu.values()), 1), 'cus': len(per_cu),
+                'per_xcd_median': {str(k): round(statistics.median(v), 1) for k, v in sorted(per_xcd.items())},
+                'spread_mhz': [round(min(per_cu.values()), 1), round(max(per_cu.values()), 1)]}
