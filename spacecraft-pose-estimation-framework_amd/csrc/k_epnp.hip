@@ -2,12 +2,13 @@
 // (src/spe/keypoints_utils.py:112-150) = cv2.solvePnP(SOLVEPNP_EPNP) -> Rodrigues -> dcm2quat (spe/utils.py:56-118),
 // including solvePnP's undistortPoints for cameras with lens distortion (SPEED+, data/datasets/speed_plus.py:18-40).
 //
-// One fp64 thread per problem; the algorithm is OpenCV 4.5.5 epnp.cpp's (the reference's pinned OpenCV):
+// One 64-lane wave per problem, fp64; the algorithm is OpenCV 4.5.5 epnp.cpp's (the reference's pinned OpenCV):
 // PCA control points, barycentric alphas, M (2n x 12), the 4 eigenvectors of M^T M with the smallest
 // eigenvalues, L_6x10 / rho, beta approximations 1/2/3 (least squares), 5 Gauss-Newton steps (Householder
 // QR), R|t by Procrustes with OpenCV's sign fixes, lowest mean reprojection error wins. Symmetric
-// eigenproblems use cyclic Jacobi (fp64) instead of LAPACK/cvSVD -- same subspaces, independent of the
-// eigenvector signs. Rodrigues(rvec(R)) == R, so R goes straight to the Spurrier quaternion.
+// eigenproblems use Jacobi (fp64: the 12x12 one lane-parallel in tournament order, the 3x3 one cyclic) instead of
+// LAPACK/cvSVD -- same subspaces, independent of the eigenvector signs. Rodrigues(rvec(R)) == R, so R goes straight
+// to the Spurrier quaternion.
 #include <math.h>
 
 #include "spef_common.hpp"
@@ -98,13 +99,6 @@ __device__ void qr_lstsq(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
   }
 }
 
-struct EpnpProblem {
-  int n;
-  double pw[EPNP_MAXN][3], us[EPNP_MAXN][2], al[EPNP_MAXN][4];
-  double cws[4][3];
-  double fu, fv, uc, vc;
-};
-
 __device__ void epnp_gn(const double (&L)[6][10], const double (&rho)[6], double (&b)[4]) {
   for (int it = 0; it < 5; ++it) {
     double A[6][4], r[6], x[4];
@@ -121,68 +115,6 @@ __device__ void epnp_gn(const double (&L)[6][10], const double (&rho)[6], double
     qr_lstsq<4>(A, r, x);
     for (int i = 0; i < 4; ++i) b[i] += x[i];
   }
-}
-
-// R|t from betas (epnp.cpp compute_R_and_t); returns the mean reprojection error
-__device__ double epnp_rt(const EpnpProblem& P, const double (&ut4)[4][12], const double (&be)[4], double (&R)[3][3],
-                          double (&t)[3]) {
-  double ccs[4][3] = {};
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < 4; ++j)
-      for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * ut4[i][3 * j + k];
-  double pcs[EPNP_MAXN][3];
-  for (int i = 0; i < P.n; ++i)
-    for (int j = 0; j < 3; ++j)
-      pcs[i][j] = P.al[i][0] * ccs[0][j] + P.al[i][1] * ccs[1][j] + P.al[i][2] * ccs[2][j] + P.al[i][3] * ccs[3][j];
-  if (pcs[0][2] < 0.0)   // solve_for_sign
-    for (int i = 0; i < P.n; ++i)
-      for (int j = 0; j < 3; ++j) pcs[i][j] = -pcs[i][j];
-  double pc0[3] = {}, pw0[3] = {};
-  for (int i = 0; i < P.n; ++i)
-    for (int j = 0; j < 3; ++j) {
-      pc0[j] += pcs[i][j];
-      pw0[j] += P.pw[i][j];
-    }
-  for (int j = 0; j < 3; ++j) {
-    pc0[j] /= P.n;
-    pw0[j] /= P.n;
-  }
-  double abt[3][3] = {};
-  for (int i = 0; i < P.n; ++i)
-    for (int j = 0; j < 3; ++j)
-      for (int k = 0; k < 3; ++k) abt[j][k] += (pcs[i][j] - pc0[j]) * (P.pw[i][k] - pw0[k]);
-  // R = U V^T of abt = U S V^T: V from eig(abt^T abt), U = abt V S^-1
-  double ata[3][3], V[3][3];
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) ata[i][j] = abt[0][i] * abt[0][j] + abt[1][i] * abt[1][j] + abt[2][i] * abt[2][j];
-  jacobi_sym<3>(ata, V);
-  double U[3][3];
-  for (int c = 0; c < 3; ++c) {
-    double col[3], nrm = 0.0;
-    for (int r = 0; r < 3; ++r) {
-      col[r] = abt[r][0] * V[0][c] + abt[r][1] * V[1][c] + abt[r][2] * V[2][c];
-      nrm += col[r] * col[r];
-    }
-    nrm = sqrt(nrm);
-    for (int r = 0; r < 3; ++r) U[r][c] = nrm > 0 ? col[r] / nrm : 0.0;
-  }
-  for (int i = 0; i < 3; ++i)
-    for (int j = 0; j < 3; ++j) R[i][j] = U[i][0] * V[j][0] + U[i][1] * V[j][1] + U[i][2] * V[j][2];
-  const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
-                     R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
-  if (det < 0)
-    for (int j = 0; j < 3; ++j) R[2][j] = -R[2][j];
-  for (int i = 0; i < 3; ++i) t[i] = pc0[i] - (R[i][0] * pw0[0] + R[i][1] * pw0[1] + R[i][2] * pw0[2]);
-  double err = 0.0;
-  for (int i = 0; i < P.n; ++i) {
-    const double* p = P.pw[i];
-    const double xc = R[0][0] * p[0] + R[0][1] * p[1] + R[0][2] * p[2] + t[0];
-    const double yc = R[1][0] * p[0] + R[1][1] * p[1] + R[1][2] * p[2] + t[1];
-    const double iz = 1.0 / (R[2][0] * p[0] + R[2][1] * p[1] + R[2][2] * p[2] + t[2]);
-    const double ue = P.uc + P.fu * xc * iz, ve = P.vc + P.fv * yc * iz;
-    err += sqrt((P.us[i][0] - ue) * (P.us[i][0] - ue) + (P.us[i][1] - ve) * (P.us[i][1] - ve));
-  }
-  return err / P.n;
 }
 
 // cv::undistortPoints as solvePnP(SOLVEPNP_EPNP) applies it before EPnP (OpenCV 4.5.5 solvepnp.cpp;
@@ -215,100 +147,213 @@ __device__ __forceinline__ void undistort_point(const EpnpDist& d, double fu, do
   v_out = (double)(float)y * fv + vc;
 }
 
+// ---- one wave per problem ----
+// Lane i < n holds point i (its 3-D point, undistorted pixel, barycentric alphas); the 12 x 12 symmetric eigenproblem
+// of M^T M runs as a parallel (tournament-ordered) cyclic Jacobi in LDS: each of the 11 rounds of a sweep applies 6
+// disjoint rotations at once, every lane updating 2-3 of the 144 entries of A and of V (A' = J^T A J, V' = V J with J
+// the product of the round's rotations), double-buffered. The small fixed-size steps (L_6x10, betas, Gauss-Newton,
+// 3x3 Procrustes) run uniformly on every lane; the per-point sums (pcs centroid, the Procrustes cross-covariance,
+// the reprojection error) are wave reductions. Latency per problem is what this buys: the former one-thread-per-
+// problem kernel took ~2 ms for any batch (its 12x12 Jacobi indexed private arrays dynamically: scratch memory).
+
+// partner of index i in round r of the 12-player round robin: pairs (r, 11) and (r + k, r - k) mod 11, k = 1..5
+__device__ __forceinline__ int rr_partner(int r, int i) {
+  if (i == 11) return r;
+  if (i == r) return 11;
+  return (2 * r - i + 22) % 11;
+}
+
 __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw, int B, int n,
                                                   const float* __restrict__ kp3d, const double* __restrict__ model,
                                                   double fu, double fv, double uc,
                                                   double vc, float nu, float nv, EpnpDist dist, int apply_sigmoid,
                                                   float* __restrict__ kp_out, float* __restrict__ quat,
                                                   float* __restrict__ pos, int* __restrict__ status) {
-  const int b = blockIdx.x * 64 + threadIdx.x;
-  if (b >= B) return;
+  __shared__ double As[2][144], Vs[2][144];
+  __shared__ double Cc[12], Cs[12];
+  __shared__ double Pal[EPNP_MAXN][4], Pdu[EPNP_MAXN], Pdv[EPNP_MAXN];
+  const int b = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (b >= B) return;   // uniform per workgroup
   const int nk = 2 * (n + 1);
-  EpnpProblem P;
-  P.n = n;
-  P.fu = fu; P.fv = fv; P.uc = uc; P.vc = vc;
-  for (int i = 0; i <= n; ++i) {
-    float x = raw[(size_t)b * nk + 2 * i], y = raw[(size_t)b * nk + 2 * i + 1];
+
+  // ---- points: lane i <= n reads raw point i (origin first); lane j < n then owns keypoint j
+  double uu = 0.0, vv = 0.0;
+  if (lane <= n) {
+    float x = raw[(size_t)b * nk + 2 * lane], y = raw[(size_t)b * nk + 2 * lane + 1];
     if (apply_sigmoid) {   // spe_utils.py:68, float32
       x = 1.0f / (1.0f + expf(-x));
       y = 1.0f / (1.0f + expf(-y));
     }
     if (kp_out) {
-      kp_out[(size_t)b * nk + 2 * i] = x;
-      kp_out[(size_t)b * nk + 2 * i + 1] = y;
+      kp_out[(size_t)b * nk + 2 * lane] = x;
+      kp_out[(size_t)b * nk + 2 * lane + 1] = y;
     }
-    if (i > 0)   // keypoints_utils.py:127-131: pixels (float32 products), origin dropped; then undistortPoints
-      undistort_point(dist, fu, fv, uc, vc, x * nu, y * nv, P.us[i - 1][0], P.us[i - 1][1]);
+    // keypoints_utils.py:127-131: pixels (float32 products), origin dropped; then undistortPoints
+    undistort_point(dist, fu, fv, uc, vc, x * nu, y * nv, uu, vv);
   }
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < 3; ++j) P.pw[i][j] = (double)kp3d[3 * i + j];
+  const double us0 = __shfl_down(uu, 1, 64), us1 = __shfl_down(vv, 1, 64);   // lane j: keypoint j = raw point j + 1
+  const bool pt = lane < n;
+  double pw[3] = {0, 0, 0}, al[4] = {0, 0, 0, 0};
+  if (pt) {
+#pragma unroll
+    for (int k = 0; k < 3; ++k) pw[k] = (double)kp3d[3 * lane + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) al[k] = model[12 + 4 * lane + k];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) Pal[lane][k] = al[k];
+    Pdu[lane] = uc - us0;
+    Pdv[lane] = vc - us1;
+  }
+  double cws[4][3];   // control points (model-only, spef_set_keypoints)
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 3; ++j) cws[i][j] = model[3 * i + j];
+  __syncthreads();
 
-  // control points and barycentric coordinates: model-only, precomputed on the host (spef_set_keypoints)
-  for (int i = 0; i < 4; ++i)
-    for (int j = 0; j < 3; ++j) P.cws[i][j] = model[3 * i + j];
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < 4; ++j) P.al[i][j] = model[12 + 4 * i + j];
-  // M^T M accumulated row pair by row pair (M is never stored)
-  double mtm[12][12] = {};
-  for (int i = 0; i < n; ++i) {
-    double r1[12], r2[12];
-    for (int j = 0; j < 4; ++j) {
-      r1[3 * j] = P.al[i][j] * fu;
-      r1[3 * j + 1] = 0.0;
-      r1[3 * j + 2] = P.al[i][j] * (uc - P.us[i][0]);
-      r2[3 * j] = 0.0;
-      r2[3 * j + 1] = P.al[i][j] * fv;
-      r2[3 * j + 2] = P.al[i][j] * (vc - P.us[i][1]);
-    }
-    for (int p = 0; p < 12; ++p)
-      for (int q = p; q < 12; ++q) mtm[p][q] += r1[p] * r1[q] + r2[p] * r2[q];
-  }
-  for (int p = 0; p < 12; ++p)
-    for (int q = 0; q < p; ++q) mtm[p][q] = mtm[q][p];
-  double ev[12][12];
-  jacobi_sym<12>(mtm, ev);
-  // the 4 eigenvectors of smallest eigenvalue, ascending: ut4[0] = ut row 11 (smallest), ..., ut4[3] = row 8
-  int idx[12];
-  for (int i = 0; i < 12; ++i) idx[i] = i;
-  for (int i = 0; i < 4; ++i)
-    for (int j = i + 1; j < 12; ++j)
-      if (mtm[idx[j]][idx[j]] < mtm[idx[i]][idx[i]]) {
-        const int tmp = idx[i];
-        idx[i] = idx[j];
-        idx[j] = tmp;
+  // ---- M^T M (M never stored): entry e = (p, q) accumulated point by point as r1[p] r1[q] + r2[p] r2[q]
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    const int e = lane + 64 * s;
+    if (e < 144) {
+      const int p = e / 12, q = e - 12 * (e / 12);
+      const int cp = p / 3, dp = p - 3 * cp, cq = q / 3, dq = q - 3 * cq;
+      double acc = 0.0;
+      for (int i = 0; i < n; ++i) {
+        const double ap = Pal[i][cp], aq = Pal[i][cq];
+        const double r1p = dp == 0 ? ap * fu : dp == 2 ? ap * Pdu[i] : 0.0;
+        const double r1q = dq == 0 ? aq * fu : dq == 2 ? aq * Pdu[i] : 0.0;
+        const double r2p = dp == 1 ? ap * fv : dp == 2 ? ap * Pdv[i] : 0.0;
+        const double r2q = dq == 1 ? aq * fv : dq == 2 ? aq * Pdv[i] : 0.0;
+        acc += r1p * r1q + r2p * r2q;
       }
-  double ut4[4][12];
-  for (int i = 0; i < 4; ++i)
-    for (int k = 0; k < 12; ++k) ut4[i][k] = ev[k][idx[i]];
-  // L_6x10 and rho
-  const int pa[6] = {0, 0, 0, 1, 1, 2}, pb[6] = {1, 2, 3, 2, 3, 3};
-  double L[6][10], rho[6];
-  for (int r = 0; r < 6; ++r) {
-    double dv[4][3];
-    for (int i = 0; i < 4; ++i)
-      for (int k = 0; k < 3; ++k) dv[i][k] = ut4[i][3 * pa[r] + k] - ut4[i][3 * pb[r] + k];
-    auto dot = [&](int i, int j) { return dv[i][0] * dv[j][0] + dv[i][1] * dv[j][1] + dv[i][2] * dv[j][2]; };
-    L[r][0] = dot(0, 0);
-    L[r][1] = 2 * dot(0, 1);
-    L[r][2] = dot(1, 1);
-    L[r][3] = 2 * dot(0, 2);
-    L[r][4] = 2 * dot(1, 2);
-    L[r][5] = dot(2, 2);
-    L[r][6] = 2 * dot(0, 3);
-    L[r][7] = 2 * dot(1, 3);
-    L[r][8] = 2 * dot(2, 3);
-    L[r][9] = dot(3, 3);
-    double d2 = 0.0;
-    for (int k = 0; k < 3; ++k) d2 += (P.cws[pa[r]][k] - P.cws[pb[r]][k]) * (P.cws[pa[r]][k] - P.cws[pb[r]][k]);
-    rho[r] = d2;
+      As[0][e] = acc;
+      Vs[0][e] = p == q ? 1.0 : 0.0;
+    }
   }
-  double bestR[3][3], bestT[3], bestE = INFINITY;
+  __syncthreads();
+
+  // ---- parallel cyclic Jacobi (tournament order): sweeps of 11 rounds x 6 disjoint rotations
+  int cur = 0;
+  for (int sweep = 0; sweep < 40; ++sweep) {
+    double off = 0.0, diag = 0.0;
+#pragma unroll
+    for (int s = 0; s < 3; ++s) {
+      const int e = lane + 64 * s;
+      if (e < 144) {
+        const double a = As[cur][e];
+        if (e / 12 == e - 12 * (e / 12)) diag += a * a;
+        else if (e / 12 < e - 12 * (e / 12)) off += a * a;
+      }
+    }
+    off = warp_sum_d(off);
+    diag = warp_sum_d(diag);
+    if (off <= 1e-32 * diag || off == 0.0) break;
+    for (int r = 0; r < 11; ++r) {
+      if (lane < 12) {   // lane i: the rotation of its pair, its own signed coefficient
+        const int j = rr_partner(r, lane);
+        const int p = lane < j ? lane : j, q = lane < j ? j : lane;
+        const double apq = As[cur][12 * p + q];
+        double c = 1.0, sn = 0.0;
+        if (fabs(apq) >= 1e-300) {
+          const double theta = (As[cur][13 * q] - As[cur][13 * p]) / (2.0 * apq);
+          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
+          c = 1.0 / sqrt(t * t + 1.0);
+          sn = t * c;
+        }
+        Cc[lane] = c;
+        Cs[lane] = lane == p ? -sn : sn;
+      }
+      __syncthreads();
+#pragma unroll
+      for (int s = 0; s < 3; ++s) {
+        const int e = lane + 64 * s;
+        if (e < 144) {
+          const int i = e / 12, j = e - 12 * (e / 12);
+          const int i2 = rr_partner(r, i), j2 = rr_partner(r, j);
+          const double ci = Cc[i], si = Cs[i], cj = Cc[j], sj = Cs[j];
+          const double* a = As[cur];
+          As[cur ^ 1][e] = ci * (cj * a[12 * i + j] + sj * a[12 * i + j2]) + si * (cj * a[12 * i2 + j] + sj * a[12 * i2 + j2]);
+          const double* v = Vs[cur];
+          Vs[cur ^ 1][e] = cj * v[12 * i + j] + sj * v[12 * i + j2];
+        }
+      }
+      cur ^= 1;
+      __syncthreads();
+    }
+  }
+  // the 4 eigenvectors of smallest eigenvalue, ascending (ties keep the lower index); static loops only (a
+  // dynamically indexed private array would live in scratch)
+  double ev[12];
+#pragma unroll
+  for (int i = 0; i < 12; ++i) ev[i] = As[cur][13 * i];
+  int idx[4];
+  uint32_t used = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    double best = INFINITY;
+    int bi = 0;
+#pragma unroll
+    for (int j = 0; j < 12; ++j)
+      if (!((used >> j) & 1u) && ev[j] < best) {
+        best = ev[j];
+        bi = j;
+      }
+    idx[i] = bi;
+    used |= 1u << bi;
+  }
+  // ut4[i][k] = V[k][idx[i]] stays in LDS (read as broadcasts); L_6x10 rows and rho by lanes 0..5 into LDS
+  __shared__ double Ls[6][10], Rho[6];
+  const double* Vf = Vs[cur];
+  auto ut4 = [&](int i, int k) { return Vf[12 * k + idx[i]]; };
+  if (lane < 6) {
+    const int r = lane;
+    const int pa = r < 3 ? 0 : r < 5 ? 1 : 2, pb = r < 3 ? r + 1 : r < 5 ? r - 1 : 3;
+    double dv[4][3];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) dv[i][k] = ut4(i, 3 * pa + k) - ut4(i, 3 * pb + k);
+    auto dot = [&](int i, int j) { return dv[i][0] * dv[j][0] + dv[i][1] * dv[j][1] + dv[i][2] * dv[j][2]; };
+    Ls[r][0] = dot(0, 0);
+    Ls[r][1] = 2 * dot(0, 1);
+    Ls[r][2] = dot(1, 1);
+    Ls[r][3] = 2 * dot(0, 2);
+    Ls[r][4] = 2 * dot(1, 2);
+    Ls[r][5] = dot(2, 2);
+    Ls[r][6] = 2 * dot(0, 3);
+    Ls[r][7] = 2 * dot(1, 3);
+    Ls[r][8] = 2 * dot(2, 3);
+    Ls[r][9] = dot(3, 3);
+    double d2 = 0.0;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) d2 += (cws[pa][k] - cws[pb][k]) * (cws[pa][k] - cws[pb][k]);
+    Rho[r] = d2;
+  }
+  __syncthreads();
+  double L[6][10], rho[6];
+#pragma unroll
+  for (int r = 0; r < 6; ++r) {
+    rho[r] = Rho[r];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) L[r][k] = Ls[r][k];
+  }
+  // pw centroid (uniform): a wave reduction over the point lanes
+  double pw0[3];
+#pragma unroll
+  for (int k = 0; k < 3; ++k) pw0[k] = warp_sum_d(pw[k]) / n;
+
+  double bestR[3][3] = {}, bestT[3] = {}, bestE = INFINITY;
+#pragma unroll 1
   for (int ap = 1; ap <= 3; ++ap) {
     double be[4] = {0, 0, 0, 0};
     double rr[6];
+#pragma unroll
     for (int i = 0; i < 6; ++i) rr[i] = rho[i];
     if (ap == 1) {
       double A[6][4], x[4];
+#pragma unroll
       for (int i = 0; i < 6; ++i) {
         A[i][0] = L[i][0]; A[i][1] = L[i][1]; A[i][2] = L[i][3]; A[i][3] = L[i][6];
       }
@@ -320,6 +365,7 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
       be[3] = s * x[3] / be[0];
     } else if (ap == 2) {
       double A[6][3], x[3];
+#pragma unroll
       for (int i = 0; i < 6; ++i) {
         A[i][0] = L[i][0]; A[i][1] = L[i][1]; A[i][2] = L[i][2];
       }
@@ -334,7 +380,9 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
       if (x[1] < 0) be[0] = -be[0];
     } else {
       double A[6][5], x[5];
+#pragma unroll
       for (int i = 0; i < 6; ++i)
+#pragma unroll
         for (int k = 0; k < 5; ++k) A[i][k] = L[i][k];
       qr_lstsq<5>(A, rr, x);
       if (x[0] < 0) {
@@ -348,16 +396,79 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
       be[2] = x[3] / be[0];
     }
     epnp_gn(L, rho, be);
-    double R[3][3], t[3];
-    const double e = epnp_rt(P, ut4, be, R, t);
+    // R|t (epnp.cpp compute_R_and_t): ccs uniform, pcs of point = lane, sums by wave reduction
+    double ccs[4][3] = {};
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int k = 0; k < 3; ++k) ccs[j][k] += be[i] * ut4(i, 3 * j + k);
+    double pc[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pc[j] = pt ? al[0] * ccs[0][j] + al[1] * ccs[1][j] + al[2] * ccs[2][j] + al[3] * ccs[3][j] : 0.0;
+    if (__shfl(pc[2], 0, 64) < 0.0)   // solve_for_sign
+#pragma unroll
+      for (int j = 0; j < 3; ++j) pc[j] = -pc[j];
+    double pc0[3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j) pc0[j] = warp_sum_d(pc[j]) / n;
+    double abt[3][3];
+#pragma unroll
+    for (int j = 0; j < 3; ++j)
+#pragma unroll
+      for (int k = 0; k < 3; ++k) abt[j][k] = warp_sum_d(pt ? (pc[j] - pc0[j]) * (pw[k] - pw0[k]) : 0.0);
+    // R = U V^T of abt = U S V^T: V from eig(abt^T abt), U = abt V S^-1
+    double ata[3][3], Vm[3][3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) ata[i][j] = abt[0][i] * abt[0][j] + abt[1][i] * abt[1][j] + abt[2][i] * abt[2][j];
+    jacobi_sym<3>(ata, Vm);
+    double U[3][3], R[3][3], t[3];
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+      double col[3], nrm = 0.0;
+#pragma unroll
+      for (int r = 0; r < 3; ++r) {
+        col[r] = abt[r][0] * Vm[0][c] + abt[r][1] * Vm[1][c] + abt[r][2] * Vm[2][c];
+        nrm += col[r] * col[r];
+      }
+      nrm = sqrt(nrm);
+#pragma unroll
+      for (int r = 0; r < 3; ++r) U[r][c] = nrm > 0 ? col[r] / nrm : 0.0;
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) R[i][j] = U[i][0] * Vm[j][0] + U[i][1] * Vm[j][1] + U[i][2] * Vm[j][2];
+    const double det = R[0][0] * R[1][1] * R[2][2] + R[0][1] * R[1][2] * R[2][0] + R[0][2] * R[1][0] * R[2][1] -
+                       R[0][2] * R[1][1] * R[2][0] - R[0][1] * R[1][0] * R[2][2] - R[0][0] * R[1][2] * R[2][1];
+    if (det < 0)
+#pragma unroll
+      for (int j = 0; j < 3; ++j) R[2][j] = -R[2][j];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) t[i] = pc0[i] - (R[i][0] * pw0[0] + R[i][1] * pw0[1] + R[i][2] * pw0[2]);
+    double err = 0.0;
+    if (pt) {
+      const double xc = R[0][0] * pw[0] + R[0][1] * pw[1] + R[0][2] * pw[2] + t[0];
+      const double yc = R[1][0] * pw[0] + R[1][1] * pw[1] + R[1][2] * pw[2] + t[1];
+      const double iz = 1.0 / (R[2][0] * pw[0] + R[2][1] * pw[1] + R[2][2] * pw[2] + t[2]);
+      const double ue = uc + fu * xc * iz, ve = vc + fv * yc * iz;
+      err = sqrt((us0 - ue) * (us0 - ue) + (us1 - ve) * (us1 - ve));
+    }
+    const double e = warp_sum_d(err) / n;
     if (e < bestE) {   // strict: ties keep the lower approximation index (epnp.cpp compute_pose)
       bestE = e;
+#pragma unroll
       for (int i = 0; i < 3; ++i) {
         bestT[i] = t[i];
+#pragma unroll
         for (int j = 0; j < 3; ++j) bestR[i][j] = R[i][j];
       }
     }
   }
+  if (lane != 0) return;
   // dcm2quat (spe/utils.py:56-118, Spurrier)
   const double m11 = bestR[0][0], m12 = bestR[0][1], m13 = bestR[0][2];
   const double m21 = bestR[1][0], m22 = bestR[1][1], m23 = bestR[1][2];
@@ -382,6 +493,7 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
   quat[4 * b + 1] = (float)(q1 / qn);
   quat[4 * b + 2] = (float)(q2 / qn);
   quat[4 * b + 3] = (float)(q3 / qn);
+#pragma unroll
   for (int i = 0; i < 3; ++i) pos[3 * b + i] = (float)bestT[i];
   if (!(bestE < INFINITY) || isnan(qn)) status[b] |= 8;
 }
@@ -390,8 +502,8 @@ hipError_t launch_epnp(const float* raw, int B, int n, const float* kp3d, const 
                        float nu, float nv, const EpnpDist& dist, int apply_sigmoid, float* kp_out, float* quat,
                        float* pos, int* status, hipStream_t s) {
   if (n < 4 || n > EPNP_MAXN) return hipErrorInvalidValue;
-  epnp_kernel<<<(B + 63) / 64, 64, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, dist,
-                                           apply_sigmoid, kp_out, quat, pos, status);
+  epnp_kernel<<<B, 64, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, dist, apply_sigmoid, kp_out,
+                                quat, pos, status);
   return hipGetLastError();
 }
 
