@@ -755,20 +755,16 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   X(0, 32, 32, 16, 1, 16, 16, false, false, 8, 1, true, false)    /* block 1      */ \
   X(0, 16, 96, 24, 2, 4, 16, true, false, 4, 1, false, false)     /* block 2      */ \
   X(2, 16, 96, 24, 2, 8, 16, true, false, 8, 1, false, false)                        \
-  X(3, 16, 96, 24, 2, 8, 16, true, false, 4, 1, false, false)                        \
-  X(4, 16, 96, 24, 2, 8, 8, true, false, 2, 1, false, false)                         \
   X(0, 24, 144, 24, 1, 16, 16, true, true, 4, 1, false, false)    /* block 3      */ \
   X(1, 24, 144, 24, 1, 8, 16, true, true, 8, 1, false, false)                        \
   X(2, 24, 144, 24, 1, 8, 16, true, true, 4, 1, false, false)                        \
   X(0, 24, 144, 32, 2, 8, 8, true, false, 4, 1, false, false)     /* block 4      */ \
   X(2, 24, 144, 32, 2, 8, 16, true, false, 8, 1, false, false)                       \
-  X(3, 24, 144, 32, 2, 8, 16, true, false, 4, 1, false, false)                       \
   X(0, 32, 192, 32, 1, 8, 16, true, true, 4, 1, false, false)     /* blocks 5-6   */ \
   X(1, 32, 192, 32, 1, 16, 16, true, true, 8, 1, false, false)                       \
   X(0, 32, 192, 64, 2, 8, 8, true, false, 4, 1, false, false)     /* block 7      */ \
   X(1, 32, 192, 64, 2, 8, 8, true, false, 8, 2, false, false)                        \
   X(2, 32, 192, 64, 2, 8, 16, true, false, 8, 1, false, false)                       \
-  X(3, 32, 192, 64, 2, 8, 16, true, false, 4, 1, false, false)                       \
   X(0, 64, 384, 64, 1, 16, 16, true, true, 8, 1, true, true)      /* blocks 8-10  */ \
   X(1, 64, 384, 64, 1, 8, 16, true, true, 8, 1, false, true)                         \
   X(2, 64, 384, 64, 1, 16, 16, true, true, 8, 1, false, true)                        \

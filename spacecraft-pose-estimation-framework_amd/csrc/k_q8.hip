@@ -138,18 +138,16 @@ __global__ __launch_bounds__(256) void q_stem_rows_kernel(const void* __restrict
     if (i < NS) {
       uint32_t v = 0;
       if ((okm >> it) & 1u) {
+        // u8: bytes (ix - cx0) * 3 + ci of window row r's span, which starts (rs & 3) bytes into Raw; rs mod 4 only
+        // needs the low bits of the byte offset, so 32-bit arithmetic (wrapping) gives it exactly
+        const int r = i / kStemIW, ix = ix0 + (i - r * kStemIW);
+        const uint32_t rs = (((uint32_t)b * (uint32_t)H + (uint32_t)(iy0 + r)) * (uint32_t)W + (uint32_t)cx0) * 3u;
+        const uint8_t* rb = reinterpret_cast<const uint8_t*>(Raw + r * RAWDW) + (rs & 3u) + (ix - cx0) * 3;
 #pragma unroll
         for (int ci = 0; ci < 3; ++ci) {
           int q;
-          if (F32IN) {
-            q = (int)fminf(fmaxf(rintf(fv[it * 3 + ci] / s_img), (float)in_lo), (float)in_hi);
-          } else {   // byte (ix - cx0) * 3 + ci of window row r's span, which starts (rs & 3) bytes into Raw
-            const int r = i / kStemIW, ix = ix0 + (i - r * kStemIW);
-            const int iy = iy0 + r;
-            const size_t rs = (((size_t)b * H + iy) * W + cx0) * 3;
-            const int pos = (int)(rs & 3) + (ix - cx0) * 3 + ci;
-            q = Ll[reinterpret_cast<const uint8_t*>(Raw + r * RAWDW)[pos]];
-          }
+          if (F32IN) q = (int)fminf(fmaxf(rintf(fv[it * 3 + ci] / s_img), (float)in_lo), (float)in_hi);
+          else q = Ll[rb[ci]];
           v |= ((uint32_t)q & 0xffu) << (8 * ci);
         }
       }
