@@ -29,6 +29,10 @@ namespace spef {
 #else
 #define SPEF_IRW_CHUNK_SYNC() __syncthreads()
 #endif
+// Further tools/kbench timing ablations (wrong results, never in the library): SPEF_KBENCH_IRW_NO_WLOAD (no weight
+// fragment loads after the first chunks), SPEF_KBENCH_IRW_NO_EXPAND (expand waves only keep the barrier count),
+// SPEF_KBENCH_IRW_NO_DWMATH (depthwise reads kept, 2 instead of 4 VALU per channel and tap column),
+// SPEF_KBENCH_IRW_NO_PROJ (no project MFMAs).
 
 // Vertical-pair depthwise (fp16, stride 1, 16-wide tiles; blocks 8-13): the hidden slab holds, per (row pair, column)
 // position, one dword per channel = (row 2m, row 2m+1), in four 8-channel regions (k_irb.hip's VP layout); a kernel
@@ -190,6 +194,9 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
   x8 ea0[G::KS], ea1[G::KS];                             // expand A fragments of the chunk being produced
   x4 eq0, eq1;                                           // (16-channel input: K = 16 fragments)
   auto load_ea = [&](int c) {
+#ifdef SPEF_KBENCH_IRW_NO_WLOAD
+    if (c > 1) return;
+#endif
     const bool ok0 = c < G::NCH, ok1 = ok0 && 32 * c + 16 < HID;
     if constexpr (G::K16) {
       const T* w0 = We + (size_t)(32 * c + r16) * G::WKP + 4 * kg;
@@ -204,6 +211,9 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
       }
     }
   };
+#ifdef SPEF_KBENCH_IRW_RESIDENT
+  typename std::conditional<G::K16, x4, x8>::type vres[G::EPU][2][G::K16 ? 1 : G::KS];
+#endif
   // expand of chunk c into slab Es[c & 1] by this expand wave
   auto expand_vp = [&](int c) {
     // unit u = 16 pair positions q; lane r16 computes the even- and odd-row pixel of its position (two MFMA pixel
@@ -214,7 +224,11 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     constexpr int NBX = G::K16 ? 1 : G::KS;
     using BX = typename std::conditional<G::K16, x4, x8>::type;
     constexpr bool VBATCH = G::EPU * 2 * NBX * (G::K16 ? 2 : 4) <= 48;
+#ifdef SPEF_KBENCH_IRW_RESIDENT
+    auto& vbx = vres;
+#else
     BX vbx[G::EPU][2][NBX];
+#endif
     auto read_vbx = [&](int jj) {
       const int q = (ew + NE * jj) * 16 + r16;
       const int qc = q < G::NQ ? q : G::NQ - 1;
@@ -234,6 +248,9 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     };
 #pragma unroll
     for (int jj = 0; jj < G::EPU; ++jj) {
+#ifdef SPEF_KBENCH_IRW_RESIDENT
+      if (c > 0) break;
+#endif
       if (!VBATCH || ew + NE * jj >= G::NU) break;
       read_vbx(jj);
     }
@@ -278,6 +295,9 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     }
   };
   auto expand = [&](int c) {
+#ifdef SPEF_KBENCH_IRW_NO_EXPAND
+    if (c > 0) return;
+#endif
     if constexpr (VP) {
       expand_vp(c);
     } else {
@@ -412,18 +432,25 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
     // Retire load_pa(0) before the loop: otherwise the loop header merges "pa pending" from this edge, and the
     // waitcnt pass makes every chunk's project MFMAs wait for the next chunk's fragment loads issued just before.
     __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0)
-#pragma unroll 1
-    for (int c = 0; c < G::NCH; ++c) {
+    // One chunk: depthwise from Es[c & 1] with the project fragments pcur; the next chunk's fragments are issued
+    // into pnext (the last chunk re-reads its own: valid addresses, no branch). The chunk loop below alternates two
+    // fragment buffers instead of copying them.
+    x8 pb[G::NCTW];
+    auto dw_chunk = [&](const int c, x8 (&pcur)[G::NCTW], x8 (&pnext)[G::NCTW]) {
       const T* Es = Es0 + (c & 1) * G::PINP * G::ES;
       const DW* sl = Wds + 32 * c;                        // tap t of chunk c: sl[t * HIDP + ch]
       const bool hv = 32 * c + 8 * kg < HID;
-      x8 pn[G::NCTW];
       // next chunk's project fragments: issued now, consumed after this chunk's MFMAs
       {
-        const T* wpp = Wp + (size_t)(wc * G::NCTW * 16 + r16) * G::HIDP + 32 * (c + 1) + 8 * kg;
+        const int cn = c + 1 < G::NCH ? c + 1 : c;
+        const T* wpp = Wp + (size_t)(wc * G::NCTW * 16 + r16) * G::HIDP + 32 * cn + 8 * kg;
 #pragma unroll
         for (int t = 0; t < G::NCTW; ++t)
-          pn[t] = c + 1 < G::NCH ? load8<DT>(wpp + (size_t)t * 16 * G::HIDP) : zero8<DT>();
+#ifdef SPEF_KBENCH_IRW_NO_WLOAD
+          pnext[t] = pcur[t];
+#else
+          pnext[t] = load8<DT>(wpp + (size_t)t * 16 * G::HIDP);
+#endif
       }
       float db[8];
       {
@@ -461,20 +488,29 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
               rd8(pb + (G::IW + kx) * 32, pn);
 #pragma unroll
               for (int e = 0; e < 8; ++e) {
+#ifdef SPEF_KBENCH_IRW_NO_DWMATH
+                a0[e] = dot2h(pc[e], w01[kx][e], a0[e]);
+                a1[e] = dot2h(pn[e], w12[kx][e], a1[e]);
+#else
                 a1[e] = fmaf(h_hi(pc[e]), h_lo(w01[kx][e]), a1[e]);
                 a0[e] = dot2h(pc[e], w01[kx][e], a0[e]);
                 a0[e] = fmaf(h_lo(pn[e]), h_hi(w12[kx][e]), a0[e]);
                 a1[e] = dot2h(pn[e], w12[kx][e], a1[e]);
+#endif
               }
             }
             bf0 = relu_cvt8<DT>(a0);
             bf1 = relu_cvt8<DT>(a1);
           }
+#ifdef SPEF_KBENCH_IRW_NO_PROJ
+          asm volatile("" ::"v"(bf0), "v"(bf1));
+#else
 #pragma unroll
           for (int t = 0; t < G::NCTW; ++t) {
-            acc[qi][t] = DT::mfma(pa[t], bf0, acc[qi][t]);
-            acc[qi + 1][t] = DT::mfma(pa[t], bf1, acc[qi + 1][t]);
+            acc[qi][t] = DT::mfma(pcur[t], bf0, acc[qi][t]);
+            acc[qi + 1][t] = DT::mfma(pcur[t], bf1, acc[qi + 1][t]);
           }
+#endif
         }
       } else {
       // the chunk's 9 depthwise weight vectors, read once for all of this wave's pixel tiles
@@ -510,8 +546,8 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
           }
 #pragma unroll
           for (int t = 0; t < G::NCTW; ++t) {
-            acc[qi][t] = DT::mfma(pa[t], bf0, acc[qi][t]);
-            acc[qi + 1][t] = DT::mfma(pa[t], bf1, acc[qi + 1][t]);
+            acc[qi][t] = DT::mfma(pcur[t], bf0, acc[qi][t]);
+            acc[qi + 1][t] = DT::mfma(pcur[t], bf1, acc[qi + 1][t]);
           }
         }
       } else {
@@ -538,15 +574,28 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
             bf = relu_cvt8<DT>(a8);
           }
 #pragma unroll
-          for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
+          for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pcur[t], bf, acc[qi][t]);
         }
       }
       }
-#pragma unroll
-      for (int t = 0; t < G::NCTW; ++t) pa[t] = pn[t];
       SPEF_TRACE(6 + 2 * c);
       SPEF_IRW_CHUNK_SYNC();
       SPEF_TRACE(7 + 2 * c);
+    };
+    if constexpr (VP) {
+#pragma unroll 1
+      for (int c = 0; c + 1 < G::NCH; c += 2) {
+        dw_chunk(c, pa, pb);
+        dw_chunk(c + 1, pb, pa);
+      }
+      if constexpr (G::NCH % 2 == 1) dw_chunk(G::NCH - 1, pa, pb);
+    } else {   // (the unpaired depthwise has no registers for two inlined chunk bodies)
+#pragma unroll 1
+      for (int c = 0; c < G::NCH; ++c) {
+        dw_chunk(c, pa, pb);
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) pa[t] = pb[t];
+      }
     }
   }
 
