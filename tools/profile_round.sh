@@ -16,9 +16,9 @@ echo "bench ok"
 (cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/prof_$TAG -o run --output-format csv \
   -- python3 $R/bench.py --steps 10 --warmup 2 --no-cpu-baseline) > $O/prof_$TAG.log 2>&1
 echo "stats ok"
-(cd /tmp && timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$TAG -o run --output-format csv \
+(cd /tmp && timeout -s KILL 150 rocprofv3 --pmc FETCH_SIZE -d $O/pmc_fetch_$TAG -o run --output-format csv \
   -- python3 $R/tools/fwd_only.py 2) > $O/pmc_fetch_$TAG.log 2>&1
 echo "fetch ok"
-(cd /tmp && timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$TAG -o run --output-format csv \
+(cd /tmp && timeout -s KILL 150 rocprofv3 --pmc WRITE_SIZE -d $O/pmc_write_$TAG -o run --output-format csv \
   -- python3 $R/tools/fwd_only.py 2) > $O/pmc_write_$TAG.log 2>&1
 echo "write ok"
