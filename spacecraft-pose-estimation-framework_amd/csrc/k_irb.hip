@@ -315,6 +315,15 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     oxq[qi] = o - oyq[qi] * TW;
   }
 
+  // Per-lane LDS element offsets, computed once: every other slab / input-tile access of this lane is one of these
+  // plus a compile-time constant, which the ds_read / ds_write immediate offset field carries (no per-tap address
+  // registers).
+  int dwoff[G::QPW];   // top-left tap of output tile qi's 3x3 window in a hidden slab, this lane's 8 channels
+#pragma unroll
+  for (int qi = 0; qi < G::QPW; ++qi) dwoff[qi] = (oyq[qi] * S * G::IW + oxq[qi] * S) * G::ES + 8 * kg;
+  const int xoff = (wave * 16 + r16) * G::XS + (G::K16 ? 4 : 8) * kg;   // expand B fragment of pixel tile `wave`
+  const int eoff = (wave * 16 + r16) * G::ES + 4 * kg;                   // its expand output in the slab
+
   f32x4 acc[G::QPW][G::NCTW];   // project accumulators start at the folded-BN bias
 #pragma unroll
   for (int t = 0; t < G::NCTW; ++t) {
@@ -486,11 +495,11 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       auto read_bx = [&](int j) {
         const int pt = wave + NW * j;
         if constexpr (G::K16) {
-          bxs[j][0] = *reinterpret_cast<const x4*>(Xs + (pt * 16 + r16) * G::XS + 4 * kg);
+          bxs[j][0] = *reinterpret_cast<const x4*>(Xs + xoff + (pt - wave) * 16 * G::XS);
         } else {
 #pragma unroll
           for (int ks = 0; ks < G::KS; ++ks)
-            bxs[j][ks] = *reinterpret_cast<const x8*>(Xs + (pt * 16 + r16) * G::XS + 8 * kg + 32 * ks);
+            bxs[j][ks] = *reinterpret_cast<const x8*>(Xs + xoff + (pt - wave) * 16 * G::XS + 32 * ks);
         }
       };
 #pragma unroll
@@ -524,7 +533,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
           u0.x &= m0; u0.y &= m0; u1.x &= m0; u1.y &= m0;
         }
         // channels >= HID of a partial chunk are already 0: zero weight rows and zero bias
-        T* er = Ew + (pt * 16 + r16) * G::ES + 4 * kg;
+        T* er = Ew + eoff + (pt - wave) * 16 * G::ES;
         if constexpr (ABL != 3) {
           *reinterpret_cast<uint2*>(er) = u0;
           *reinterpret_cast<uint2*>(er + 16) = u1;
@@ -664,7 +673,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
             x8 v[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r)
-              v[r] = *reinterpret_cast<const x8*>(Es + ((oyq[qi] + r) * G::IW + oxq[qi] + kx) * G::ES + 8 * kg);
+              v[r] = *reinterpret_cast<const x8*>(Es + dwoff[qi] + (r * G::IW + kx) * G::ES);
 #pragma unroll
             for (int ky = 0; ky < 3; ++ky)
 #pragma unroll
@@ -699,8 +708,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky) {
             if (ABL == 1 && !(ky == 1 && kx == 1)) continue;
-            const int p = (oyq[qi] * S + ky) * G::IW + (oxq[qi] * S + kx);
-            const x8 v = *reinterpret_cast<const x8*>(Es + p * G::ES + 8 * kg);
+            const x8 v = *reinterpret_cast<const x8*>(Es + dwoff[qi] + (ky * G::IW + kx) * G::ES);
             DW8<DT> wt;   // fp16 weights: one ds_read_b128 per tap, consumed by v_fma_mix directly
             wt.load(sl + (ky * 3 + kx) * 32 + 8 * kg);
 #pragma unroll
