@@ -166,11 +166,153 @@ __global__ __launch_bounds__(2 * NWM * 64) void pool_gemm_kernel(const typename 
   }
 }
 
+// K = 32 * KSC fixed (URSONet: 320): each wave keeps its 32 output channels' weights for the whole K in registers
+// (2 channel tiles x KSC fragments, loaded once), so the only LDS traffic is the pixel map, staged 64 pixels x K at a
+// time with one barrier pair per chunk instead of one per 32-wide K step (the kernel above is bound by that per-step
+// round trip). Every wave covers all pixels of its image for its channels: the mean needs no cross-wave reduction.
+// Workgroup = 4 waves = 128 channels of one image; the next chunk's pixels are loaded into registers during the
+// current chunk's MFMAs; full chunks skip the pixel masks; ReLU sums use packed adds. Measured (tools/ab.py, B=64,
+// 512²): 31.3 -> 25.9 us per launch. What is left: 252 VGPRs (2 waves per SIMD) make the 640 workgroups 1.25 rounds
+// of the 512 slots, and holding fewer registers (3 waves per SIMD, one round) spills 33.
+template <typename DT, int KSC>
+__global__ __launch_bounds__(256) void pool_gemm_rk_kernel(const typename DT::T* __restrict__ X,
+                                                           const typename DT::T* __restrict__ Wt,
+                                                           const float* __restrict__ bias, float* __restrict__ pooled,
+                                                           int HW, int N) {
+  using T = typename DT::T;
+  using x8 = typename DT::x8;
+  constexpr int K = 32 * KSC;
+  constexpr int PC = 64;                          // pixels per chunk (4 MFMA pixel tiles)
+  constexpr int RS = K + 16;                      // LDS row stride: K*2 + 32 B = 2 mod 4 granules, conflict-free b128
+  static_assert(((RS * 2 / 16) & 3) == 2, "row stride");
+  constexpr int GPR = K / 8;                      // 16-B pieces per pixel row
+  constexpr int NP = PC * GPR / 256;              // pieces per thread per chunk
+  static_assert(PC * GPR % 256 == 0, "chunk split");
+  __shared__ __attribute__((aligned(16))) T Bs[PC * RS];
+
+  const uint32_t nblk = gridDim.x * gridDim.y;
+  const uint32_t L = xcd_remap(blockIdx.y * gridDim.x + blockIdx.x, nblk);   // an image's channel blocks on one XCD
+  const int b = (int)(L / gridDim.x), n0 = (int)(L % gridDim.x) * 128;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  const int c0 = n0 + 32 * wave;                  // this wave's 32 output channels
+  const T* Xb = X + (size_t)b * HW * K;
+
+  // the wave's weight fragments for all of K (A operand: row = output channel c0 + 16 t + r16)
+  x8 wa[2][KSC];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int ks = 0; ks < KSC; ++ks) wa[t][ks] = load8<DT>(Wt + (size_t)(c0 + 16 * t + r16) * K + 32 * ks + 8 * kg);
+  float4 bb[2];
+#pragma unroll
+  for (int t = 0; t < 2; ++t) bb[t] = *reinterpret_cast<const float4*>(bias + c0 + 16 * t + 4 * kg);
+
+  const int nch = (HW + PC - 1) / PC;
+  // this thread's 16-B pieces of a chunk: pixel row and granule are chunk-invariant (computed once)
+  int prow[NP], pofs[NP];
+#pragma unroll
+  for (int i = 0; i < NP; ++i) {
+    const int p = tid + 256 * i, row = p / GPR;
+    prow[i] = row;
+    pofs[i] = row * RS + 8 * (p - row * GPR);
+  }
+  x8 xr[NP];
+  auto gload = [&](int ch) {   // branch-free: pixels past HW read pixel 0 and are zeroed at the store
+#pragma unroll
+    for (int i = 0; i < NP; ++i) {
+      const int px = ch * PC + prow[i];
+      xr[i] = load8<DT>(Xb + (size_t)(px < HW ? px : 0) * K + (pofs[i] - prow[i] * RS));
+    }
+  };
+  typedef float f32x2 __attribute__((ext_vector_type(2)));
+  f32x2 sum[2][2] = {};   // [channel tile][channel pair]: packed adds
+  gload(0);
+#pragma unroll 1
+  for (int ch = 0; ch < nch; ++ch) {
+    const bool full = (ch + 1) * PC <= HW;   // workgroup-uniform: masks only in a partial last chunk
+    if (ch > 0) __syncthreads();   // every wave's reads of the previous chunk are done
+    if (full) {
+#pragma unroll
+      for (int i = 0; i < NP; ++i) *reinterpret_cast<x8*>(&Bs[pofs[i]]) = xr[i];
+    } else {
+#pragma unroll
+      for (int i = 0; i < NP; ++i)
+        *reinterpret_cast<x8*>(&Bs[pofs[i]]) = ch * PC + prow[i] < HW ? xr[i] : zero8<DT>();
+    }
+    __syncthreads();
+    if (ch + 1 < nch) gload(ch + 1);   // in flight across this chunk's MFMAs
+    f32x4 acc[2][4];
+#pragma unroll
+    for (int ks = 0; ks < KSC; ++ks) {
+      x8 bf[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) bf[q] = *reinterpret_cast<const x8*>(&Bs[(q * 16 + r16) * RS + 32 * ks + 8 * kg]);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)   // bias as the first MFMA's C operand
+          acc[t][q] = DT::mfma(wa[t][ks], bf[q], ks == 0 ? f32x4{bb[t].x, bb[t].y, bb[t].z, bb[t].w} : acc[t][q]);
+    }
+    if (full) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            sum[t][e] += f32x2{fmaxf(acc[t][q][2 * e], 0.f), fmaxf(acc[t][q][2 * e + 1], 0.f)};
+    } else {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float pv = ch * PC + q * 16 + r16 < HW ? 1.f : 0.f;
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int e = 0; e < 2; ++e)
+            sum[t][e] += f32x2{fmaxf(acc[t][q][2 * e], 0.f), fmaxf(acc[t][q][2 * e + 1], 0.f)} * pv;
+      }
+    }
+  }
+  // reduce over the 16 pixel lanes; lane r16 == 0 of each channel group writes its 4 channels' means
+  float red[2][4];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float v = sum[t][e >> 1][e & 1];
+      v += __shfl_xor(v, 1, 64);
+      v += __shfl_xor(v, 2, 64);
+      v += __shfl_xor(v, 4, 64);
+      v += __shfl_xor(v, 8, 64);
+      red[t][e] = v;
+    }
+  if (r16 == 0) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int c = c0 + 16 * t + 4 * kg;
+      float4 o = make_float4(red[t][0] / (float)HW, red[t][1] / (float)HW, red[t][2] / (float)HW,
+                             red[t][3] / (float)HW);
+      if (c + 3 < N) *reinterpret_cast<float4*>(pooled + (size_t)b * N + c) = o;
+      else
+        for (int e = 0; e < 4; ++e)
+          if (c + e < N) pooled[(size_t)b * N + c + e] = (&o.x)[e];
+    }
+  }
+}
+
 hipError_t launch_pool_gemm(int dtype, const void* x, const void* wt, const float* bias, float* pooled, int B, int HW,
                             int K, int N, hipStream_t s) {
   const int Kp = (K + 31) & ~31, Np = (N + 15) & ~15;
   if ((K & 7) || (Np % 128)) return hipErrorInvalidValue;
   dim3 g(Np / 128, B);
+  if (K == 320) {   // the URSONet last conv: register-resident weights, one barrier pair per 64-pixel chunk
+    if (dtype == DT_F16)
+      pool_gemm_rk_kernel<F16, 10><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, N);
+    else
+      pool_gemm_rk_kernel<BF16, 10><<<g, 256, 0, s>>>((const __bf16*)x, (const __bf16*)wt, bias, pooled, HW, N);
+    return hipGetLastError();
+  }
   if (dtype == DT_F16) {
     if (Kp == 320)
       pool_gemm_kernel<F16, 10, SPEF_POOL_MT, SPEF_POOL_NWM><<<g, 2 * SPEF_POOL_NWM * 64, 0, s>>>((const _Float16*)x, (const _Float16*)wt, bias, pooled, HW, K, Kp, N);
