@@ -22,15 +22,12 @@ __global__ __launch_bounds__(256) void stem_kernel(const void* __restrict__ in, 
   for (int i = threadIdx.x; i < 27 * 32; i += 256) sw[i] = w[i];
   if (threadIdx.x < 32) sb[threadIdx.x] = bias[threadIdx.x];
   __syncthreads();
-  const int64_t total = (int64_t)B * OH * OW * 4;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= total) return;
-  const int g = (int)(idx & 3);
-  int64_t p = idx >> 2;
-  const int ox = (int)(p % OW);
-  p /= OW;
-  const int oy = (int)(p % OH);
-  const int b = (int)(p / OH);
+  // grid = output rows x ceil(OW * 4 / 256) blocks per row (workgroup-uniform row split, as dw_kernel)
+  const int RW = OW * 4, nbx = (RW + 255) >> 8;
+  const int row = (int)blockIdx.x / nbx, t = ((int)blockIdx.x - row * nbx) * 256 + (int)threadIdx.x;
+  if (t >= RW) return;
+  const int g = t & 3, ox = t >> 2;
+  const int oy = row % OH, b = row / OH;
 
   float xin[27];
 #pragma unroll
@@ -158,16 +155,14 @@ __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restric
                                                  const float* __restrict__ bias, typename DT::T* __restrict__ Y,
                                                  int B, int H, int W, int C, int OH, int OW) {
   using T = typename DT::T;
-  const int CG = C >> 3;
-  const int64_t total = (int64_t)B * OH * OW * CG;
-  const int64_t idx = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= total) return;
-  const int cg = (int)(idx % CG);
-  int64_t p = idx / CG;
-  const int ox = (int)(p % OW);
-  p /= OW;
-  const int oy = (int)(p % OH);
-  const int b = (int)(p / OH);
+  // grid = output rows x ceil(OW * C/8 / 256) blocks per row: the row split is workgroup-uniform (scalar), the
+  // per-thread (column, channel group) split one 32-bit division (64-bit div/mod per thread cost more than the
+  // arithmetic on the fp32 path)
+  const int CG = C >> 3, RW = OW * CG, nbx = (RW + 255) >> 8;
+  const int row = (int)blockIdx.x / nbx, t = ((int)blockIdx.x - row * nbx) * 256 + (int)threadIdx.x;
+  if (t >= RW) return;
+  const int ox = t / CG, cg = t - ox * CG;
+  const int oy = row % OH, b = row / OH;
   const int c = cg * 8;
   float acc[8];
   {
@@ -303,7 +298,9 @@ static inline unsigned blocks_for(int64_t n, int per) { return (unsigned)((n + p
 
 hipError_t launch_stem(int dtype, int in_layout, const void* in, const float* w, const float* bias, void* y, int B,
                        int H, int W, int OH, int OW, hipStream_t s) {
-  const unsigned g = blocks_for((int64_t)B * OH * OW * 4, 256);
+  const int64_t g64 = (int64_t)B * OH * (((int64_t)OW * 4 + 255) / 256);
+  if (g64 > 0x7fffffff) return hipErrorInvalidValue;
+  const unsigned g = (unsigned)g64;
   if (dtype == DT_F32) {
     if (in_layout == IN_U8_NHWC)
       stem_kernel<F32, IN_U8_NHWC><<<g, 256, 0, s>>>(in, w, bias, (float*)y, B, H, W, OH, OW);
@@ -372,7 +369,9 @@ hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias
                      int stride, int OH, int OW, bool pairs, hipStream_t s) {
   if (C & 7) return hipErrorInvalidValue;
   if (pairs && dtype != DT_F16) return hipErrorInvalidValue;
-  const unsigned g = blocks_for((int64_t)B * OH * OW * (C / 8), 256);
+  const int64_t g64 = (int64_t)B * OH * (((int64_t)OW * (C / 8) + 255) / 256);
+  if (g64 > 0x7fffffff || (int64_t)OW * (C / 8) > 0x7fffffff) return hipErrorInvalidValue;
+  const unsigned g = (unsigned)g64;
   if (pairs) {
     if (stride == 1)
       dw_kernel<F16, 1, true><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
