@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void pw_kernel(const typename DT::T* __restric
 }
 
 // ------------------------------------------------------------------------------------------ depthwise
-template <typename DT, int S, bool VP = false>
+template <typename DT, int S, int MODE = DW_FP32>
 __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restrict__ X, const typename DT::DW* __restrict__ W9,
                                                  const float* __restrict__ bias, typename DT::T* __restrict__ Y,
                                                  int B, int H, int W, int C, int OH, int OW) {
@@ -164,6 +164,29 @@ __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restric
   const int ox = t / CG, cg = t - ox * CG;
   const int oy = row % OH, b = row / OH;
   const int c = cg * 8;
+  if constexpr (MODE == DW_PK16) {
+    // packed fp16 (k_irb.hip, fp16 stride-2 blocks): 4 x v_pk_fma_f16 per tap, accumulator = the bias rounded to
+    // fp16, kx outer / ky inner, taps outside the image multiply a zero -- the fused kernel's operations and order
+    const float4 b0 = *reinterpret_cast<const float4*>(bias + c);
+    const float4 b1 = *reinterpret_cast<const float4*>(bias + c + 4);
+    f16x2 a[4] = {f16x2{(_Float16)b0.x, (_Float16)b0.y}, f16x2{(_Float16)b0.z, (_Float16)b0.w},
+                  f16x2{(_Float16)b1.x, (_Float16)b1.y}, f16x2{(_Float16)b1.z, (_Float16)b1.w}};
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      const int ix = ox * S - 1 + kx;
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const int iy = oy * S - 1 + ky;
+        const bool in = ix >= 0 && ix < W && iy >= 0 && iy < H;
+        const uint4 xv = in ? *reinterpret_cast<const uint4*>(X + (((int64_t)b * H + iy) * W + ix) * C + c)
+                            : make_uint4(0, 0, 0, 0);
+        const uint4 wv = *reinterpret_cast<const uint4*>(W9 + (ky * 3 + kx) * C + c);
+        pk_fma4(a, xv, wv);
+      }
+    }
+    *reinterpret_cast<uint4*>(Y + (((int64_t)b * OH + oy) * OW + ox) * C + c) = relu_pk4(a);
+    return;
+  }
   float acc[8];
   {
     const float4 b0 = *reinterpret_cast<const float4*>(bias + c);
@@ -171,7 +194,7 @@ __global__ __launch_bounds__(256) void dw_kernel(const typename DT::T* __restric
     acc[0] = b0.x; acc[1] = b0.y; acc[2] = b0.z; acc[3] = b0.w;
     acc[4] = b1.x; acc[5] = b1.y; acc[6] = b1.z; acc[7] = b1.w;
   }
-  if constexpr (VP) {
+  if constexpr (MODE == DW_PAIRS) {
     // vertical pairs (k_irb.hip, fp16 blocks 2-7): per kernel column, even output rows (and every stride-2 row)
     // dot2(ky 0, 1) then fma(ky 2); odd stride-1 rows fma(ky 0) then dot2(ky 1, 2). Rows outside the image are 0
     // (the fused kernels' zero padding), so the same instructions see the same operands.
@@ -366,33 +389,21 @@ hipError_t launch_pw(int dtype, int epi, const void* x, const void* wt, const fl
 }
 
 hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias, void* y, int B, int H, int W, int C,
-                     int stride, int OH, int OW, bool pairs, hipStream_t s) {
+                     int stride, int OH, int OW, int mode, hipStream_t s) {
   if (C & 7) return hipErrorInvalidValue;
-  if (pairs && dtype != DT_F16) return hipErrorInvalidValue;
+  if (mode != DW_FP32 && (dtype != DT_F16 || (mode != DW_PAIRS && mode != DW_PK16))) return hipErrorInvalidValue;
   const int64_t g64 = (int64_t)B * OH * (((int64_t)OW * (C / 8) + 255) / 256);
   if (g64 > 0x7fffffff || (int64_t)OW * (C / 8) > 0x7fffffff) return hipErrorInvalidValue;
   const unsigned g = (unsigned)g64;
-  if (pairs) {
-    if (stride == 1)
-      dw_kernel<F16, 1, true><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
-    else
-      dw_kernel<F16, 2, true><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
-  } else if (dtype == DT_F32) {
-    if (stride == 1)
-      dw_kernel<F32, 1><<<g, 256, 0, s>>>((const float*)x, (const float*)w9, bias, (float*)y, B, H, W, C, OH, OW);
-    else
-      dw_kernel<F32, 2><<<g, 256, 0, s>>>((const float*)x, (const float*)w9, bias, (float*)y, B, H, W, C, OH, OW);
-  } else if (dtype == DT_F16) {
-    if (stride == 1)
-      dw_kernel<F16, 1><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
-    else
-      dw_kernel<F16, 2><<<g, 256, 0, s>>>((const _Float16*)x, (const _Float16*)w9, bias, (_Float16*)y, B, H, W, C, OH, OW);
-  } else {
-    if (stride == 1)
-      dw_kernel<BF16, 1><<<g, 256, 0, s>>>((const __bf16*)x, (const float*)w9, bias, (__bf16*)y, B, H, W, C, OH, OW);
-    else
-      dw_kernel<BF16, 2><<<g, 256, 0, s>>>((const __bf16*)x, (const float*)w9, bias, (__bf16*)y, B, H, W, C, OH, OW);
-  }
+#define SPEF_DW(DT_, TT, WT, M_)                                                                                     \
+  (stride == 1 ? dw_kernel<DT_, 1, M_><<<g, 256, 0, s>>>((const TT*)x, (const WT*)w9, bias, (TT*)y, B, H, W, C, OH, OW) \
+               : dw_kernel<DT_, 2, M_><<<g, 256, 0, s>>>((const TT*)x, (const WT*)w9, bias, (TT*)y, B, H, W, C, OH, OW))
+  if (mode == DW_PAIRS) SPEF_DW(F16, _Float16, _Float16, DW_PAIRS);
+  else if (mode == DW_PK16) SPEF_DW(F16, _Float16, _Float16, DW_PK16);
+  else if (dtype == DT_F32) SPEF_DW(F32, float, float, DW_FP32);
+  else if (dtype == DT_F16) SPEF_DW(F16, _Float16, _Float16, DW_FP32);
+  else SPEF_DW(BF16, __bf16, float, DW_FP32);
+#undef SPEF_DW
   return hipGetLastError();
 }
 

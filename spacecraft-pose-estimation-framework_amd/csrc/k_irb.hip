@@ -26,11 +26,25 @@ namespace spef {
 // Vertical-pair depthwise (VP, fp16 stride-1 blocks 3, 5, 6, 8-13): the hidden slab holds, per position (row pair pr,
 // column), one dword per channel = (row 2pr, row 2pr+1) -- the depthwise takes two taps of a kernel column with one
 // v_dot2_f32_f16 and the third with one v_fma_mix. The unfused dw_kernel uses the same order for these blocks
-// (irb_dw_pairs), so both schedules stay bit-identical. (Stride 2 measured slower: a 3-row window straddles two
+// (irb_dw_mode), so both schedules stay bit-identical. (Stride 2 measured slower: a 3-row window straddles two
 // pairs, so every output row reads 1.5x the slab bytes, and the odd input-tile height wastes half a pair row.)
 // Blocks 8-13 (hid 384, 576) run the same pair order in the role-split kernel (k_irw.hip); their slab-kernel variants
 // follow it so every schedule of those blocks stays bit-identical.
-constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) { return f16 && expand && hid <= 576 && stride == 1; }
+// Packed-fp16 depthwise (PK, fp16 stride-2 blocks 2, 4, 7): 4 v_pk_fma_f16 per tap for a lane's 8 channels (two
+// channels per op, fp16 accumulation from the fp16-rounded bias, one rounding per fused tap) instead of 8 v_fma_mix
+// -- half the depthwise VALU of the VALU-issue-bound high-resolution blocks. The ReLU'd sums are the project MFMA's B
+// fragment as they are (no convert). Error budget (tools/dw_acc_budget.py, float64 restatement at 512^2): URSONet
+// logits 5.26e-4 -> 5.76e-4 max |d| against fp32, inside the north star's 1e-3. The unfused dw_kernel<DW_PK16>
+// evaluates the same operations in the same order (bit-identical).
+// Blocks 2, 4, 7 (stride 2) and 5-6 (hid 192). Block 3 and the role-split blocks 8-13 (k_irw.hip) keep the vertical
+// pairs: there the plain slab's larger footprint / read pattern costs more than the VALU saved (measured +15 us on
+// block 3, +10 to +29 us per role-split kernel, against -4 to -5 us on blocks 2 and 5-6).
+constexpr bool irb_pk(bool f16, int hid, bool expand, int stride) {
+  return f16 && expand && (stride == 2 ? hid <= 192 : hid == 192);
+}
+constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) {
+  return f16 && expand && hid <= 576 && stride == 1 && !irb_pk(f16, hid, expand, stride);
+}
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
           bool STW, int DWB = 4, bool VP = false>
@@ -119,6 +133,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     int tiles_y, uint32_t nwg) {
   using DW = typename DT::DW;
   constexpr bool VP = irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
+  constexpr bool PK = irb_pk(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
   using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
@@ -269,7 +284,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     for (int j = 0; j < NBI; ++j) {   // all biases, once
       const int u = tid + NW * 64 * j;
       if (u < G::NCH * 32) {
-        Bd[u] = u < HID ? bdv[j] : 0.f;
+        if constexpr (PK) reinterpret_cast<_Float16*>(Bd)[u] = (_Float16)(u < HID ? bdv[j] : 0.f);   // fp16 bias
+        else Bd[u] = u < HID ? bdv[j] : 0.f;
         if constexpr (EXPAND) Be[u] = u < HID ? bev[j] : 0.f;
       }
     }
@@ -560,7 +576,52 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     // and unfused schedules accumulate in the same order and stay bit-identical.
     // (no channel-validity branch below: channels >= HID of a partial chunk are zero in the slab, the depthwise
     // weights and bias, so they yield ReLU(0) = +0 exactly like an explicit zero fragment)
-    if constexpr (VP) {
+    if constexpr (PK && G::PAIR) {
+      // stride 1: two vertically adjacent output rows per step share each kernel column's 4 input rows and 3 weights
+#pragma unroll
+      for (int qi = 0; qi < G::QPW; qi += 2) {
+        const uint4 bh = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(Bd) + 32 * c + 8 * kg);
+        f16x2 a0[4] = {__builtin_bit_cast(f16x2, bh.x), __builtin_bit_cast(f16x2, bh.y),
+                       __builtin_bit_cast(f16x2, bh.z), __builtin_bit_cast(f16x2, bh.w)};
+        f16x2 a1[4] = {a0[0], a0[1], a0[2], a0[3]};
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          uint4 w[3], v[4];
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) w[ky] = *reinterpret_cast<const uint4*>(sl + (ky * 3 + kx) * 32 + 8 * kg);
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = *reinterpret_cast<const uint4*>(Es + dwoff[qi] + (r * G::IW + kx) * G::ES);
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            pk_fma4(a0, v[ky], w[ky]);
+            pk_fma4(a1, v[ky + 1], w[ky]);
+          }
+        }
+        const x8 bf0 = __builtin_bit_cast(x8, relu_pk4(a0)), bf1 = __builtin_bit_cast(x8, relu_pk4(a1));
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) {
+          acc[qi][t] = DT::mfma(pa[t], bf0, acc[qi][t]);
+          acc[qi + 1][t] = DT::mfma(pa[t], bf1, acc[qi + 1][t]);
+        }
+      }
+    } else if constexpr (PK) {
+#pragma unroll
+      for (int qi = 0; qi < G::QPW; ++qi) {
+        const uint4 bh = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(Bd) + 32 * c + 8 * kg);
+        f16x2 a[4] = {__builtin_bit_cast(f16x2, bh.x), __builtin_bit_cast(f16x2, bh.y),
+                      __builtin_bit_cast(f16x2, bh.z), __builtin_bit_cast(f16x2, bh.w)};
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+            pk_fma4(a, *reinterpret_cast<const uint4*>(Es + dwoff[qi] + (ky * G::IW + kx) * G::ES),
+                    *reinterpret_cast<const uint4*>(sl + (ky * 3 + kx) * 32 + 8 * kg));
+        const uint4 o = relu_pk4(a);
+        const x8 bf = __builtin_bit_cast(x8, o);
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
+      }
+    } else if constexpr (VP) {
       // Per kernel column kx: two taps by v_dot2 on a row pair, the third by v_fma_mix on one half. Output row
       // parity fixes the order: even rows (and every stride-2 row) dot2(ky 0,1) then fma(ky 2); odd rows
       // fma(ky 0) then dot2(ky 1,2) -- exactly dw_kernel<.., VP>'s order.
@@ -859,7 +920,10 @@ static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stri
   return hipErrorNotSupported;
 }
 
-bool irb_dw_pairs(int dtype, int hid, bool expand, int stride) { return irb_vp(dtype == DT_F16, hid, expand, stride); }
+int irb_dw_mode(int dtype, int hid, bool expand, int stride) {
+  return irb_vp(dtype == DT_F16, hid, expand, stride) ? DW_PAIRS
+         : irb_pk(dtype == DT_F16, hid, expand, stride) ? DW_PK16 : DW_FP32;
+}
 
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
   return irb_has(0, cin, hid, cout, stride, expand, res);

@@ -38,7 +38,7 @@ namespace spef {
 // position, one dword per channel = (row 2m, row 2m+1), in four 8-channel regions (k_irb.hip's VP layout); a kernel
 // column's taps ky 0,1 (or 1,2) are one v_dot2_f32_f16 and the third one v_fma_mix: 6 instead of 9 VALU per 3x3
 // tap set. The depthwise weights are staged once as (w[0][kx], w[1][kx]) / (w[1][kx], w[2][kx]) pairs. The unfused
-// dw_kernel (irb_dw_pairs) evaluates the same instructions in the same order: bit-identical.
+// dw_kernel (irb_dw_mode) evaluates the same instructions in the same order: bit-identical.
 constexpr bool irw_vp(bool f16, int s, int th, int tw) { return f16 && s == 1 && tw == 16 && th % 2 == 0; }
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, int NE, int ND, int WCO, int DWB, bool VP = false>

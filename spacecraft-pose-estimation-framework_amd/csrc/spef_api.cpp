@@ -345,12 +345,13 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         }
         void* h2 = pick({x, h1});
         const double opx = (double)B * OH * OW;
-        const bool dw_pairs = irb_dw_pairs(dt, (int)op.hidden, expand, (int)op.stride);
-        HIP_TRY(prof_launch(c, s, op.stride == 1 ? (dw_pairs ? "dw_kernel<1,pairs>" : "dw_kernel<1>")
-                                                 : (dw_pairs ? "dw_kernel<2,pairs>" : "dw_kernel<2>"),
+        const int dw_mode = irb_dw_mode(dt, (int)op.hidden, expand, (int)op.stride);
+        static const char* const dw_names[2][3] = {{"dw_kernel<1>", "dw_kernel<1,pairs>", "dw_kernel<1,pk16>"},
+                                                   {"dw_kernel<2>", "dw_kernel<2,pairs>", "dw_kernel<2,pk16>"}};
+        HIP_TRY(prof_launch(c, s, dw_names[op.stride == 1 ? 0 : 1][dw_mode],
                             ((double)B * h * w + opx) * op.hidden * es + 40.0 * op.hidden, opx * op.hidden * 18.0, [&] {
           return launch_dw(dt, h1, ptr<void>(c, op.w1), ptr<float>(c, op.b1), h2, B, h, w, (int)op.hidden,
-                           (int)op.stride, OH, OW, dw_pairs, s);
+                           (int)op.stride, OH, OW, dw_mode, s);
         }));
         void* y = res ? pick({x, h2}) : pick({h2});
         const int64_t M2 = (int64_t)B * OH * OW;

@@ -156,6 +156,22 @@ __device__ __forceinline__ uint32_t relu_pk2(float lo, float hi) {
   return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(p, z));
 }
 
+// Packed-fp16 depthwise step (fp16 stride-2 blocks): a[i] += x[i] * w[i] for 8 channels as 4 v_pk_fma_f16 (fused,
+// one fp16 rounding per tap), and the ReLU of the 8 sums as 4 v_pk_max_f16
+__device__ __forceinline__ void pk_fma4(f16x2 a[4], uint4 x, uint4 w) {
+  const uint32_t xs[4] = {x.x, x.y, x.z, x.w}, ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    a[i] = __builtin_elementwise_fma(__builtin_bit_cast(f16x2, xs[i]), __builtin_bit_cast(f16x2, ws[i]), a[i]);
+}
+__device__ __forceinline__ uint4 relu_pk4(const f16x2 a[4]) {
+  const f16x2 z = {(_Float16)0.0f, (_Float16)0.0f};
+  uint32_t o[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) o[i] = __builtin_bit_cast(uint32_t, __builtin_elementwise_max(a[i], z));
+  return make_uint4(o[0], o[1], o[2], o[3]);
+}
+
 template <typename DT>
 __device__ __forceinline__ typename DT::x8 zero8() {
   typename DT::x8 z;

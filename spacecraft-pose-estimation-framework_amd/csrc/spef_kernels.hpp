@@ -30,9 +30,10 @@ hipError_t launch_gemm_pw(int dtype, int epi, const void* x, const void* wt, con
 const char* gemm_key(int dtype, int epi, int N);
 
 // Depthwise 3x3 conv, pad 1, stride 1|2, BN folded, ReLU. W9: [9][C] (fp16 for fp16 blobs, fp32 for bf16),
-// bias fp32 [C]. pairs: the vertical-pair tap order of the fused fp16 blocks 3, 5, 6 (irb_dw_pairs; fp16 only).
+// bias fp32 [C]. mode (irb_dw_mode; fp16 only for mode > 0): DW_PAIRS = the vertical-pair tap order of the fused fp16
+// stride-1 blocks, DW_PK16 = the packed-fp16 accumulation of the fused fp16 stride-2 blocks.
 hipError_t launch_dw(int dtype, const void* x, const void* w9, const float* bias, void* y, int B, int H, int W,
-                     int C, int stride, int OH, int OW, bool pairs, hipStream_t s);
+                     int C, int stride, int OH, int OW, int mode, hipStream_t s);
 
 // Last 1x1 conv (+BN, ReLU) fused with the global mean over HW: pooled fp32 [B][N].
 hipError_t launch_pw_pool(int dtype, const void* x, const void* wt, const float* bias, float* pooled, int B,
@@ -49,9 +50,11 @@ hipError_t launch_fc(const float* x, const float* w, const float* bias, float* o
 
 // Fused InvertedResidual block (expand -> depthwise -> project [+x]) for the geometries in k_irb.hip's table.
 bool irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
-// true when the fused kernel of this block evaluates its depthwise in vertical pairs (v_dot2_f32_f16 + v_fma_mix):
-// the unfused schedule must then run dw_kernel with the same order to stay bit-identical
-bool irb_dw_pairs(int dtype, int hid, bool expand, int stride);
+// How the fused kernel of this block evaluates its depthwise: DW_FP32 (v_fma_mix, fp32 accumulation), DW_PAIRS
+// (vertical pairs: v_dot2_f32_f16 + v_fma_mix) or DW_PK16 (v_pk_fma_f16: two channels per op, fp16 accumulation).
+// The unfused schedule runs dw_kernel in the same mode to stay bit-identical.
+enum { DW_FP32 = 0, DW_PAIRS = 1, DW_PK16 = 2 };
+int irb_dw_mode(int dtype, int hid, bool expand, int stride);
 hipError_t launch_irb(int variant, int dtype, int cin, int hid, int cout, int stride, bool expand, bool res, const void* x,
                       const void* we, const float* be, const void* wd, const float* bd, const void* wp,
                       const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
