@@ -375,7 +375,7 @@ def main():
     ap.add_argument('--gpus', type=int, default=1)
     ap.add_argument('--steps', type=int, default=100)
     ap.add_argument('--warmup', type=int, default=10)
-    ap.add_argument('--settle', type=float, default=0.3,
+    ap.add_argument('--settle', type=float, default=0.5,
                     help='seconds of untimed steps before the warm-up steps (shader clock out of idle; 0 = off)')
     ap.add_argument('--batch', type=int, default=64)
     ap.add_argument('--size', type=int, default=512)
