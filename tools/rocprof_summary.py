@@ -69,12 +69,16 @@ def main():
     ap.add_argument('--leg', type=int, default=0,
                     help="bench.py's single-stream HIP-event leg = the last LEG steps of the traced run")
     ap.add_argument('--total', type=int, default=0, help='all steps of the traced run (warmup + steps + leg)')
+    ap.add_argument('--per-step', default='',
+                    help='a kernel launched once per step (e.g. front_vp_kernel): the leg of every kernel is then its '
+                         'last LEG x (its dispatches / this kernel\'s dispatches), whatever the number of steps '
+                         '(bench.py\'s time-based settle phase makes --total unknown)')
     a = ap.parse_args()
     out = os.path.join(ROOT, 'profiles')
     os.makedirs(out, exist_ok=True)
     st = glob.glob(os.path.join(a.stats, '*kernel_stats.csv'))[0]
     shutil.copy(st, os.path.join(out, f'{a.tag}_kernel_stats.csv'))
-    if a.leg and a.total:
+    if a.leg and (a.total or a.per_step):
         # Per kernel, the dispatches of bench.py's roofline leg (one stream, no overlap with other batches): the
         # durations bench.py's HIP events measure. The pipelined steps before it overlap up to --inflight batches,
         # which stretches their individual kernel durations in the --stats average.
@@ -87,7 +91,11 @@ def main():
             w.writerow(['Name', 'LegCalls', 'AverageNs', 'MinNs', 'MaxNs', 'AllCalls', 'AllAverageNs'])
             for k, v in sorted(by.items(), key=lambda kv: -sum(e - s for s, e in kv[1])):
                 v.sort()
-                n = max(1, round(len(v) * a.leg / a.total))
+                if a.per_step:
+                    ref = next(len(x) for kk, x in by.items() if kk.startswith(a.per_step))
+                    n = max(1, min(len(v), round(a.leg * len(v) / ref)))
+                else:
+                    n = max(1, round(len(v) * a.leg / a.total))
                 d = [e - s for s, e in v[-n:]]
                 alld = [e - s for s, e in v]
                 w.writerow([k, n, round(sum(d) / n, 1), min(d), max(d), len(v), round(sum(alld) / len(alld), 1)])
