@@ -45,9 +45,20 @@ constexpr bool irb_pk(bool f16, int hid, bool expand, int stride) {
 constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) {
   return f16 && expand && hid <= 576 && stride == 1 && !irb_pk(f16, hid, expand, stride);
 }
+// PK with wave-uniform depthwise weights (PKU; the 4-wave, single-slab PK configurations): in the depthwise phase wave
+// g owns channels 8g..8g+7 of the chunk for every output pixel of the tile (a lane per pixel, or per vertical pixel
+// pair on the 8x16 stride-1 tiles), so a tap's 8 weights are one wave-uniform 16-B scalar load used straight from
+// SGPRs by v_pk_fma_f16 -- no LDS weight slab and none of its 9 ds_read_b128 per chunk and wave. The ReLU'd sums go
+// to a 64/128-pixel LDS buffer from which each wave reads its project B fragments after one barrier (the barrier
+// before the next expand is then redundant, so the barrier count is unchanged). Same operations in the same order as
+// the lane-per-channel-group PK path and dw_kernel<DW_PK16>.
+constexpr bool irb_pku(bool pk, int nw, bool dbuf, bool stw, int s, int th, int tw) {
+  return pk && nw == 4 && !dbuf && !stw && th * tw == 64;   // 128-pixel tiles: the buffer costs a workgroup per CU
+}
+constexpr int IRB_DSU = 48;   // PKU buffer row (halves): 96 B = 6 granules, 2 mod 4 -> conflict-free ds_read_b128
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
-          bool STW, int DWB = 4, bool VP = false>
+          bool STW, int DWB = 4, bool VP = false, bool PKU = false>
 struct IrbGeom {
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW;
@@ -86,7 +97,8 @@ struct IrbGeom {
   static constexpr int W_PPT = (WE_PIECES + WP_PIECES + NW * 64 - 1) / (NW * 64);   // 16-B pieces per thread
   static constexpr int bytes_for(int xs, int es) {
     return VP ? (PINP * xs + WE_ELEMS + WP_ELEMS) * 2 + NBUF * 4 * RS + 2 * VSLAB * 4 + BIAS * 4
-              : (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 + 2 * SLAB * DWB + BIAS * 4;
+              : (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 +
+                    (PKU ? TH * TW * IRB_DSU * 2 : 2 * SLAB * DWB) + BIAS * 4;
   }
   // Xs / slab row strides: the first of (conflict-free, +16 B, unpadded Xs) that reaches the most workgroups per
   // CU. The LDS, not the VGPRs, sets the slab kernels' occupancy (3-5 waves per SIMD), and an unpadded input tile
@@ -134,7 +146,8 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   using DW = typename DT::DW;
   constexpr bool VP = irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
   constexpr bool PK = irb_pk(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP>;
+  constexpr bool PKU = irb_pku(PK, NW, DBUF, STW, S, TH, TW);
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP, PKU>;
   using T = typename DT::T;
   using x8 = typename DT::x8;
   using x4 = typename DT::x4;
@@ -147,7 +160,10 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   T* WPs = WEs + G::WE_ELEMS;                                               // [2][NCTP][WPS] project weights
   DW* Sl = reinterpret_cast<DW*>(WPs + G::WP_ELEMS);                        // [2][SLAB] dw weights
   uint32_t* Slv = reinterpret_cast<uint32_t*>(Sl);                          // VP: [2][VSLAB] weight pairs
-  float* Bd = reinterpret_cast<float*>(reinterpret_cast<char*>(Sl) + (VP ? 2 * G::VSLAB * 4 : 2 * G::SLAB * (int)sizeof(DW)));
+  T* Dk = reinterpret_cast<T*>(Sl);                                         // PKU: [POUT][IRB_DSU] depthwise out
+  float* Bd = reinterpret_cast<float*>(reinterpret_cast<char*>(Sl) + (VP    ? 2 * G::VSLAB * 4
+                                                                      : PKU ? G::POUT * IRB_DSU * 2
+                                                                            : 2 * G::SLAB * (int)sizeof(DW)));
   float* Be = Bd + G::NCH * 32;                                             // [HIDP] expand bias
 
   SPEF_TRACE(0);   // timeline probes (tools/kbench/blk_trace.hip irb): nothing in the library build
@@ -170,10 +186,12 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   // from two 8-B pieces of the [9][HID] fp16 weights
   const int vt = NW * 64 - 1 - tid;   // VP piece index: the last wave (fewest expand units) builds the pairs
   auto slab_ok = [&](int cc) {
+    if constexpr (PKU) return false;
     if constexpr (VP) return vt < 48 && cc < G::NCH && 32 * cc + 4 * (vt & 7) < HID;
     return ABL != 7 && tid < G::SLAB_PIECES && cc < G::NCH && 32 * cc + ((tid * EPP) & 31) < HID;
   };
   auto slab_load = [&](int cc) -> uint4 {
+    if constexpr (PKU) return make_uint4(0, 0, 0, 0);   // (no weight slab)
     if constexpr (VP) {
       const int kx = vt >> 4, ky = (vt >> 3) & 1;
       const bool ok = slab_ok(cc);
@@ -186,6 +204,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     return *reinterpret_cast<const uint4*>(Wd + (slab_ok(cc) ? tap * HID + ch : 0));
   };
   auto slab_store = [&](int cc, uint4 v) {
+    if constexpr (PKU) return;
     if constexpr (VP) {
       if (vt < 48) {
         const int kx = vt >> 4, ky = (vt >> 3) & 1;
@@ -390,9 +409,9 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     }
     const T* Es;
     if constexpr (EXPAND) {
-      if constexpr (G::NBUF == 1) {
-        if (c > 0) __syncthreads();   // single hidden slab: all depthwise reads of chunk c-1 done
-      }
+      if constexpr (G::NBUF == 1 && !PKU) {
+        if (c > 0) __syncthreads();   // single hidden slab: all depthwise reads of chunk c-1 done (PKU: the barrier
+      }                               // between its depthwise and project already separates them)
       T* Ew = (c & 1) ? Es1 : Es0;
       const int vh = HID - 32 * c < 32 ? HID - 32 * c : 32;   // valid hidden channels in this chunk
       // ---- 2. expand: E[p][h] = relu(sum_k X[p][k] We[32c+h][k] + be) for all tile pixels
@@ -576,7 +595,51 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     // and unfused schedules accumulate in the same order and stay bit-identical.
     // (no channel-validity branch below: channels >= HID of a partial chunk are zero in the slab, the depthwise
     // weights and bias, so they yield ReLU(0) = +0 exactly like an explicit zero fragment)
-    if constexpr (PK && G::PAIR) {
+    if constexpr (PKU) {
+      const int g = __builtin_amdgcn_readfirstlane(wave);   // this wave's channel group in the depthwise phase
+      const uint4* wsrc = reinterpret_cast<const uint4*>(Wd + 32 * c + 8 * g);   // wave-uniform: scalar loads
+      uint4 wt[9];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) wt[tap] = wsrc[tap * (HID / 8)];
+      const uint4 bh = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(Bd) + 32 * c + 8 * g);
+      const f16x2 b2[4] = {__builtin_bit_cast(f16x2, bh.x), __builtin_bit_cast(f16x2, bh.y),
+                           __builtin_bit_cast(f16x2, bh.z), __builtin_bit_cast(f16x2, bh.w)};
+      if constexpr (G::POUT == 64) {
+        const int oy = lane / TW, ox = lane % TW;
+        f16x2 a[4] = {b2[0], b2[1], b2[2], b2[3]};
+        const T* e0 = Es + (oy * S * G::IW + ox * S) * G::ES + 8 * g;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+            pk_fma4(a, *reinterpret_cast<const uint4*>(e0 + (ky * G::IW + kx) * G::ES), wt[ky * 3 + kx]);
+        *reinterpret_cast<uint4*>(Dk + lane * IRB_DSU + 8 * g) = relu_pk4(a);
+      } else {   // 8x16 stride-1 tile: lane = (row pair, column), rows 2rp and 2rp + 1 share the column's 4 input rows
+        const int rp = lane >> 4, ox = lane & 15;
+        f16x2 a0[4] = {b2[0], b2[1], b2[2], b2[3]}, a1[4] = {b2[0], b2[1], b2[2], b2[3]};
+        const T* e0 = Es + (2 * rp * G::IW + ox) * G::ES + 8 * g;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          uint4 v[4];
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[r] = *reinterpret_cast<const uint4*>(e0 + (r * G::IW + kx) * G::ES);
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky) {
+            pk_fma4(a0, v[ky], wt[ky * 3 + kx]);
+            pk_fma4(a1, v[ky + 1], wt[ky * 3 + kx]);
+          }
+        }
+        *reinterpret_cast<uint4*>(Dk + (2 * rp * 16 + ox) * IRB_DSU + 8 * g) = relu_pk4(a0);
+        *reinterpret_cast<uint4*>(Dk + ((2 * rp + 1) * 16 + ox) * IRB_DSU + 8 * g) = relu_pk4(a1);
+      }
+      __syncthreads();   // every channel group of every pixel in Dk
+#pragma unroll
+      for (int qi = 0; qi < G::QPW; ++qi) {
+        const x8 bf = *reinterpret_cast<const x8*>(Dk + ((wp * G::QPW + qi) * 16 + r16) * IRB_DSU + 8 * kg);
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
+      }
+    } else if constexpr (PK && G::PAIR) {
       // stride 1: two vertically adjacent output rows per step share each kernel column's 4 input rows and 3 weights
 #pragma unroll
       for (int qi = 0; qi < G::QPW; qi += 2) {
@@ -857,7 +920,8 @@ static hipError_t irb_go(const void* x, const void* we, const float* be, const v
                          hipStream_t s) {
   using DW = typename DT::DW;
   constexpr bool VP = irb_vp(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0;
-  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP>;
+  constexpr bool PKU = irb_pku(irb_pk(std::is_same<DT, F16>::value, HID, EXPAND, S) && ABL == 0, NW, DBUF, STW, S, TH, TW);
+  using G = IrbGeom<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, (int)sizeof(DW), VP, PKU>;
   using T = typename DT::T;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
