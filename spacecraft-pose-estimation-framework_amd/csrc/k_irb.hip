@@ -53,9 +53,11 @@ constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) {
 // before the next expand is then redundant, so the barrier count is unchanged). Same operations in the same order as
 // the lane-per-channel-group PK path and dw_kernel<DW_PK16>.
 constexpr bool irb_pku(bool pk, int nw, bool dbuf, bool stw, int s, int th, int tw) {
-  return pk && nw == 4 && !dbuf && !stw && th * tw == 64;   // 128-pixel tiles: the buffer costs a workgroup per CU
+  return pk && nw == 4 && !dbuf && !stw && (th * tw == 64 || (th * tw == 128 && tw == 16 && s == 1));
 }
-constexpr int IRB_DSU = 48;   // PKU buffer row (halves): 96 B = 6 granules, 2 mod 4 -> conflict-free ds_read_b128
+// PKU buffer row (halves): 96 B = 6 granules, 2 mod 4 -> conflict-free ds_read_b128; 80 B on 128-pixel tiles, where
+// the wider rows would cost a workgroup per CU
+constexpr int irb_dsu(int pout) { return pout == 64 ? 48 : 40; }
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
           bool STW, int DWB = 4, bool VP = false, bool PKU = false>
@@ -98,7 +100,7 @@ struct IrbGeom {
   static constexpr int bytes_for(int xs, int es) {
     return VP ? (PINP * xs + WE_ELEMS + WP_ELEMS) * 2 + NBUF * 4 * RS + 2 * VSLAB * 4 + BIAS * 4
               : (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 +
-                    (PKU ? TH * TW * IRB_DSU * 2 : 2 * SLAB * DWB) + BIAS * 4;
+                    (PKU ? TH * TW * irb_dsu(TH * TW) * 2 : 2 * SLAB * DWB) + BIAS * 4;
   }
   // Xs / slab row strides: the first of (conflict-free, +16 B, unpadded Xs) that reaches the most workgroups per
   // CU. The LDS, not the VGPRs, sets the slab kernels' occupancy (3-5 waves per SIMD), and an unpadded input tile
@@ -160,9 +162,10 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   T* WPs = WEs + G::WE_ELEMS;                                               // [2][NCTP][WPS] project weights
   DW* Sl = reinterpret_cast<DW*>(WPs + G::WP_ELEMS);                        // [2][SLAB] dw weights
   uint32_t* Slv = reinterpret_cast<uint32_t*>(Sl);                          // VP: [2][VSLAB] weight pairs
-  T* Dk = reinterpret_cast<T*>(Sl);                                         // PKU: [POUT][IRB_DSU] depthwise out
+  T* Dk = reinterpret_cast<T*>(Sl);                                         // PKU: [POUT][DSU] depthwise out
+  constexpr int DSU = irb_dsu(TH * TW);
   float* Bd = reinterpret_cast<float*>(reinterpret_cast<char*>(Sl) + (VP    ? 2 * G::VSLAB * 4
-                                                                      : PKU ? G::POUT * IRB_DSU * 2
+                                                                      : PKU ? G::POUT * DSU * 2
                                                                             : 2 * G::SLAB * (int)sizeof(DW)));
   float* Be = Bd + G::NCH * 32;                                             // [HIDP] expand bias
 
@@ -613,7 +616,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
 #pragma unroll
           for (int ky = 0; ky < 3; ++ky)
             pk_fma4(a, *reinterpret_cast<const uint4*>(e0 + (ky * G::IW + kx) * G::ES), wt[ky * 3 + kx]);
-        *reinterpret_cast<uint4*>(Dk + lane * IRB_DSU + 8 * g) = relu_pk4(a);
+        *reinterpret_cast<uint4*>(Dk + lane * DSU + 8 * g) = relu_pk4(a);
       } else {   // 8x16 stride-1 tile: lane = (row pair, column), rows 2rp and 2rp + 1 share the column's 4 input rows
         const int rp = lane >> 4, ox = lane & 15;
         f16x2 a0[4] = {b2[0], b2[1], b2[2], b2[3]}, a1[4] = {b2[0], b2[1], b2[2], b2[3]};
@@ -629,13 +632,13 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
             pk_fma4(a1, v[ky + 1], wt[ky * 3 + kx]);
           }
         }
-        *reinterpret_cast<uint4*>(Dk + (2 * rp * 16 + ox) * IRB_DSU + 8 * g) = relu_pk4(a0);
-        *reinterpret_cast<uint4*>(Dk + ((2 * rp + 1) * 16 + ox) * IRB_DSU + 8 * g) = relu_pk4(a1);
+        *reinterpret_cast<uint4*>(Dk + (2 * rp * 16 + ox) * DSU + 8 * g) = relu_pk4(a0);
+        *reinterpret_cast<uint4*>(Dk + ((2 * rp + 1) * 16 + ox) * DSU + 8 * g) = relu_pk4(a1);
       }
       __syncthreads();   // every channel group of every pixel in Dk
 #pragma unroll
       for (int qi = 0; qi < G::QPW; ++qi) {
-        const x8 bf = *reinterpret_cast<const x8*>(Dk + ((wp * G::QPW + qi) * 16 + r16) * IRB_DSU + 8 * kg);
+        const x8 bf = *reinterpret_cast<const x8*>(Dk + ((wp * G::QPW + qi) * 16 + r16) * DSU + 8 * kg);
 #pragma unroll
         for (int t = 0; t < G::NCTW; ++t) acc[qi][t] = DT::mfma(pa[t], bf, acc[qi][t]);
       }
