@@ -23,25 +23,24 @@
 
 namespace spef {
 
-// Vertical-pair depthwise (VP, fp16 stride-1 blocks 3, 5, 6, 8-13): the hidden slab holds, per position (row pair pr,
+// Vertical-pair depthwise (VP, the fp16 slab-kernel variants of blocks 8-13): the hidden slab holds, per position (row pair pr,
 // column), one dword per channel = (row 2pr, row 2pr+1) -- the depthwise takes two taps of a kernel column with one
 // v_dot2_f32_f16 and the third with one v_fma_mix. The unfused dw_kernel uses the same order for these blocks
 // (irb_dw_mode), so both schedules stay bit-identical. (Stride 2 measured slower: a 3-row window straddles two
 // pairs, so every output row reads 1.5x the slab bytes, and the odd input-tile height wastes half a pair row.)
 // Blocks 8-13 (hid 384, 576) run the same pair order in the role-split kernel (k_irw.hip); their slab-kernel variants
 // follow it so every schedule of those blocks stays bit-identical.
-// Packed-fp16 depthwise (PK, fp16 stride-2 blocks 2, 4, 7): 4 v_pk_fma_f16 per tap for a lane's 8 channels (two
+// Packed-fp16 depthwise (PK, fp16 blocks 2-7): 4 v_pk_fma_f16 per tap for a lane's 8 channels (two
 // channels per op, fp16 accumulation from the fp16-rounded bias, one rounding per fused tap) instead of 8 v_fma_mix
 // -- half the depthwise VALU of the VALU-issue-bound high-resolution blocks. The ReLU'd sums are the project MFMA's B
 // fragment as they are (no convert). Error budget (tools/dw_acc_budget.py, float64 restatement at 512^2): URSONet
-// logits 5.26e-4 -> 5.76e-4 max |d| against fp32, inside the north star's 1e-3. The unfused dw_kernel<DW_PK16>
+// logits 5.26e-4 -> 5.76e-4 max |d| against fp32 with the stride-2 blocks packed, 5.25e-4 with every block packed,
+// inside the north star's 1e-3 (tests/test_dw_precision.py). The unfused dw_kernel<DW_PK16>
 // evaluates the same operations in the same order (bit-identical).
-// Blocks 2, 4, 7 (stride 2) and 5-6 (hid 192). Block 3 and the role-split blocks 8-13 (k_irw.hip) keep the vertical
-// pairs: there the plain slab's larger footprint / read pattern costs more than the VALU saved (measured +15 us on
-// block 3, +10 to +29 us per role-split kernel, against -4 to -5 us on blocks 2 and 5-6).
-constexpr bool irb_pk(bool f16, int hid, bool expand, int stride) {
-  return f16 && expand && (stride == 2 ? hid <= 192 : hid == 192);
-}
+// Blocks 2-7 (hid 96-192). The role-split blocks 8-13 (k_irw.hip, hid 384 / 576) keep the vertical pairs: there the
+// plain slab's read pattern costs more than the VALU saved (measured +10 to +29 us per role-split kernel). Block 3
+// needs the wave-uniform form below (PKU) to gain: with a lane per channel group its plain slab lost 15 us.
+constexpr bool irb_pk(bool f16, int hid, bool expand, int stride) { return f16 && expand && hid <= 192; }
 constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) {
   return f16 && expand && hid <= 576 && stride == 1 && !irb_pk(f16, hid, expand, stride);
 }
@@ -49,15 +48,16 @@ constexpr bool irb_vp(bool f16, int hid, bool expand, int stride) {
 // g owns channels 8g..8g+7 of the chunk for every output pixel of the tile (a lane per pixel, or per vertical pixel
 // pair on the 8x16 stride-1 tiles), so a tap's 8 weights are one wave-uniform 16-B scalar load used straight from
 // SGPRs by v_pk_fma_f16 -- no LDS weight slab and none of its 9 ds_read_b128 per chunk and wave. The ReLU'd sums go
-// to a 64/128-pixel LDS buffer from which each wave reads its project B fragments after one barrier (the barrier
-// before the next expand is then redundant, so the barrier count is unchanged). Same operations in the same order as
+// to an LDS buffer from which each wave reads its project B fragments after one barrier (the barrier before the next
+// expand is then redundant, so the barrier count is unchanged). Block 3's 16x16 tile (a lane per 4 rows of a column)
+// puts the buffer over the hidden slab after one more barrier: a separate 24 KB buffer would cost a workgroup per CU. Same operations in the same order as
 // the lane-per-channel-group PK path and dw_kernel<DW_PK16>.
 constexpr bool irb_pku(bool pk, int nw, bool dbuf, bool stw, int s, int th, int tw) {
-  return pk && nw == 4 && !dbuf && !stw && (th * tw == 64 || (th * tw == 128 && tw == 16 && s == 1));
+  return pk && nw == 4 && !dbuf && !stw && (th * tw == 64 || (th * tw >= 128 && tw == 16 && s == 1));
 }
 // PKU buffer row (halves): 96 B = 6 granules, 2 mod 4 -> conflict-free ds_read_b128; 80 B on 128-pixel tiles, where
-// the wider rows would cost a workgroup per CU
-constexpr int irb_dsu(int pout) { return pout == 64 ? 48 : 40; }
+// the wider rows would cost a workgroup per CU (256-pixel tiles: 24 KB over the slab)
+constexpr int irb_dsu(int pout) { return pout == 128 ? 40 : 48; }
 
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, bool DBUF,
           bool STW, int DWB = 4, bool VP = false, bool PKU = false>
@@ -100,7 +100,7 @@ struct IrbGeom {
   static constexpr int bytes_for(int xs, int es) {
     return VP ? (PINP * xs + WE_ELEMS + WP_ELEMS) * 2 + NBUF * 4 * RS + 2 * VSLAB * 4 + BIAS * 4
               : (PINP * xs + NBUF * PINP * es + WE_ELEMS + WP_ELEMS) * 2 +
-                    (PKU ? TH * TW * irb_dsu(TH * TW) * 2 : 2 * SLAB * DWB) + BIAS * 4;
+                    (PKU ? (TH * TW == 256 ? 0 : TH * TW * irb_dsu(TH * TW) * 2) : 2 * SLAB * DWB) + BIAS * 4;
   }
   // Xs / slab row strides: the first of (conflict-free, +16 B, unpadded Xs) that reaches the most workgroups per
   // CU. The LDS, not the VGPRs, sets the slab kernels' occupancy (3-5 waves per SIMD), and an unpadded input tile
@@ -162,10 +162,14 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
   T* WPs = WEs + G::WE_ELEMS;                                               // [2][NCTP][WPS] project weights
   DW* Sl = reinterpret_cast<DW*>(WPs + G::WP_ELEMS);                        // [2][SLAB] dw weights
   uint32_t* Slv = reinterpret_cast<uint32_t*>(Sl);                          // VP: [2][VSLAB] weight pairs
-  T* Dk = reinterpret_cast<T*>(Sl);                                         // PKU: [POUT][DSU] depthwise out
+  // PKU: [POUT][DSU] depthwise out; 256-pixel tiles (block 3) put it over the hidden slab once every wave has read
+  // the slab (one more barrier per chunk), since a separate buffer would cost a workgroup per CU
+  constexpr bool DALIAS = PKU && TH * TW == 256;
+  T* Dk = DALIAS ? Es0 : reinterpret_cast<T*>(Sl);
   constexpr int DSU = irb_dsu(TH * TW);
+  static_assert(!DALIAS || (G::NBUF == 1 && G::POUT * DSU <= G::PINP * G::ES), "depthwise buffer over the slab");
   float* Bd = reinterpret_cast<float*>(reinterpret_cast<char*>(Sl) + (VP    ? 2 * G::VSLAB * 4
-                                                                      : PKU ? G::POUT * DSU * 2
+                                                                      : PKU ? (DALIAS ? 0 : G::POUT * DSU * 2)
                                                                             : 2 * G::SLAB * (int)sizeof(DW)));
   float* Be = Bd + G::NCH * 32;                                             // [HIDP] expand bias
 
@@ -412,7 +416,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     }
     const T* Es;
     if constexpr (EXPAND) {
-      if constexpr (G::NBUF == 1 && !PKU) {
+      if constexpr (G::NBUF == 1 && !(PKU && !DALIAS)) {
         if (c > 0) __syncthreads();   // single hidden slab: all depthwise reads of chunk c-1 done (PKU: the barrier
       }                               // between its depthwise and project already separates them)
       T* Ew = (c & 1) ? Es1 : Es0;
@@ -617,6 +621,30 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
           for (int ky = 0; ky < 3; ++ky)
             pk_fma4(a, *reinterpret_cast<const uint4*>(e0 + (ky * G::IW + kx) * G::ES), wt[ky * 3 + kx]);
         *reinterpret_cast<uint4*>(Dk + lane * DSU + 8 * g) = relu_pk4(a);
+      } else if constexpr (G::POUT == 256) {   // 16x16 stride-1 tile: lane = (row quad, column), 4 rows per lane
+        const int rq = lane >> 4, ox = lane & 15;
+        f16x2 a[4][4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) a[j][i] = b2[i];
+        const T* e0 = Es + (4 * rq * G::IW + ox) * G::ES + 8 * g;
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) {
+          uint4 v[6];
+#pragma unroll
+          for (int r = 0; r < 6; ++r) v[r] = *reinterpret_cast<const uint4*>(e0 + (r * G::IW + kx) * G::ES);
+#pragma unroll
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) pk_fma4(a[j], v[j + ky], wt[ky * 3 + kx]);
+        }
+        uint4 o[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = relu_pk4(a[j]);
+        __syncthreads();   // every wave's slab reads done: Dk overwrites the slab
+#pragma unroll
+        for (int j = 0; j < 4; ++j) *reinterpret_cast<uint4*>(Dk + ((4 * rq + j) * 16 + ox) * DSU + 8 * g) = o[j];
       } else {   // 8x16 stride-1 tile: lane = (row pair, column), rows 2rp and 2rp + 1 share the column's 4 input rows
         const int rp = lane >> 4, ox = lane & 15;
         f16x2 a0[4] = {b2[0], b2[1], b2[2], b2[3]}, a1[4] = {b2[0], b2[1], b2[2], b2[3]};
