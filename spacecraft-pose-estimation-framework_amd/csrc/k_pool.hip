@@ -172,17 +172,18 @@ __global__ __launch_bounds__(2 * NWM * 64) void pool_gemm_kernel(const typename 
 // round trip). Every wave covers all pixels of its image for its channels: the mean needs no cross-wave reduction.
 // Workgroup = 4 waves = 128 channels of one image; the next chunk's pixels are loaded into registers during the
 // current chunk's MFMAs; full chunks skip the pixel masks; ReLU sums use packed adds. Measured (tools/ab.py, B=64,
-// 512²): 31.3 -> 25.9 us per launch. What is left: 252 VGPRs (2 waves per SIMD) make the 640 workgroups 1.25 rounds
-// of the 512 slots, and holding fewer registers (3 waves per SIMD, one round) spills 33.
-template <typename DT, int KSC>
-__global__ __launch_bounds__(256) void pool_gemm_rk_kernel(const typename DT::T* __restrict__ X,
+// 512²): 31.3 -> 25.9 us per launch with 64-pixel chunks, whose 252 VGPRs (2 waves per SIMD) made the 640
+// workgroups 1.25 rounds of the 512 slots; 32-pixel chunks (the same per-lane summation order) fit 168 VGPRs, 3 waves
+// per SIMD, all 640 workgroups in one round of 768 slots: -1.7 us (A/B).
+template <typename DT, int KSC, int PC = 32>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 3))) void pool_gemm_rk_kernel(const typename DT::T* __restrict__ X,
                                                            const typename DT::T* __restrict__ Wt,
                                                            const float* __restrict__ bias, float* __restrict__ pooled,
                                                            int HW, int N) {
   using T = typename DT::T;
   using x8 = typename DT::x8;
   constexpr int K = 32 * KSC;
-  constexpr int PC = 64;                          // pixels per chunk (4 MFMA pixel tiles)
+  constexpr int NQ = PC / 16;                     // MFMA pixel tiles per chunk
   constexpr int RS = K + 16;                      // LDS row stride: K*2 + 32 B = 2 mod 4 granules, conflict-free b128
   static_assert(((RS * 2 / 16) & 3) == 2, "row stride");
   constexpr int GPR = K / 8;                      // 16-B pieces per pixel row
@@ -242,21 +243,21 @@ __global__ __launch_bounds__(256) void pool_gemm_rk_kernel(const typename DT::T*
     }
     __syncthreads();
     if (ch + 1 < nch) gload(ch + 1);   // in flight across this chunk's MFMAs
-    f32x4 acc[2][4];
+    f32x4 acc[2][NQ];
 #pragma unroll
     for (int ks = 0; ks < KSC; ++ks) {
-      x8 bf[4];
+      x8 bf[NQ];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) bf[q] = *reinterpret_cast<const x8*>(&Bs[(q * 16 + r16) * RS + 32 * ks + 8 * kg]);
+      for (int q = 0; q < NQ; ++q) bf[q] = *reinterpret_cast<const x8*>(&Bs[(q * 16 + r16) * RS + 32 * ks + 8 * kg]);
 #pragma unroll
       for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int q = 0; q < 4; ++q)   // bias as the first MFMA's C operand
+        for (int q = 0; q < NQ; ++q)   // bias as the first MFMA's C operand
           acc[t][q] = DT::mfma(wa[t][ks], bf[q], ks == 0 ? f32x4{bb[t].x, bb[t].y, bb[t].z, bb[t].w} : acc[t][q]);
     }
     if (full) {
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
+      for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -264,7 +265,7 @@ __global__ __launch_bounds__(256) void pool_gemm_rk_kernel(const typename DT::T*
             sum[t][e] += f32x2{fmaxf(acc[t][q][2 * e], 0.f), fmaxf(acc[t][q][2 * e + 1], 0.f)};
     } else {
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
+      for (int q = 0; q < NQ; ++q) {
         const float pv = ch * PC + q * 16 + r16 < HW ? 1.f : 0.f;
 #pragma unroll
         for (int t = 0; t < 2; ++t)
