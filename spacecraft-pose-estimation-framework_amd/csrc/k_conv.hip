@@ -420,7 +420,7 @@ hipError_t launch_pw_pool(int dtype, const void* x, const void* wt, const float*
 }
 
 hipError_t launch_to_f32(int dtype, const void* x, float* y, int64_t n, hipStream_t s) {
-  if (dtype == DT_F32) return hipMemcpyAsync(y, x, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s);
+  if (dtype == DT_F32 || dtype == DT_X2) return hipMemcpyAsync(y, x, (size_t)n * sizeof(float), hipMemcpyDeviceToDevice, s);
   const unsigned g = blocks_for(n, 256);
   if (dtype == DT_F16)
     to_f32_kernel<F16><<<g, 256, 0, s>>>((const _Float16*)x, y, n);

@@ -192,8 +192,8 @@ static inline int q8_pool_shift(const spef_ctx* c, int hw) {
   return sh > 0 ? sh : 0;
 }
 
-size_t elem_size(const spef_ctx* c) {   // int8 | fp16 / bf16 | fp32 activations
-  return c->hdr.dtype == DT_I8 ? 1 : c->hdr.dtype == DT_F32 ? 4 : 2;
+size_t elem_size(const spef_ctx* c) {   // int8 | fp16 / bf16 | fp32 activations (fp32 and fp16x2 schedules)
+  return c->hdr.dtype == DT_I8 ? 1 : (c->hdr.dtype == DT_F32 || c->hdr.dtype == DT_X2) ? 4 : 2;
 }
 
 // algorithmic HBM bytes of one pointwise launch: read X, write Y (+ read residual), weights + bias once
@@ -242,7 +242,8 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
                  int stop, void** out_buf, int* oc, int* oh, int* ow, float* feat_f32 = nullptr) {
   const int dt = (int)c->hdr.dtype;
   const bool f32 = dt == DT_F32;   // fp32 schedule: one kernel per conv (k_f32.hip), no fused kernels
-  const double es = f32 ? 4.0 : 2.0;   // activation bytes per element (profiler byte counts)
+  const bool x2 = dt == DT_X2;     // fp16x2 schedule: fp32 activations, fused split-fp16 blocks (k_x2.hip)
+  const double es = (f32 || x2) ? 4.0 : 2.0;   // activation bytes per element (profiler byte counts)
   void* cur = nullptr;
   int h = H, w = W, ch = 3;
   int op_index = 0;
@@ -265,7 +266,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
     if (op.kind == OP_STEM) {
       const int OH = conv_out(h, 2), OW = conv_out(w, 2);
       const OpDesc* nx = (&op + 1 < c->ops.data() + c->ops.size()) ? &op + 1 : nullptr;
-      const bool front = !f32 && c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx && nx->kind == OP_IRB &&
+      const bool front = !f32 && !x2 && c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx && nx->kind == OP_IRB &&
                          nx->cin == 32 && nx->hidden == 32 && nx->cout == 16 && nx->expand == 1 && nx->stride == 1 &&
                          op.cout == 32 && op.x0 != kAbsent;
       if (front) {
@@ -289,7 +290,8 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const double in_b = (double)B * h * w * 3 * (layout == IN_U8_NHWC ? 1 : 4);
       HIP_TRY(prof_launch(c, s, layout == IN_U8_NHWC ? "stem_kernel<u8>" : "stem_kernel<f32>",
                           in_b + px * 32 * es, px * 2 * 27 * 32, [&] {
-        return launch_stem(dt, layout, input, ptr<float>(c, op.w0), ptr<float>(c, op.b0), y, B, h, w, OH, OW, s);
+        return launch_stem(x2 ? (int)DT_F32 : dt, layout, input, ptr<float>(c, op.w0), ptr<float>(c, op.b0), y, B, h,
+                           w, OH, OW, s);
       }));
       cur = y;
       h = OH;
@@ -301,7 +303,29 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const bool res = op.flags & 1u;
       const bool expand = op.expand != 1;
       void* x = cur;
-      if (!f32 && c->fuse && (int64_t)h * w >= c->fuse_min_hw && irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res)) {
+      if (x2) {   // fp16x2: one fused kernel per block, no unfused form
+        if (!x2_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res))
+          return fail(SPEF_ERR_ARG, "fp16x2 schedule: unsupported inverted-residual geometry");
+        void* y = pick({x});
+        const int64_t M2 = (int64_t)B * OH * OW;
+        const double flops = 2.0 * M * op.cin * op.hidden * (expand ? 1 : 0) + 18.0 * M2 * op.hidden +
+                             2.0 * M2 * op.hidden * op.cout;
+        const double hp = (op.hidden + 31) & ~31u;
+        const double bytes = (double)M * op.cin * 4 + (double)M2 * op.cout * 4 * (res ? 2 : 1) +
+                             (expand ? hp * ((op.cin + 31) & ~31u) * 4 : 0) + hp * 48 +
+                             ((op.cout + 15) & ~15u) * (hp * 4 + 4);
+        char key[96];
+        snprintf(key, sizeof(key), "x2_irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
+        HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
+          return launch_x2_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
+                               ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
+                               ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
+        }));
+        cur = y;
+        h = OH;
+        w = OW;
+        ch = (int)op.cout;
+      } else if (!f32 && c->fuse && (int64_t)h * w >= c->fuse_min_hw && irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res)) {
         void* y = pick({x});
         const int64_t M2 = (int64_t)B * OH * OW;
         const double flops = 2.0 * M * op.cin * op.hidden * (expand ? 1 : 0) + 18.0 * M2 * op.hidden +
@@ -366,7 +390,21 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         ch = (int)op.cout;
       }
     } else if (op.kind == OP_LAST) {
-      if (f32 && (mode == 0 || (mode == 2 && !feat_f32))) {   // fp32 map into a workspace buffer, then the mean
+      if (x2) {   // fp32 map (keypoint head input, feature export, or the URSONet mean's input)
+        float* y = (mode == 2 && feat_f32) ? feat_f32 : (float*)pick({cur});
+        const double M3 = (double)B * h * w;
+        HIP_TRY(prof_launch(c, s, "x2_pw_kernel<4,4>", M3 * (op.cin + op.cout) * 4 + (double)op.cout * (op.cin * 4 + 4),
+                            2.0 * M3 * op.cin * op.cout, [&] {
+          return launch_x2_pw_relu(cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), y, (int64_t)B * h * w, (int)op.cin,
+                                   (int)op.cout, s);
+        }));
+        cur = y;
+        ch = (int)op.cout;
+        if (mode == 0)
+          HIP_TRY(prof_launch(c, s, "mean_hw_kernel", M3 * op.cout * 4 + (double)B * op.cout * 4, M3 * op.cout, [&] {
+            return launch_mean_hw((const float*)cur, c->pooled, B, h * w, (int)op.cout, s);
+          }));
+      } else if (f32 && (mode == 0 || (mode == 2 && !feat_f32))) {   // fp32 map into a workspace buffer, then the mean
         void* y = pick({cur});
         const double M3 = (double)B * h * w;
         HIP_TRY(prof_launch(c, s, gemm_f32_key(op.cout), M3 * (op.cin + op.cout) * 4 + (double)op.cout * (op.cin + 1) * 4,
@@ -679,6 +717,20 @@ static void op_extents(const OpDesc& op, uint32_t dtype, uint64_t ext[9]) {
   const uint64_t rq = 20;                                 // int64 M + int64 B + int32 S per channel
   for (int i = 0; i < 9; ++i) ext[i] = 0;
   const uint64_t ci = op.cin, co = op.cout, h = op.hidden;
+  if (dtype == DT_X2) {   // fp16x2: 1x1 weights as [2][rows][Kp] fp16 planes (hi, lo); depthwise / biases padded to 32
+    switch (op.kind) {
+      case OP_STEM: ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * co * 32 * 2; break;
+      case OP_IRB:
+        if (op.expand != 1) { ext[0] = 2 * r32(h) * r32(ci) * 2; ext[1] = r32(h) * 4; }
+        ext[2] = 9 * r32(h) * 4; ext[3] = r32(h) * 4;
+        ext[4] = 2 * r16(co) * r32(h) * 2; ext[5] = r16(co) * 4;
+        break;
+      case OP_LAST: ext[0] = 2 * r16(co) * r32(ci) * 2; ext[1] = r16(co) * 4; break;
+      case OP_FC: case OP_FCKP: ext[0] = r16(co) * ci * 4; ext[1] = r16(co) * 4; break;
+      default: break;
+    }
+    return;
+  }
   switch (op.kind) {
     case OP_STEM: ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * co * 32 * a; break;
     case OP_IRB:
@@ -713,7 +765,7 @@ static int parse_blob(const uint8_t* head_bytes, size_t meta_bytes, size_t bytes
   memcpy(&h, head_bytes, sizeof(h));
   if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_BLOB, "bad blob magic");
   if (h.version != kBlobVersion) return fail(SPEF_ERR_BLOB, "unsupported blob version");
-  if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8 && h.dtype != DT_F32)
+  if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8 && h.dtype != DT_F32 && h.dtype != DT_X2)
     return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
   if (h.n_ops == 0 || h.n_ops > 4096) return fail(SPEF_ERR_BLOB, "bad op count");
   // every term bounded on its own before any sum (a crafted ops_off near 2^64 must not wrap ops_end)

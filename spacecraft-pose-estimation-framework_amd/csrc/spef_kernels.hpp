@@ -11,7 +11,7 @@ namespace spef {
 // Sets the calling thread's spef_last_error() message and returns `code` (spef_api.cpp).
 int report_error(int code, const std::string& msg);
 
-enum Dtype : int { DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3, DT_F32 = 4 };
+enum Dtype : int { DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3, DT_F32 = 4, DT_X2 = 5 /* fp32 I/O, split-fp16 MFMA (k_x2.hip) */ };
 enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RELU_F32 = 3 /* ReLU, fp32 output */ };
 enum InLayout : int { IN_U8_NHWC = 0, IN_F32_NCHW = 1 };
 
@@ -81,6 +81,16 @@ hipError_t launch_front(int dtype, const void* x, const void* wsp, const float* 
 hipError_t launch_gemm_f32(int epi, const void* x, const void* wt, const float* bias, const void* r, void* y,
                            int64_t M, int K, int N, hipStream_t s);
 const char* gemm_f32_key(int N);
+// fp16x2 schedule (k_x2.hip, blob dtype 5): fused inverted residual on fp32 NHWC activations with hi + lo fp16
+// operands (3 MFMAs per product). we: [2][r32(hid)][r32(cin)] fp16 (hi plane, lo plane), be fp32 [r32(hid)],
+// wd fp32 [9][r32(hid)], bd fp32 [r32(hid)], wp [2][r16(cout)][r32(hid)] fp16, bp fp32 [r16(cout)]; zero padded.
+bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
+hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
+                         const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
+                         int B, int H, int W, int OH, int OW, hipStream_t s);
+// 1x1 conv + BN + ReLU on fp32 activations X [M][K] with wt [2][Np][Kp] fp16 (hi, lo) -> fp32 Y [M][N]; Np % 64 == 0.
+hipError_t launch_x2_pw_relu(const void* x, const void* wt, const float* bias, float* y, int64_t M, int K, int N,
+                             hipStream_t s);
 // URSONetHead mean([2,3]) over an fp32 NHWC map: pooled [B][C].
 hipError_t launch_mean_hw(const float* x, float* pooled, int B, int HW, int C, hipStream_t s);
 

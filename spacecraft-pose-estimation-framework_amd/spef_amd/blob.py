@@ -10,6 +10,11 @@ Folding (eval-mode ``BatchNorm2d``, eps 1e-5, ``pytorch_layers.py:53-56``), done
 Pointwise weights are stored [Np][Kp] in the activation dtype (fp16 default, bf16 variant), zero padded
 (Kp = K up to a multiple of 32, Np = N up to a multiple of 16) so the MFMA kernels never mask weight loads.
 Depthwise weights are fp16 in fp16 blobs (fp32 in bf16 blobs); stem, bias and head weights stay fp32.
+
+``fp16x2`` (dtype 5, the fp32-accurate fused schedule of csrc/k_x2.hip): every 1x1 weight is stored as two fp16
+planes [2][rows][Kp], hi = fp16(w) and lo = fp16(w - hi) of the float64 folded weight (22 significant bits), expand
+rows padded to 32; depthwise weights fp32 [9][H32] and the hidden-width biases padded to H32 = hidden rounded up to
+32 (zeros), so the kernel never masks a channel.
 """
 from __future__ import annotations
 
@@ -22,7 +27,8 @@ from .arch import Arch, BN_EPS, ConvSpec, LAST_CHANNELS, arch_from_state_dict, m
 
 MAGIC = b'SPEFMI35'
 VERSION = 2   # 2: fp16 stem MFMA operand in the front_vp_kernel row-triple k order (csrc/spef_blob.hpp)
-DTYPES = {'fp16': 1, 'bf16': 2, 'fp32': 4}   # fp32: the reference's own arithmetic (k_f32.hip schedule)
+DTYPES = {'fp16': 1, 'bf16': 2, 'fp32': 4, 'fp16x2': 5}   # fp32: the reference's own arithmetic (k_f32.hip);
+# fp16x2: fp32 activations with hi + lo fp16 MFMA operands (k_x2.hip)
 DT_I8 = 3
 OP_STEM, OP_IRB, OP_LAST, OP_FC, OP_FCKP = 1, 2, 3, 4, 5
 OP_QSTEM, OP_QIRB, OP_QLAST, OP_QFC = 11, 12, 13, 14
@@ -95,6 +101,34 @@ def _pw_tensor(w: np.ndarray, b: np.ndarray, dtype: str, data: _Data):
     return data.add(_to_act(wp, dtype)), data.add(bp.tobytes())
 
 
+def split_f16(a: np.ndarray):
+    """float64 / float32 -> (hi, lo) fp16 with hi = fp16(a), lo = fp16(a - hi)."""
+    a = np.asarray(a, np.float64)
+    hi = a.astype(np.float16)
+    return hi, (a - hi.astype(np.float64)).astype(np.float16)
+
+
+def _pw_x2(w: np.ndarray, b: np.ndarray, data: _Data, rows: int):
+    """fp16x2 1x1 weights: [2][rows][Kp] fp16 (hi plane, lo plane), bias fp32 [rows]; zero padded."""
+    cout, cin = w.shape[0], w.shape[1]
+    kp = (cin + 31) // 32 * 32
+    wp = np.zeros((rows, kp), np.float64)
+    wp[:cout, :cin] = w[:, :, 0, 0]
+    hi, lo = split_f16(wp)
+    bp = np.zeros(rows, np.float32)
+    bp[:cout] = b
+    return data.add(np.concatenate([hi, lo]).tobytes()), data.add(bp.tobytes())
+
+
+def _dw_x2(w: np.ndarray, b: np.ndarray, data: _Data, hp: int):
+    c = w.shape[0]
+    w9 = np.zeros((9, hp), np.float32)
+    w9[:, :c] = w[:, 0].reshape(c, 9).T
+    bb = np.zeros(hp, np.float32)
+    bb[:c] = b
+    return data.add(w9.tobytes()), data.add(bb.tobytes())
+
+
 def _dw_tensor(w: np.ndarray, b: np.ndarray, data: _Data, dtype: str):
     """Depthwise weights [9][C] (tap = ky*3+kx): fp16 in fp16 blobs (the kernels' v_fma_mix operand), fp32 in
     bf16 blobs; bias fp32."""
@@ -130,14 +164,28 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
                 hi[:, k] = w255[ky * 9 + j]
     else:
         hi[:, :27] = w255.T
-    hi_r = _round_act(hi, dtype)
-    lo_r = _round_act(hi - hi_r, dtype)
+    if dtype == 'fp16x2':
+        sp = split_f16(hi)
+        x0 = np.concatenate(sp).tobytes()
+    else:
+        hi_r = _round_act(hi, dtype)
+        x0 = _to_act(np.concatenate([hi_r, _round_act(hi - hi_r, dtype)]), dtype)
     ops.append((OP_STEM, 3, arch.stem.cout, 0, 2, 1, 0,
                 data.add(ws.tobytes()), data.add(np.asarray(b, np.float32).tobytes()), ABSENT, ABSENT, ABSENT, ABSENT,
-                data.add(_to_act(np.concatenate([hi_r, lo_r]), dtype))))
+                data.add(x0)))
 
     for blk in arch.blocks:
         convs = list(blk.convs)
+        if dtype == 'fp16x2':
+            hp = (blk.hidden + 31) // 32 * 32
+            e = (ABSENT, ABSENT)
+            if blk.expand != 1:
+                e = _pw_x2(*fold_bn(sd, convs.pop(0)), data, hp)
+            d = _dw_x2(*fold_bn(sd, convs[0]), data, hp)
+            p = _pw_x2(*fold_bn(sd, convs[1]), data, (blk.cout + 15) // 16 * 16)
+            ops.append((OP_IRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, 1 if blk.residual else 0,
+                        e[0], e[1], d[0], d[1], p[0], p[1]))
+            continue
         e = (ABSENT, ABSENT)
         if blk.expand != 1:
             e = _pw_tensor(*fold_bn(sd, convs.pop(0)), dtype, data)
@@ -146,7 +194,10 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
         ops.append((OP_IRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, 1 if blk.residual else 0,
                     e[0], e[1], d[0], d[1], p[0], p[1]))
 
-    lw, lb = _pw_tensor(*fold_bn(sd, arch.last), dtype, data)
+    if dtype == 'fp16x2':
+        lw, lb = _pw_x2(*fold_bn(sd, arch.last), data, (arch.last.cout + 15) // 16 * 16)
+    else:
+        lw, lb = _pw_tensor(*fold_bn(sd, arch.last), dtype, data)
     ops.append((OP_LAST, arch.last.cin, arch.last.cout, 0, 1, 1, 0, lw, lb, ABSENT, ABSENT, ABSENT, ABSENT))
 
     if arch.head == 'ursonet':

@@ -80,7 +80,7 @@ def load_config(path: str | None = None) -> Config:
     if h['ORI'] == 'keypoints' or h['POS'] == 'keypoints':
         assert h['ORI'] == 'keypoints' and h['POS'] == 'keypoints', \
             "Both ORI and POS must be 'keypoints' if one is 'keypoints'"
-    assert cfg['MI355X']['DTYPE'] in ('fp16', 'bf16', 'int8', 'fp32')
+    assert cfg['MI355X']['DTYPE'] in ('fp16', 'bf16', 'int8', 'fp32', 'fp16x2')
     return _wrap(cfg)
 
 

@@ -68,7 +68,7 @@ class Engine:
         L.check(self.lib.spef_model_info(self.ctx, C.byref(head), C.byref(n0), C.byref(n1), C.byref(dt),
                                          C.byref(nops)))
         self.head, self.n_out0, self.n_out1 = head.value, n0.value, n1.value
-        self.dtype = {1: 'fp16', 2: 'bf16', 3: 'int8', 4: 'fp32'}[dt.value]
+        self.dtype = {1: 'fp16', 2: 'bf16', 3: 'int8', 4: 'fp32', 5: 'fp16x2'}[dt.value]
         self.n_ops = nops.value
         self._reserved = (0, 0, 0)
 
