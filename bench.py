@@ -46,6 +46,7 @@ INT8_BOUND = (0.05, 0.030, 0.25)   # logits, position (m), orientation (deg)
 # committed rocprofv3 FETCH_SIZE / WRITE_SIZE summaries, newest first (profiles/)
 FP16_TRAFFIC = ['r03f_pmc_traffic.json', 'r03e_pmc_traffic.json']
 INT8_TRAFFIC = ['r03_int8_pmc_traffic.json']
+X2_TRAFFIC = ['r04_x2_pmc_traffic.json']
 
 
 def pmc_traffic(kernel_key: str, path: str):
@@ -179,13 +180,14 @@ def device_batches(B, S, first, n_buf, dev):
     return [base] + [torch.roll(base, shifts=(37 * k, 53 * k), dims=(1, 2)).contiguous() for k in range(1, n_buf)]
 
 
-def time_steps(step, n_warm, n_steps, sync, barrier, probe=None, settle_s=0.0):
+def time_steps(step, n_warm, n_steps, sync, barrier, probe=None, settle_s=0.0, keep=None):
     """W warm-up steps, then exactly K timed steps bracketed by barrier + device sync on both sides. ``probe``
     (measure.ClockProbe) stamps the shader clock just outside the bracket (its kernels are synchronised before t0
     and launched after t1). ``settle_s``: before the W warm-up steps, the same steps run untimed for at least this
     long (synchronised every 8 steps), so the timed region sees the shader clock the GPU holds under this load
     rather than its ramp out of idle: measured on MI355X, 20 steps right after 5 warm-up steps ran at 2,030-2,090 MHz
-    and 80.0-82.2k img/s, 100 steps at 2,290 MHz and 92.1k img/s (same box, same build)."""
+    and 80.0-82.2k img/s, 100 steps at 2,290 MHz and 92.1k img/s (same box, same build).
+    ``keep``: called with every timed step's output (e.g. to collect each step's decode status)."""
     i = 0
     t = time.perf_counter()
     while time.perf_counter() - t < settle_s:
@@ -204,6 +206,8 @@ def time_steps(step, n_warm, n_steps, sync, barrier, probe=None, settle_s=0.0):
     out = None
     for i in range(n_steps):
         out = step(i)
+        if keep is not None:
+            keep(out)
     sync()
     barrier()
     sync()
@@ -258,14 +262,20 @@ def newest_profile(names):
 
 def run_int8(args, sd, dev, frames, ref, peaks=None):
     """C5 sub-record: the INT8 (Brevitas-mirroring) path at the same workload, same timing protocol (N=1)."""
+    from spef_amd.blob_q8 import pack_int8
+    from spef_amd.quant import calibrate
+    blob = pack_int8(sd, calibrate(sd, synth_frames(4, 128, 128, 900)))
+    return run_variant(args, blob, 'int8', dev, frames, ref, peaks)
+
+
+def run_variant(args, blob, dtype, dev, frames, ref, peaks=None):
+    """A precision variant's sub-record at the headline workload and timing protocol (N=1): int8 (C5) or fp16x2
+    (the fp32-accurate split-fp16 schedule)."""
     import torch
     from spef_amd import _lib as L
-    from spef_amd.blob_q8 import pack_int8
     from spef_amd.pipeline import StreamPipeline
-    from spef_amd.quant import calibrate
     from spef_amd.spe.spe_utils import SPEUtils
     su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
-    blob = pack_int8(sd, calibrate(sd, synth_frames(4, 128, 128, 900)))
     pipe = StreamPipeline(blob, dev, depth=max(1, args.inflight), ori_bins=su.orientation.histogram)
     B, S = args.batch, args.size
     pipe.reserve(B, S, S)
@@ -281,14 +291,58 @@ def run_int8(args, sd, dev, frames, ref, peaks=None):
         o, p = eng.forward(frames[i % len(frames)])
         eng.decode(1, 0, o, p, want_soft=True)
     prof = eng.profile_end()
-    rec = {'workload': f'C5: INT8 (Brevitas-mirroring, PTQ-calibrated scales) full net + decode, {S}x{S}, batch {B}',
+    int8 = dtype == 'int8'
+    rec = {'workload': (f'C5: INT8 (Brevitas-mirroring, PTQ-calibrated scales) full net + decode, {S}x{S}, batch {B}'
+                        if int8 else f'C3 {dtype}: full net + decode, {S}x{S}, batch {B} (fp32 activations, hi + lo '
+                                     f'fp16 MFMA operands)'),
            'value': round(B * args.steps / el, 2), 'unit': 'images/sec', 'ms_per_step': round(el / args.steps * 1e3, 4),
-           'dtype': 'int8', 'sclk_timed_region': probe.mhz(),
-           'roofline_kernel': roofline(prof, args.steps, B, newest_profile(INT8_TRAFFIC), peaks, int8=True)}
+           'dtype': dtype, 'sclk_timed_region': probe.mhz(),
+           'roofline_kernel': roofline(prof, args.steps, B, newest_profile(INT8_TRAFFIC if int8 else X2_TRAFFIC),
+                                       peaks, int8=int8),
+           'kernels': kernel_table(prof, args.steps)}
     if ref is not None:
-        rec['pose_err_vs_fp32'] = pose_error(eng, dev, *ref, tolerance=INT8_TOLERANCE)
+        rec['pose_err_vs_fp32'] = pose_error(eng, dev, *ref, tolerance=INT8_TOLERANCE if int8 else
+                                             'logits 1e-3, pose 0.1 deg / 1 mm (BASELINE.json north_star)')
     pipe.close()
     return rec
+
+
+def sharp_head(args, dev, fr):
+    """'pose err vs fp32 ref' with a sharp orientation head: the bench's backbone weights with the
+    orientation Linear at std 0.3 (logits up to ~20, peaked histograms; the reference-generated predict fixtures' scale,
+    tests/golden/cases.py) and a SPEED-range position bias, on the CPU baseline's frames, for the fp16 headline and the
+    fp16x2 parity variant, against the FP32 oracle at the north star's absolute bounds."""
+    import numpy as np
+    import torch
+    from oracle import decode_ref as D
+    from oracle import model_ref as M
+    from spef_amd import blob as Bl
+    from spef_amd.arch import mobilenet_v2
+    from spef_amd.engine import Engine
+    from spef_amd.weights import synthetic_state_dict
+    n = min(args.sharp_frames, fr.shape[0])
+    fr = fr[:n]
+    sd = synthetic_state_dict(mobilenet_v2('ursonet', 1728, 3), seed=1001, head_std=0.3, pos_std=0.01,
+                              pos_bias=(0.3, -0.2, 12.0))
+    ro, rp = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd)
+    ro, rp = ro.numpy(), rp.numpy()
+    h, _ = D.orientation_histogram(12, False)
+    rq = D.decode_orientation_batch(D.softmax_f32(ro), h)
+    out = {'frames': n, 'head': 'ori Linear std 0.3 (logit max |%.1f|), pos std 0.01 + bias (0.3, -0.2, 12.0) m'
+                                % float(np.abs(ro).max())}
+    for dt in ('fp16', 'fp16x2'):
+        e = Engine(Bl.pack(sd, dtype=dt), dev)
+        e.set_decode_tables(h, None)
+        o, p = e.forward(torch.from_numpy(fr).to(dev))
+        dec = e.decode(1, 0, o, p)
+        ang = D.angle_deg_stable(dec['ori'].cpu().numpy().astype(np.float64), rq)
+        r = {'ori_logit_max_abs': float(np.abs(o.cpu().numpy() - ro).max()),
+             'pos_max_abs_m': float(np.abs(p.cpu().numpy() - rp).max()), 'ori_max_deg': float(ang.max())}
+        r['within_tolerance'] = bool(r['ori_logit_max_abs'] < 1e-3 and r['pos_max_abs_m'] < 1e-3 and
+                                     r['ori_max_deg'] < 0.1)
+        out[dt] = r
+        e.close()
+    return out
 
 
 def run_keypoint(args, dev, with_ref: bool):
@@ -320,7 +374,7 @@ def run_keypoint(args, dev, with_ref: bool):
         raw_ref = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd, head='keypoints').numpy()
         rq, rt = E.decode_batch(D.sigmoid_f32(raw_ref), kp3d, K)
         ref = (raw_ref, rq, rt, D)
-    for dtype in ('fp32', 'fp16'):
+    for dtype in ('fp32', 'fp16x2', 'fp16'):
         eng = Engine(Bl.pack(sd, arch, dtype=dtype), dev)
         eng.set_keypoints(kp3d, K, nu, nv)
         eng.reserve(B, H, W)
@@ -333,6 +387,10 @@ def run_keypoint(args, dev, with_ref: bool):
                                     settle_s=args.settle)
         n = max(5, args.steps // 4)
         r = {'value': round(B * n / el, 2), 'unit': 'images/sec', 'ms_per_step': round(el / n * 1e3, 4), 'steps': n}
+        eng.profile_begin()
+        for _ in range(n):
+            step(0)
+        r['kernels'] = kernel_table(eng.profile_end(), n)
         if ref is not None:
             raw_ref, rq, rt, D = ref
             ang = D.angle_deg_stable(out['ori'].cpu().numpy().astype(np.float64), rq)
@@ -388,6 +446,9 @@ def main():
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-int8', action='store_true', help='skip the C5 (int8) sub-record')
     ap.add_argument('--no-keypoint', action='store_true', help='skip the keypoint-mode / EPnP sub-record')
+    ap.add_argument('--no-x2', action='store_true', help='skip the fp16x2 (fp32-accurate) sub-record')
+    ap.add_argument('--sharp-frames', type=int, default=16,
+                    help='frames of the sharp-head pose-error check (FP32 oracle on the CPU: ~0.1 s per frame)')
     ap.add_argument('--no-peaks', action='store_true', help='skip the on-box peak microbenchmark')
     ap.add_argument('--cpu-threads', type=int, default=0, help='0 = one socket\'s physical cores (capped by quota)')
     ap.add_argument('--cpu-batch', type=int, default=64)
@@ -476,18 +537,24 @@ def main():
             peaks = measure_peaks(local)                   # < 1 s, before the warm-up
         probe = ClockProbe(dev)
         barrier()
+    statuses = []
     elapsed, out = time_steps(step, args.warmup, args.steps, sync, barrier, probe,
-                              0.0 if args.dry_run else args.settle)
+                              0.0 if args.dry_run else args.settle, keep=lambda o: statuses.append(o['status']))
     elapsed = max_over_ranks(elapsed, dev)
-    assert not out['status'].any().item(), 'decode reported NaN'
+    assert len(statuses) == args.steps and not torch.stack(statuses).any().item(), 'decode reported NaN in a timed step'
 
+    leg_probe = None
     if not args.dry_run:
-        # roofline leg: per-kernel HIP events on the engine's stream, K more steps on one stream
+        # roofline leg: per-kernel HIP events on the engine's stream, K more steps on one stream, with the shader
+        # clock of the leg stamped around it (the roofline's achieved rate is priced at this clock)
+        leg_probe = ClockProbe(dev)
+        leg_probe.start()
         eng.profile_begin()
         for i in range(args.steps):
             o, p = eng.forward(frames[i % len(frames)])
             eng.decode(1, 0, o, p, want_soft=True)
         prof = eng.profile_end()
+        leg_probe.stop()
 
     if rank == 0:
         total_img = B * args.steps * world
@@ -526,6 +593,9 @@ def main():
             rec['dry_run'] = True
         else:
             rec['roofline'] = roofline(prof, args.steps, B, args.traffic, peaks, int8=args.dtype == 'int8')
+            leg_clk = leg_probe.mhz()
+            rec['roofline']['sclk_mhz'] = leg_clk['sclk_mhz'] if leg_clk else None
+            rec['roofline']['sclk_leg'] = leg_clk
             rec['kernels'] = kernel_table(prof, args.steps)
             ref = None
             if world == 1 and not args.no_cpu_baseline:
@@ -534,6 +604,11 @@ def main():
                     eng, dev, *ref, tolerance='logits 1e-3, pose 0.1 deg / 1 mm (BASELINE.json north_star)')
             if world == 1 and args.dtype != 'int8' and not args.no_int8:
                 rec['c5'] = run_int8(args, sd, dev, frames, ref, peaks)
+            if world == 1 and args.dtype != 'int8' and not args.no_x2:
+                from spef_amd import blob as Bl2
+                rec['fp16x2'] = run_variant(args, Bl2.pack(sd, dtype='fp16x2'), 'fp16x2', dev, frames, ref, peaks)
+            if world == 1 and ref is not None:
+                rec['pose_err_vs_fp32_sharp_head'] = sharp_head(args, dev, ref[0])
             if world == 1 and not args.no_keypoint:
                 rec['keypoint_mode'] = run_keypoint(args, dev, with_ref=not args.no_cpu_baseline)
         print(json.dumps(rec), flush=True)

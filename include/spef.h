@@ -177,7 +177,9 @@ int spef_profile_end(spef_ctx* ctx, char* buf, size_t cap, size_t* needed);
  * v_mfma_f32_16x16x32_f16 loop, a v_mfma_i32_16x16x64_i8 loop (random operands, 8 independent chains per wave,
  * 4 waves per SIMD), a 1 GiB HBM copy and a 1 GiB HBM read, and writes the best rates: out[0] fp16 TFLOP/s,
  * out[1] int8 TOP/s, out[2] copy GB/s (read + write bytes), out[3] read GB/s, out[4] / out[5] the shader clock in
- * MHz held inside the fp16 / int8 loop (median over workgroups of delta s_memtime / delta s_memrealtime x 100).
+ * MHz held inside the fp16 / int8 loop (median over workgroups of delta s_memtime / delta s_memrealtime x 100),
+ * out[6] / out[7] the stream configuration behind out[2] / out[3] (workgroups per CU x 100 + 16-B loads in flight
+ * per thread x 10 + 1 if nontemporal): `out` holds 8 doubles. The calling thread's current device is restored.
  * spef_clock_stamp enqueues n_wg one-wave workgroups on `stream`, each writing (location, s_memtime,
  * s_memrealtime) as three uint64 into the device buffer `out` -- location = XCD id << 8 | HW_ID[15:8] (CU, SH,
  * SE): two stamps around a timed region give the clock held during it (deltas within one CU). */

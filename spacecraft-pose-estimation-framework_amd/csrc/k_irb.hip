@@ -605,10 +605,14 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
     if constexpr (PKU) {
       const int g = __builtin_amdgcn_readfirstlane(wave);   // this wave's channel group in the depthwise phase
       const uint4* wsrc = reinterpret_cast<const uint4*>(Wd + 32 * c + 8 * g);   // wave-uniform: scalar loads
+      // channels >= HID of a partial last chunk (hid 144: chunk 4, groups 2-3) have no weights in the [9][HID] tensor:
+      // zero taps and bias instead of reading the next tap's row (wave-uniform branch)
+      const bool gv = 32 * c + 8 * g < HID;
       uint4 wt[9];
 #pragma unroll
-      for (int tap = 0; tap < 9; ++tap) wt[tap] = wsrc[tap * (HID / 8)];
-      const uint4 bh = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(Bd) + 32 * c + 8 * g);
+      for (int tap = 0; tap < 9; ++tap) wt[tap] = gv ? wsrc[tap * (HID / 8)] : make_uint4(0, 0, 0, 0);
+      const uint4 bh = gv ? *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(Bd) + 32 * c + 8 * g)
+                          : make_uint4(0, 0, 0, 0);
       const f16x2 b2[4] = {__builtin_bit_cast(f16x2, bh.x), __builtin_bit_cast(f16x2, bh.y),
                            __builtin_bit_cast(f16x2, bh.z), __builtin_bit_cast(f16x2, bh.w)};
       if constexpr (G::POUT == 64) {

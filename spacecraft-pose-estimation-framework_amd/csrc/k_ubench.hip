@@ -72,27 +72,39 @@ __global__ __launch_bounds__(256) void mfma_peak_kernel(const uint32_t* __restri
   }
 }
 
-// Streaming kernels: each thread moves 4 x 16 B per iteration (4 loads in flight), grid-stride over n (n % (4 *
-// grid * 256) == 0 for the 1 GiB buffers used here).
-__global__ __launch_bounds__(256) void hbm_copy_kernel(const uint4* __restrict__ src, uint4* __restrict__ dst, size_t n) {
-  const size_t stride = (size_t)gridDim.x * 256;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
-    const uint4 a = *(src + i), b = *(src + i + stride);
-    const uint4 c = *(src + i + 2 * stride), d = *(src + i + 3 * stride);
-    *(dst + i) = a;
-    *(dst + i + stride) = b;
-    *(dst + i + 2 * stride) = c;
-    *(dst + i + 3 * stride) = d;
+// Streaming kernels: a workgroup moves one contiguous block of 256 x U x 16 B per iteration (thread t: pieces
+// t, t + 256, ...: U loads in flight, every wave-instruction one 1 KiB contiguous run), blocks grid-strided over the
+// buffer (n % (256 U) == 0 for the 1 GiB buffers). NT: nontemporal loads / stores (the streams have no reuse).
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));   // native vector: the nontemporal builtins need one
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void hbm_copy_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst, size_t n) {
+  const size_t blk = 256 * U, nblk = n / blk;
+  for (size_t bi = blockIdx.x; bi < nblk; bi += gridDim.x) {
+    const size_t o = bi * blk + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + o + 256 * u) : src[o + 256 * u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (NT)
+        __builtin_nontemporal_store(v[u], dst + o + 256 * u);
+      else
+        dst[o + 256 * u] = v[u];
+    }
   }
 }
 
-__global__ __launch_bounds__(256) void hbm_read_kernel(const uint4* __restrict__ src, size_t n, uint32_t* __restrict__ sink) {
-  const size_t stride = (size_t)gridDim.x * 256;
+template <int U, bool NT>
+__global__ __launch_bounds__(256) void hbm_read_kernel(const u32x4* __restrict__ src, size_t n, uint32_t* __restrict__ sink) {
+  const size_t blk = 256 * U, nblk = n / blk;
   uint32_t x = 0;
-  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i + 3 * stride < n; i += 4 * stride) {
-    const uint4 a = *(src + i), b = *(src + i + stride);
-    const uint4 c = *(src + i + 2 * stride), d = *(src + i + 3 * stride);
-    x ^= a.x ^ a.y ^ a.z ^ a.w ^ b.x ^ b.y ^ b.z ^ b.w ^ c.x ^ c.y ^ c.z ^ c.w ^ d.x ^ d.y ^ d.z ^ d.w;
+  for (size_t bi = blockIdx.x; bi < nblk; bi += gridDim.x) {
+    const size_t o = bi * blk + threadIdx.x;
+    u32x4 v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) v[u] = NT ? __builtin_nontemporal_load(src + o + 256 * u) : src[o + 256 * u];
+#pragma unroll
+    for (int u = 0; u < U; ++u) x ^= v[u].x ^ v[u].y ^ v[u].z ^ v[u].w;
   }
   if (x == 0x9e3779b9u) sink[0] = x;
 }
@@ -138,10 +150,21 @@ double median(std::vector<double> v) {
 }  // namespace
 
 // out[0] fp16 MFMA TFLOP/s, out[1] int8 MFMA TOP/s, out[2] HBM copy GB/s (read + write bytes), out[3] HBM read
-// GB/s, out[4] shader clock MHz held in the fp16 loop, out[5] in the int8 loop. Best of `reps` launches each.
+// GB/s, out[4] shader clock MHz held in the fp16 loop, out[5] in the int8 loop, out[6] / out[7] the stream
+// configuration that gave out[2] / out[3] (workgroups per CU * 100 + loads in flight per thread * 10 + nontemporal).
+// Best of `reps` launches each (streams: best configuration of a small sweep).
+static int measure_peaks_on(int device, int reps, double* out);
 extern "C" int spef_measure_peaks(int device, int reps, double* out) {
   if (!out || reps < 1) return ub_fail("bad arguments");
+  int prev = -1;   // restore the calling thread's current device on every exit path (torch shares the runtime)
+  UB_TRY(hipGetDevice(&prev));
   UB_TRY(hipSetDevice(device));
+  const int rc = measure_peaks_on(device, reps, out);
+  if (prev >= 0 && prev != device) (void)hipSetDevice(prev);
+  return rc;
+}
+
+static int measure_peaks_on(int device, int reps, double* out) {
   hipDeviceProp_t prop;
   UB_TRY(hipGetDeviceProperties(&prop, device));
   const int cus = prop.multiProcessorCount;
@@ -205,20 +228,45 @@ extern "C" int spef_measure_peaks(int device, int reps, double* out) {
     out[4 + kind] = clk;
   }
   const size_t n16 = hbm_bytes / 16;
-  double best_copy = 0.0, best_read = 0.0;
-  for (int r = 0; r < reps + 1; ++r) {
-    float ms = 0.f;
-    int rc = time_launch([&] {
-      hbm_copy_kernel<<<cus * 16, 256>>>((const uint4*)sc.p[3], (uint4*)sc.p[4], n16);
-    }, &ms);
-    if (rc) return rc;
-    if (r > 0) best_copy = std::max(best_copy, 2.0 * hbm_bytes / (ms * 1e-3) / 1e9);
-    rc = time_launch([&] { hbm_read_kernel<<<cus * 16, 256>>>((const uint4*)sc.p[4], n16, (uint32_t*)sc.p[1]); }, &ms);
-    if (rc) return rc;
-    if (r > 0) best_read = std::max(best_read, (double)hbm_bytes / (ms * 1e-3) / 1e9);
+  double best_copy = 0.0, best_read = 0.0, cfg_copy = 0.0, cfg_read = 0.0;
+  for (int wpc : {4, 8, 16}) {          // workgroups (of 4 waves) per CU
+    for (int ui = 0; ui < 4; ++ui) {    // (loads in flight, nontemporal)
+      const int U = ui < 2 ? 4 : 8;
+      const bool nt = ui & 1;
+      const double cfg = wpc * 100 + U * 10 + (nt ? 1 : 0);
+      auto copy = [&] {
+        const u32x4* a = (const u32x4*)sc.p[3];
+        u32x4* d = (u32x4*)sc.p[4];
+        if (ui == 0) hbm_copy_kernel<4, false><<<cus * wpc, 256>>>(a, d, n16);
+        else if (ui == 1) hbm_copy_kernel<4, true><<<cus * wpc, 256>>>(a, d, n16);
+        else if (ui == 2) hbm_copy_kernel<8, false><<<cus * wpc, 256>>>(a, d, n16);
+        else hbm_copy_kernel<8, true><<<cus * wpc, 256>>>(a, d, n16);
+      };
+      auto read = [&] {
+        const u32x4* a = (const u32x4*)sc.p[4];
+        uint32_t* k = (uint32_t*)sc.p[1];
+        if (ui == 0) hbm_read_kernel<4, false><<<cus * wpc, 256>>>(a, n16, k);
+        else if (ui == 1) hbm_read_kernel<4, true><<<cus * wpc, 256>>>(a, n16, k);
+        else if (ui == 2) hbm_read_kernel<8, false><<<cus * wpc, 256>>>(a, n16, k);
+        else hbm_read_kernel<8, true><<<cus * wpc, 256>>>(a, n16, k);
+      };
+      for (int r = 0; r < reps + 1; ++r) {
+        float ms = 0.f;
+        int rc = time_launch(copy, &ms);
+        if (rc) return rc;
+        const double gc = 2.0 * hbm_bytes / (ms * 1e-3) / 1e9;
+        if (r > 0 && gc > best_copy) best_copy = gc, cfg_copy = cfg;
+        rc = time_launch(read, &ms);
+        if (rc) return rc;
+        const double gr = (double)hbm_bytes / (ms * 1e-3) / 1e9;
+        if (r > 0 && gr > best_read) best_read = gr, cfg_read = cfg;
+      }
+    }
   }
   out[2] = best_copy;
   out[3] = best_read;
+  out[6] = cfg_copy;
+  out[7] = cfg_read;
   return SPEF_OK;
 }
 

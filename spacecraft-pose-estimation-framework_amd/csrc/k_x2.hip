@@ -10,12 +10,15 @@
 // (v_mfma_f32_16x16x4_f32, 8 instructions of 32 cycles for the same 16x16x32 tile; cdna_hip_programming.md section 3).
 // The dropped a_lo b_lo term is below 2^-22 relative.
 //
-//   x2_irb_kernel  one InvertedResidual (pytorch_layers.py:65-98) per kernel: input tile (+halo) fp32 from HBM, split
-//                  once into hi / lo LDS tiles; per 32-channel hidden chunk the expand (3 MFMAs per K step) writes
-//                  ReLU(x We^T + be) as fp32 into an LDS slab; the depthwise 3x3 runs in fp32 (v_fma_f32 chains,
-//                  kx-outer / ky-inner) on the slab, its ReLU'd output is split into hi / lo project B fragments in
+//   x2_irb_kernel  one InvertedResidual (pytorch_layers.py:65-98) per kernel (high-resolution blocks 1-7): each wave
+//                  loads the fp32 input pixels of its expand tiles once and keeps them split (hi / lo B fragments) in
+//                  registers; per 32-channel hidden chunk the expand (3 MFMAs per K step) writes ReLU(x We^T + be) as
+//                  fp32 into an LDS slab; the depthwise 3x3 runs in fp32 (v_fma_f32 chains, kx-outer / ky-inner, weights
+//                  staged in LDS once) on the slab, its ReLU'd output is split into hi / lo project B fragments in
 //                  registers; the project accumulates over chunks in fp32 MFMA accumulators; + residual (fp32, read
-//                  back from HBM) -> fp32 block output. Block 1 (t = 1) stages its input straight into the slab.
+//                  back from L2) -> fp32 block output. Block 1 (t = 1) stages its input straight into the slab.
+//   x2_irw_kernel  the same block, role-split into expand and depthwise/project waves with LDS-staged weights (blocks
+//                  8-17, below).
 //   x2_pw_kernel   1x1 conv on fp32 activations (the last ConvBnAct 320 -> 1280, mobilenet_v2.py:264): B fragments
 //                  split on load, ReLU, fp32 output (the keypoint head's flatten input or the URSONet mean's).
 //
@@ -52,6 +55,24 @@ __device__ __forceinline__ f32x4 mfma_x2(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl,
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
 }
 
+// Hidden-chunk slab in LDS (fp32): two planes per 32-channel chunk, plane h holding channels 8k + 4h .. 8k + 4h + 3
+// (k = 0..3) of every tile pixel as one 16-B granule each. A depthwise lane (pixel r16, channels 8kg .. 8kg + 7)
+// reads granule kg of its pixel row in plane 0 and in plane 1; an expand lane writes the float4 of channels
+// 16h + 4kg .. +3 (plane kg & 1, granule 2h + kg / 2). Row strides from the ds_read_b128 lane groups of
+// MI355X_MICROARCH.md (LDS): 24 floats make the 16 consecutive rows of a 16-wide stride-1 pixel tile conflict-free
+// (2-way on 8-wide tiles), 20 floats the stride-2 rows; the plane-1 base is offset to keep the expand's mixed-plane
+// stores conflict-free.
+template <int S, int PINP>
+struct X2Slab {
+  static constexpr int SSP = S == 2 ? 20 : 24;                   // floats per pixel row of a plane
+  static constexpr int TGT = S == 2 ? 0 : 1;                     // plane-1 base, granules mod 16
+  static constexpr int PLANE = PINP * SSP + ((TGT - PINP * SSP / 4) % 16 + 16) % 16 * 4;
+  static constexpr int FLOATS = 2 * PLANE;
+  static __device__ __forceinline__ int at(int p, int c4) {      // float offset of channels 4 c4 .. 4 c4 + 3 of pixel p
+    return (c4 & 1) * PLANE + p * SSP + 4 * (c4 >> 1);
+  }
+};
+
 // Geometry. Output tile TH x TW, NW waves; the depthwise/project phase gives wave w the output pixel tiles of group
 // w % WP and the output-channel tiles of group w / WP (WCO groups; WCO > 1 repeats the depthwise to cut accumulators).
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, int NW, int WCO>
@@ -60,17 +81,16 @@ struct X2Geom {
   static constexpr int PIN = IH * IW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
   static constexpr int CINP = (CIN + 31) / 32 * 32;   // K of the expand (blob rows padded to 32, zeros)
   static constexpr int KS = CINP / 32;
-  static constexpr int XS = CINP + 16;                // hi / lo tile row (halves): 2 mod 4 granules
-  static constexpr int SS = S == 1 ? 40 : 36;         // slab row (floats)
+  using SL = X2Slab<S, PINP>;
   static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
   static constexpr int NCT = (COUT + 15) / 16;
   static constexpr int POUT16 = TH * TW / 16;
   static constexpr int WP = NW / WCO, QPW = POUT16 / WP, NCTW = NCT / WCO;
   static constexpr int EPT = (PIN16 + NW - 1) / NW;   // expand pixel tiles per wave
-  static constexpr int X_BYTES = EXPAND ? 2 * PINP * XS * 2 : 0;
-  static constexpr int LDS_BYTES = X_BYTES + PINP * SS * 4;
-  static_assert(CIN % 4 == 0 && COUT % 4 == 0 && HID % 8 == 0, "channel counts");
-  static_assert(EXPAND || (CIN == HID && CIN % 32 == 0), "t == 1 blocks stage their input as the hidden slab");
+  static constexpr int DWS = 11 * HIDP;               // staged floats: depthwise [9][HIDP], bias, expand bias
+  static constexpr int LDS_BYTES = (SL::FLOATS + DWS) * 4;
+  static_assert(CIN % 8 == 0 && COUT % 4 == 0 && HID % 8 == 0, "channel counts");
+  static_assert(EXPAND || (CIN == HID && CIN == 32), "t == 1 blocks stage their 32-channel input as the hidden slab");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && NW % WCO == 0 && NCT % WCO == 0, "tile split");
   static_assert(EPT <= 32, "validity mask is 32 bits");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
@@ -83,10 +103,10 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
     uint32_t nwg) {
   using G = X2Geom<CIN, HID, COUT, S, TH, TW, EXPAND, NW, WCO>;
+  using SL = typename G::SL;
   extern __shared__ __attribute__((aligned(16))) char smem[];
-  _Float16* Xh = reinterpret_cast<_Float16*>(smem);   // [PINP][XS] input tile, hi
-  _Float16* Xl = Xh + G::PINP * G::XS;                 // [PINP][XS] lo
-  float* Sl = reinterpret_cast<float*>(smem + G::X_BYTES);   // [PINP][SS] hidden chunk (fp32)
+  float* Sl = reinterpret_cast<float*>(smem);          // hidden chunk slab (plane layout)
+  float* Ds = Sl + SL::FLOATS;                          // [9][HIDP] depthwise weights, [HIDP] bias, [HIDP] expand bias
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
@@ -99,49 +119,75 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   const float* Xb = X + (size_t)b * H * W * CIN;
 
-  // ---- 1. input tile (+halo, zero outside the image): fp32 -> hi / lo LDS tiles (t = 1: fp32 slab). All global
-  // loads of a thread are issued before its LDS stores.
+  // ---- 1. staging: depthwise weights + biases of every chunk (LDS, once per workgroup); the input tile: B fragments
+  // of this wave's expand pixel tiles pt = wave + NW j (hi / lo, split once, in registers for every chunk), or for
+  // t = 1 the tile itself as the slab. All global loads are issued before the first LDS store.
+  f16x8 bxh[EXPAND ? G::EPT : 1][G::KS], bxl[EXPAND ? G::EPT : 1][G::KS];
+  uint32_t pvmask = 0;
   {
-    constexpr int GPR = G::CINP / 4, CG = CIN / 4;     // float4 pieces per pixel row (padded / real)
-    constexpr int NP = G::PINP * GPR;
-    constexpr int NIT = (NP + NW * 64 - 1) / (NW * 64);
+    constexpr int NDP = G::DWS / 4;                       // float4 pieces of the depthwise stage
+    constexpr int NTP = EXPAND ? 0 : G::PINP * 8;         // t = 1: float4 pieces of the 32-channel input tile
+    constexpr int NIT = (NDP + NTP + NW * 64 - 1) / (NW * 64);
     float4 v[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int u = tid + NW * 64 * i;
-      const int p = u / GPR, g = u - p * GPR;
-      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (u < NP && p < G::PIN && g < CG) {
-        const int py = p / G::IW, px = p - py * G::IW;
-        const int iy = iy0 + py, ix = ix0 + px;
-        if (iy >= 0 && iy < H && ix >= 0 && ix < W) v[i] = *reinterpret_cast<const float4*>(Xb + ((size_t)iy * W + ix) * CIN + 4 * g);
+      int u = tid + NW * 64 * i;
+      const float* src = nullptr;
+      if (u < NDP) {
+        const int part = u / (G::HIDP / 4), g = u - part * (G::HIDP / 4);
+        if (part < 10 || EXPAND) src = (part < 9 ? Wd + (size_t)part * G::HIDP : part == 9 ? bd : be) + 4 * g;   // t = 1: no be
+      } else if ((u -= NDP) < NTP) {
+        const int p = u >> 3, g = u & 7;
+        if (p < G::PIN) {
+          const int py = p / G::IW, px = p - py * G::IW;
+          const int iy = iy0 + py, ix = ix0 + px;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + ((size_t)iy * W + ix) * CIN + 4 * g;
+        }
       }
+      v[i] = src ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    if constexpr (EXPAND) {
+      float4 raw[G::EPT][G::KS][2];
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        const int p = (wave + NW * j) * 16 + r16;
+        bool ok = false;
+        int iy = 0, ix = 0;
+        if (p < G::PIN) {
+          const int py = p / G::IW, px = p - py * G::IW;
+          iy = iy0 + py;
+          ix = ix0 + px;
+          ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+        }
+        if (ok) pvmask |= 1u << j;
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const int ch = 32 * ks + 8 * kg;
+          raw[j][ks][0] = raw[j][ks][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok && ch < CIN) {
+            const float* src = Xb + ((size_t)iy * W + ix) * CIN + ch;
+            raw[j][ks][0] = *reinterpret_cast<const float4*>(src);
+            raw[j][ks][1] = *reinterpret_cast<const float4*>(src + 4);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j)
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const float4 a = raw[j][ks][0], c = raw[j][ks][1];
+          const float v8[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+          split8(v8, bxh[j][ks], bxl[j][ks]);
+        }
     }
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
-      const int u = tid + NW * 64 * i;
-      if (u >= NP) break;
-      const int p = u / GPR, g = u - p * GPR;
-      if constexpr (EXPAND) {
-        uint2 h, l;
-        split4(v[i], h, l);
-        *reinterpret_cast<uint2*>(Xh + p * G::XS + 4 * g) = h;
-        *reinterpret_cast<uint2*>(Xl + p * G::XS + 4 * g) = l;
-      } else {
-        *reinterpret_cast<float4*>(Sl + p * G::SS + 4 * g) = v[i];
+      int u = tid + NW * 64 * i;
+      if (u < NDP) {
+        *reinterpret_cast<float4*>(Ds + 4 * u) = v[i];
+      } else if ((u -= NDP) < NTP) {
+        *reinterpret_cast<float4*>(Sl + SL::at(u >> 3, u & 7)) = v[i];
       }
-    }
-  }
-  // expand validity: bit jj = pixel (wave + NW jj) * 16 + r16 of the input tile lies in the image (the depthwise's
-  // zero padding applies to the hidden tensor, whose out-of-image values must be 0, not ReLU(bias))
-  uint32_t pvmask = 0;
-#pragma unroll
-  for (int jj = 0; jj < G::EPT; ++jj) {
-    const int p = (wave + NW * jj) * 16 + r16;
-    if (p < G::PIN) {
-      const int py = p / G::IW, px = p - py * G::IW;
-      const int iy = iy0 + py, ix = ix0 + px;
-      if (iy >= 0 && iy < H && ix >= 0 && ix < W) pvmask |= 1u << jj;
     }
   }
 
@@ -153,55 +199,75 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
 #pragma unroll
     for (int q = 0; q < G::QPW; ++q) acc[q][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
   }
-  constexpr int NPC = (G::NCT * 16);                   // project weight rows per plane
+  constexpr int NPC = G::NCT * 16;                      // project weight rows per plane
   const _Float16* WpLo = Wp + (size_t)NPC * G::HIDP;
   const _Float16* WeLo = We + (size_t)G::HIDP * G::CINP;
+  // weight fragments of the chunk being computed, from L2; the next chunk's are issued right after their last use
+  f16x8 eah[EXPAND ? 2 : 1][G::KS], eal[EXPAND ? 2 : 1][G::KS], pah[G::NCTW], pal[G::NCTW];
+  auto load_ea = [&](int k) {
+    if constexpr (EXPAND) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const size_t off = (size_t)(32 * k + 16 * h + r16) * G::CINP + 32 * ks + 8 * kg;
+          eah[h][ks] = *reinterpret_cast<const f16x8*>(We + off);
+          eal[h][ks] = *reinterpret_cast<const f16x8*>(WeLo + off);
+        }
+    }
+  };
+  auto load_pa = [&](int k) {
+#pragma unroll
+    for (int t = 0; t < G::NCTW; ++t) {
+      const size_t off = (size_t)((wc * G::NCTW + t) * 16 + r16) * G::HIDP + 32 * k + 8 * kg;
+      pah[t] = *reinterpret_cast<const f16x8*>(Wp + off);
+      pal[t] = *reinterpret_cast<const f16x8*>(WpLo + off);
+    }
+  };
+  load_ea(0);
+  load_pa(0);
+  int pbase[G::QPW];
+#pragma unroll
+  for (int q = 0; q < G::QPW; ++q) {
+    const int o = (wp * G::QPW + q) * 16 + r16;
+    const int oy = o / TW, ox = o - (o / TW) * TW;
+    pbase[q] = oy * S * G::IW + ox * S;
+  }
 
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
-    __syncthreads();   // c == 0: the staged tile; c > 0: every wave is done reading the slab of chunk c - 1
+    __syncthreads();   // c == 0: the staged depthwise weights / t = 1 tile; c > 0: the slab of chunk c - 1 is consumed
     if constexpr (EXPAND) {
       // ---- expand chunk c: hidden channels 32c + 16h + 4kg + r of input-tile pixel 16 pt + r16 -> slab
       f32x4 e[G::EPT][2];
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const float4 eb = *reinterpret_cast<const float4*>(be + 32 * c + 16 * h + 4 * kg);
+        const float4 eb = *reinterpret_cast<const float4*>(Ds + 10 * G::HIDP + 32 * c + 16 * h + 4 * kg);
 #pragma unroll
-        for (int jj = 0; jj < G::EPT; ++jj) e[jj][h] = f32x4{eb.x, eb.y, eb.z, eb.w};
+        for (int j = 0; j < G::EPT; ++j) e[j][h] = f32x4{eb.x, eb.y, eb.z, eb.w};
       }
 #pragma unroll
-      for (int ks = 0; ks < G::KS; ++ks) {
-        f16x8 ah[2], al[2];
+      for (int ks = 0; ks < G::KS; ++ks)
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          const size_t off = (size_t)(32 * c + 16 * h + r16) * G::CINP + 32 * ks + 8 * kg;
-          ah[h] = *reinterpret_cast<const f16x8*>(We + off);
-          al[h] = *reinterpret_cast<const f16x8*>(WeLo + off);
+        for (int j = 0; j < G::EPT; ++j) {
+          if (wave + NW * j >= G::PIN16) break;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) e[j][h] = mfma_x2(eah[h][ks], eal[h][ks], bxh[j][ks], bxl[j][ks], e[j][h]);
         }
+      if (c + 1 < G::NCH) load_ea(c + 1);
 #pragma unroll
-        for (int jj = 0; jj < G::EPT; ++jj) {
-          const int pt = wave + NW * jj;
-          if (pt >= G::PIN16) break;
-          const int ro = (pt * 16 + r16) * G::XS + 32 * ks + 8 * kg;
-          const f16x8 bh = *reinterpret_cast<const f16x8*>(Xh + ro);
-          const f16x8 bl = *reinterpret_cast<const f16x8*>(Xl + ro);
-#pragma unroll
-          for (int h = 0; h < 2; ++h) e[jj][h] = mfma_x2(ah[h], al[h], bh, bl, e[jj][h]);
-        }
-      }
-#pragma unroll
-      for (int jj = 0; jj < G::EPT; ++jj) {
-        const int pt = wave + NW * jj;
+      for (int j = 0; j < G::EPT; ++j) {
+        const int pt = wave + NW * j;
         if (pt >= G::PIN16) break;
-        const bool ok = (pvmask >> jj) & 1u;
+        const bool ok = (pvmask >> j) & 1u;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           float4 o;
-          o.x = ok ? fmaxf(e[jj][h][0], 0.f) : 0.f;
-          o.y = ok ? fmaxf(e[jj][h][1], 0.f) : 0.f;
-          o.z = ok ? fmaxf(e[jj][h][2], 0.f) : 0.f;
-          o.w = ok ? fmaxf(e[jj][h][3], 0.f) : 0.f;
-          *reinterpret_cast<float4*>(Sl + (pt * 16 + r16) * G::SS + 16 * h + 4 * kg) = o;
+          o.x = ok ? fmaxf(e[j][h][0], 0.f) : 0.f;
+          o.y = ok ? fmaxf(e[j][h][1], 0.f) : 0.f;
+          o.z = ok ? fmaxf(e[j][h][2], 0.f) : 0.f;
+          o.w = ok ? fmaxf(e[j][h][3], 0.f) : 0.f;
+          *reinterpret_cast<float4*>(Sl + SL::at(pt * 16 + r16, 4 * h + kg)) = o;
         }
       }
       __syncthreads();   // slab of chunk c complete
@@ -211,32 +277,26 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
     // channels 32c + 8kg .. +7 -> hi / lo B fragments -> project accumulation
     float a[G::QPW][8];
     {
-      const float4 d0 = *reinterpret_cast<const float4*>(bd + 32 * c + 8 * kg);
-      const float4 d1 = *reinterpret_cast<const float4*>(bd + 32 * c + 8 * kg + 4);
+      const float4 d0 = *reinterpret_cast<const float4*>(Ds + 9 * G::HIDP + 32 * c + 8 * kg);
+      const float4 d1 = *reinterpret_cast<const float4*>(Ds + 9 * G::HIDP + 32 * c + 8 * kg + 4);
 #pragma unroll
       for (int q = 0; q < G::QPW; ++q) {
         a[q][0] = d0.x; a[q][1] = d0.y; a[q][2] = d0.z; a[q][3] = d0.w;
         a[q][4] = d1.x; a[q][5] = d1.y; a[q][6] = d1.z; a[q][7] = d1.w;
       }
     }
-    int pbase[G::QPW];
-#pragma unroll
-    for (int q = 0; q < G::QPW; ++q) {
-      const int o = (wp * G::QPW + q) * 16 + r16;
-      const int oy = o / TW, ox = o - (o / TW) * TW;
-      pbase[q] = (oy * S * G::IW + ox * S) * G::SS + 8 * kg;
-    }
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
       for (int ky = 0; ky < 3; ++ky) {
-        const float* wt = Wd + (size_t)(ky * 3 + kx) * G::HIDP + 32 * c + 8 * kg;
+        const float* wt = Ds + (ky * 3 + kx) * G::HIDP + 32 * c + 8 * kg;
         const float4 w0 = *reinterpret_cast<const float4*>(wt), w1 = *reinterpret_cast<const float4*>(wt + 4);
         const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
 #pragma unroll
         for (int q = 0; q < G::QPW; ++q) {
-          const float* sp = Sl + pbase[q] + (ky * G::IW + kx) * G::SS;
-          const float4 x0 = *reinterpret_cast<const float4*>(sp), x1 = *reinterpret_cast<const float4*>(sp + 4);
+          const int p = pbase[q] + ky * G::IW + kx;
+          const float4 x0 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
+          const float4 x1 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
           const float x8[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
 #pragma unroll
           for (int e = 0; e < 8; ++e) a[q][e] = fmaf(x8[e], w8[e], a[q][e]);
@@ -250,13 +310,10 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
       split8(a[q], bh[q], bl[q]);
     }
 #pragma unroll
-    for (int t = 0; t < G::NCTW; ++t) {
-      const size_t off = (size_t)((wc * G::NCTW + t) * 16 + r16) * G::HIDP + 32 * c + 8 * kg;
-      const f16x8 ph = *reinterpret_cast<const f16x8*>(Wp + off);
-      const f16x8 pl = *reinterpret_cast<const f16x8*>(WpLo + off);
+    for (int t = 0; t < G::NCTW; ++t)
 #pragma unroll
-      for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(ph, pl, bh[q], bl[q], acc[q][t]);
-    }
+      for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(pah[t], pal[t], bh[q], bl[q], acc[q][t]);
+    if (c + 1 < G::NCH) load_pa(c + 1);
   }
 
   // ---- epilogue: + residual (fp32 block input, pytorch_layers.py:93-96, added after the BN bias) -> fp32 NHWC
@@ -281,46 +338,414 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
   }
 }
 
-// (cin, hidden, cout, stride, expand, residual, TH, TW, waves, cout groups): MobileNet-V2's 17 blocks
-// (mobilenet_v2.py:240-249). Tiles keep the LDS (hi / lo input tile + fp32 slab) at 2+ workgroups per CU where the
-// geometry allows.
-#define SPEF_X2_TABLE(X)                                   \
-  X(32, 32, 16, 1, false, false, 16, 16, 4, 1)   /* 1 */   \
-  X(16, 96, 24, 2, true, false, 8, 8, 4, 1)      /* 2 */   \
-  X(24, 144, 24, 1, true, true, 8, 16, 4, 1)     /* 3 */   \
-  X(24, 144, 32, 2, true, false, 8, 8, 4, 1)     /* 4 */   \
-  X(32, 192, 32, 1, true, true, 8, 16, 4, 1)     /* 5-6 */ \
-  X(32, 192, 64, 2, true, false, 8, 8, 4, 1)     /* 7 */   \
-  X(64, 384, 64, 1, true, true, 8, 8, 4, 1)      /* 8-10 */ \
-  X(64, 384, 96, 1, true, false, 8, 8, 4, 2)     /* 11 */  \
-  X(96, 576, 96, 1, true, true, 8, 8, 4, 2)      /* 12-13 */ \
-  X(96, 576, 160, 2, true, false, 4, 8, 2, 2)    /* 14 */  \
-  X(160, 960, 160, 1, true, true, 8, 8, 4, 2)    /* 15-16 */ \
-  X(160, 960, 320, 1, true, false, 8, 8, 4, 4)   /* 17 */
+// ------------------------------------------------------------------------------------------ role-split form
+// The low-resolution blocks (8-17: 32x32 and 16x16 maps at 512^2, 256-1024 tiles for 256 CUs, 12-30 hidden chunks)
+// are bound by how fast a workgroup streams the chunk weights, not by arithmetic: every chunk needs its expand and
+// project weights (hi + lo, 20 KB each for 160 -> 960 -> 160) from L2 at ~29 B/clk per CU, and a lone workgroup per
+// CU exposes every round trip. Here 8 waves take fixed roles in a two-stage pipeline with ONE barrier per chunk:
+//
+//   expand waves [0, 4): stage the weights of chunks c+1 / c+2 (global -> registers -> LDS, once per workgroup) and
+//                        expand chunk c+1 into slab (c+1) & 1; their input-tile B fragments (hi + lo) are loaded and
+//                        split once and stay in registers for every chunk (no input tile in LDS)
+//   depthwise waves [4, 8): depthwise of chunk c from slab c & 1 + project accumulation (weights from the LDS stage)
+//
+// Stage buffers (double-buffered, written one iteration before use): expand weights + expand bias of chunk k in
+// iteration k - 2, depthwise weights + bias and project weights of chunk k in iteration k - 1. Same arithmetic and
+// rounding as x2_irb_kernel (bit-identical results).
+template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST>
+struct X2wGeom {
+  static constexpr int NE = 4, ND = 4, NW = NE + ND;
+  static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
+  static constexpr int PIN = IH * IW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
+  static constexpr int CINP = (CIN + 31) / 32 * 32, KS = CINP / 32;
+  static constexpr int WES = CINP + 16;                 // staged expand row (halves): 2 mod 4 granules
+  static constexpr int WPS = 48;                        // staged project row (halves, 32 used)
+  using SL = X2Slab<S, PINP>;
+  static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
+  static constexpr int NCT = (COUT + 15) / 16, NPC = NCT * 16;
+  static constexpr int POUT16 = TH * TW / 16;
+  static constexpr int WP = ND / WCO, QPW = POUT16 / WP, NCTW = NCT / WCO;
+  static constexpr int EPT = (PIN16 + NE - 1) / NE;     // expand pixel tiles per expand wave
+  // LDS: slabs | expand stage [2] | depthwise stage [2] | project stage [2]
+  static constexpr int SLAB_B = SL::FLOATS * 4;
+  static constexpr int SE_B = 2 * 32 * WES * 2 + 32 * 4;   // hi / lo weight planes + expand bias
+  static constexpr int SD_B = (9 * 32 + 32) * 4;            // depthwise weights [9][32] + depthwise bias
+  static constexpr int SP_B = PST ? 2 * NPC * WPS * 2 : 0;
+  static constexpr int OFF_SE = 2 * SLAB_B, OFF_SD = OFF_SE + 2 * SE_B, OFF_SP = OFF_SD + 2 * SD_B;
+  static constexpr int LDS_BYTES = OFF_SP + 2 * SP_B;
+  // 16-B stage pieces per chunk
+  static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = 9 * 8 + 8, NPP = PST ? 2 * NPC * 4 : 0;
+  static constexpr int NPIECE = (NPE + NPD + NPP + NE * 64 - 1) / (NE * 64);
+  static_assert(CIN % 8 == 0 && COUT % 4 == 0 && HID % 8 == 0, "channel counts");
+  static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
+  static_assert(EPT <= 32 && NCH >= 2, "validity mask / pipeline depth");
+  static_assert(SE_B % 16 == 0 && SD_B % 16 == 0 && SP_B % 16 == 0 && SLAB_B % 16 == 0, "16-B aligned stages");
+  static_assert(LDS_BYTES <= 163840, "LDS budget");
+};
 
-template <int CIN, int HID, int COUT, int S, bool EXPAND, bool RES, int TH, int TW, int NW, int WCO>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST>
+__global__ __launch_bounds__(512) void x2_irw_kernel(
+    const float* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
+    const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
+    const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
+    uint32_t nwg) {
+  using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST>;
+  using SL = typename G::SL;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int tx = (int)(L % (uint32_t)tiles_x);
+  L /= (uint32_t)tiles_x;
+  const int ty = (int)(L % (uint32_t)tiles_y);
+  const int b = (int)(L / (uint32_t)tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  auto slab = [&](int i) { return reinterpret_cast<float*>(smem + i * G::SLAB_B); };
+  auto se = [&](int i) { return smem + G::OFF_SE + i * G::SE_B; };
+  auto sd = [&](int i) { return reinterpret_cast<float*>(smem + G::OFF_SD + i * G::SD_B); };
+  auto sp = [&](int i) { return reinterpret_cast<_Float16*>(smem + G::OFF_SP + i * G::SP_B); };
+
+  // 16-B stage piece u of chunk k: kind 0 = expand (weights + bias, chunk ke), 1 = depthwise (chunk kd),
+  // 2 = project (chunk kd). Source / destination pointers; null source = nothing to stage (chunk out of range).
+  auto piece = [&](int u, int ke, int kd, const void*& src, void*& dst) {
+    src = nullptr;
+    dst = nullptr;
+    if (u < G::NPE) {
+      if (ke >= G::NCH) return;
+      if (u < G::NPE - 8) {
+        constexpr int PPR = G::CINP / 8;
+        const int pl = u / (32 * PPR), rr = (u / PPR) % 32, g = u % PPR;
+        src = We + (size_t)pl * G::HIDP * G::CINP + (size_t)(32 * ke + rr) * G::CINP + 8 * g;
+        dst = se(ke & 1) + ((pl * 32 + rr) * G::WES + 8 * g) * 2;
+      } else {
+        const int g = u - (G::NPE - 8);
+        src = be + 32 * ke + 4 * g;
+        dst = se(ke & 1) + 2 * 32 * G::WES * 2 + 16 * g;
+      }
+      return;
+    }
+    u -= G::NPE;
+    if (u < G::NPD) {
+      if (kd >= G::NCH) return;
+      if (u < 72) {
+        const int tap = u >> 3, g = u & 7;
+        src = Wd + (size_t)tap * G::HIDP + 32 * kd + 4 * g;
+        dst = sd(kd & 1) + tap * 32 + 4 * g;
+      } else {
+        src = bd + 32 * kd + 4 * (u - 72);
+        dst = sd(kd & 1) + 288 + 4 * (u - 72);
+      }
+      return;
+    }
+    u -= G::NPD;
+    if (PST && u < G::NPP) {
+      if (kd >= G::NCH) return;
+      const int pl = u / (G::NPC * 4), rr = (u >> 2) % G::NPC, q = u & 3;
+      src = Wp + (size_t)pl * G::NPC * G::HIDP + (size_t)rr * G::HIDP + 32 * kd + 8 * q;
+      dst = sp(kd & 1) + (pl * G::NPC + rr) * G::WPS + 8 * q;
+    }
+  };
+
+  // ---- prologue (all waves): expand stages of chunks 0 and 1, depthwise / project stage of chunk 0
+  {
+    constexpr int NP0 = 2 * G::NPE + G::NPD + G::NPP;
+    constexpr int NIT = (NP0 + G::NW * 64 - 1) / (G::NW * 64);
+    uint4 v[NIT];
+    void* dst[NIT];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      int u = tid + G::NW * 64 * i;
+      const void* src = nullptr;
+      dst[i] = nullptr;
+      if (u < G::NPE) piece(u, 1, G::NCH, src, dst[i]);                     // expand chunk 1
+      else if (u < NP0) piece(u - G::NPE, 0, 0, src, dst[i]);               // expand / dw / project chunk 0
+      v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i)
+      if (dst[i]) *reinterpret_cast<uint4*>(dst[i]) = v[i];
+  }
+
+  if (wave < G::NE) {
+    // ================= expand waves
+    const int e = wave;
+    // this wave's input-tile pixel tiles pt = e + NE j: B fragments (hi / lo) for every K step, loaded and split once
+    f16x8 bxh[G::EPT][G::KS], bxl[G::EPT][G::KS];
+    uint32_t pvmask = 0;
+    {
+      const float* Xb = X + (size_t)b * H * W * CIN;
+      float4 raw[G::EPT][G::KS][2];
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        const int p = (e + G::NE * j) * 16 + r16;
+        bool ok = false;
+        int iy = 0, ix = 0;
+        if (p < G::PIN) {
+          const int py = p / G::IW, px = p - py * G::IW;
+          iy = iy0 + py;
+          ix = ix0 + px;
+          ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
+        }
+        if (ok) pvmask |= 1u << j;
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const int ch = 32 * ks + 8 * kg;
+          raw[j][ks][0] = raw[j][ks][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+          if (ok && ch < CIN) {
+            const float* src = Xb + ((size_t)iy * W + ix) * CIN + ch;
+            raw[j][ks][0] = *reinterpret_cast<const float4*>(src);
+            raw[j][ks][1] = *reinterpret_cast<const float4*>(src + 4);
+          }
+        }
+      }
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j)
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const float4 a = raw[j][ks][0], c = raw[j][ks][1];
+          const float v8[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+          split8(v8, bxh[j][ks], bxl[j][ks]);
+        }
+    }
+    // expand of chunk k into slab k & 1 (stage k & 1)
+    auto expand = [&](int k) {
+      const char* S0 = se(k & 1);
+      const float* eb = reinterpret_cast<const float*>(S0 + 2 * 32 * G::WES * 2);
+      f32x4 acc[G::EPT][2];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 bb = *reinterpret_cast<const float4*>(eb + 16 * h + 4 * kg);
+#pragma unroll
+        for (int j = 0; j < G::EPT; ++j) acc[j][h] = f32x4{bb.x, bb.y, bb.z, bb.w};
+      }
+      const _Float16* Ws = reinterpret_cast<const _Float16*>(S0);
+#pragma unroll
+      for (int ks = 0; ks < G::KS; ++ks) {
+        f16x8 ah[2], al[2];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          ah[h] = *reinterpret_cast<const f16x8*>(Ws + (16 * h + r16) * G::WES + 32 * ks + 8 * kg);
+          al[h] = *reinterpret_cast<const f16x8*>(Ws + (32 + 16 * h + r16) * G::WES + 32 * ks + 8 * kg);
+        }
+#pragma unroll
+        for (int j = 0; j < G::EPT; ++j) {
+          if (e + G::NE * j >= G::PIN16) break;
+#pragma unroll
+          for (int h = 0; h < 2; ++h) acc[j][h] = mfma_x2(ah[h], al[h], bxh[j][ks], bxl[j][ks], acc[j][h]);
+        }
+      }
+      float* Sl = slab(k & 1);
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        const int pt = e + G::NE * j;
+        if (pt >= G::PIN16) break;
+        const bool ok = (pvmask >> j) & 1u;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          float4 o;
+          o.x = ok ? fmaxf(acc[j][h][0], 0.f) : 0.f;
+          o.y = ok ? fmaxf(acc[j][h][1], 0.f) : 0.f;
+          o.z = ok ? fmaxf(acc[j][h][2], 0.f) : 0.f;
+          o.w = ok ? fmaxf(acc[j][h][3], 0.f) : 0.f;
+          *reinterpret_cast<float4*>(Sl + SL::at(pt * 16 + r16, 4 * h + kg)) = o;
+        }
+      }
+    };
+    __syncthreads();                 // prologue stages visible
+    expand(0);
+    __syncthreads();                 // slab 0 visible
+#pragma unroll 1
+    for (int c = 0; c < G::NCH; ++c) {
+      // stage expand chunk c + 2 and depthwise / project chunk c + 1 (loads issued before the expand)
+      uint4 v[G::NPIECE];
+      void* dst[G::NPIECE];
+#pragma unroll
+      for (int i = 0; i < G::NPIECE; ++i) {
+        const void* src;
+        piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst[i]);
+        v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        if (!src) dst[i] = nullptr;
+      }
+      if (c + 1 < G::NCH) expand(c + 1);
+#pragma unroll
+      for (int i = 0; i < G::NPIECE; ++i)
+        if (dst[i]) *reinterpret_cast<uint4*>(dst[i]) = v[i];
+      __syncthreads();
+    }
+  } else {
+    // ================= depthwise / project waves
+    const int d = wave - G::NE;
+    const int wp = d % G::WP, wc = d / G::WP;
+    f32x4 acc[G::QPW][G::NCTW];
+#pragma unroll
+    for (int t = 0; t < G::NCTW; ++t) {
+      const float4 bb = *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg);
+#pragma unroll
+      for (int q = 0; q < G::QPW; ++q) acc[q][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
+    }
+    int pbase[G::QPW];
+#pragma unroll
+    for (int q = 0; q < G::QPW; ++q) {
+      const int o = (wp * G::QPW + q) * 16 + r16;
+      const int oy = o / TW, ox = o - (o / TW) * TW;
+      pbase[q] = oy * S * G::IW + ox * S;
+    }
+    const _Float16* WpLo = Wp + (size_t)G::NPC * G::HIDP;
+    f16x8 pgh[PST ? 1 : G::NCTW], pgl[PST ? 1 : G::NCTW];   // !PST: this chunk's project fragments from L2
+    auto load_pg = [&](int k) {
+      if constexpr (!PST) {
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) {
+          const size_t off = (size_t)((wc * G::NCTW + t) * 16 + r16) * G::HIDP + 32 * k + 8 * kg;
+          pgh[t] = *reinterpret_cast<const f16x8*>(Wp + off);
+          pgl[t] = *reinterpret_cast<const f16x8*>(WpLo + off);
+        }
+      }
+    };
+    load_pg(0);
+    __syncthreads();
+    __syncthreads();
+#pragma unroll 1
+    for (int c = 0; c < G::NCH; ++c) {
+      const float* Sl = slab(c & 1);
+      const float* D = sd(c & 1);
+      float a[G::QPW][8];
+      {
+        const float4 d0 = *reinterpret_cast<const float4*>(D + 288 + 8 * kg);
+        const float4 d1 = *reinterpret_cast<const float4*>(D + 288 + 8 * kg + 4);
+#pragma unroll
+        for (int q = 0; q < G::QPW; ++q) {
+          a[q][0] = d0.x; a[q][1] = d0.y; a[q][2] = d0.z; a[q][3] = d0.w;
+          a[q][4] = d1.x; a[q][5] = d1.y; a[q][6] = d1.z; a[q][7] = d1.w;
+        }
+      }
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const float* wt = D + (ky * 3 + kx) * 32 + 8 * kg;
+          const float4 w0 = *reinterpret_cast<const float4*>(wt), w1 = *reinterpret_cast<const float4*>(wt + 4);
+          const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+          for (int q = 0; q < G::QPW; ++q) {
+            const int p = pbase[q] + ky * G::IW + kx;
+            const float4 x0 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
+            const float4 x1 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
+            const float x8[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+            for (int e = 0; e < 8; ++e) a[q][e] = fmaf(x8[e], w8[e], a[q][e]);
+          }
+        }
+      f16x8 bh[G::QPW], bl[G::QPW];
+#pragma unroll
+      for (int q = 0; q < G::QPW; ++q) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[q][e] = fmaxf(a[q][e], 0.f);
+        split8(a[q], bh[q], bl[q]);
+      }
+      if constexpr (PST) {
+        const _Float16* P = sp(c & 1);
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) {
+          const int row = (wc * G::NCTW + t) * 16 + r16;
+          const f16x8 ph = *reinterpret_cast<const f16x8*>(P + row * G::WPS + 8 * kg);
+          const f16x8 pl = *reinterpret_cast<const f16x8*>(P + (G::NPC + row) * G::WPS + 8 * kg);
+#pragma unroll
+          for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(ph, pl, bh[q], bl[q], acc[q][t]);
+        }
+      } else {
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t)
+#pragma unroll
+          for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(pgh[t], pgl[t], bh[q], bl[q], acc[q][t]);
+        if (c + 1 < G::NCH) load_pg(c + 1);   // next chunk's fragments: in flight across the barrier and its depthwise
+      }
+      __syncthreads();
+    }
+    // epilogue: + residual (fp32 block input) -> fp32 NHWC
+#pragma unroll
+    for (int q = 0; q < G::QPW; ++q) {
+      const int o = (wp * G::QPW + q) * 16 + r16;
+      const int oy = o / TW, ox = o - (o / TW) * TW;
+      const int gy = oy0 + oy, gx = ox0 + ox;
+      if (gy >= OH || gx >= OW) continue;
+      const size_t pix = ((size_t)b * OH + gy) * OW + gx;
+#pragma unroll
+      for (int t = 0; t < G::NCTW; ++t) {
+        const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
+        if (co >= COUT) continue;
+        f32x4 v = acc[q][t];
+        if constexpr (RES) {
+          const float4 r = *reinterpret_cast<const float4*>(X + pix * CIN + co);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        }
+        *reinterpret_cast<float4*>(Y + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
+      }
+    }
+  }
+}
+
+// (cin, hidden, cout, stride, expand, residual, TH, TW, waves, cout groups, kind): MobileNet-V2's 17 blocks
+// (mobilenet_v2.py:240-249). kind 0: slab kernel with `waves` waves (tiles keep the hi / lo input tile + fp32 slab at
+// 2+ workgroups per CU where the geometry allows); kind 1: role-split kernel (4 + 4 waves) with the project weights
+// staged in LDS; kind 2: role-split, project weights from L2 (block 17: no two depthwise waves share a channel tile).
+#define SPEF_X2_TABLE(X)                                         \
+  X(32, 32, 16, 1, false, false, 8, 16, 4, 1, 0)    /* 1 */      \
+  X(16, 96, 24, 2, true, false, 8, 8, 4, 1, 0)      /* 2 */      \
+  X(24, 144, 24, 1, true, true, 8, 16, 4, 1, 0)     /* 3 */      \
+  X(24, 144, 32, 2, true, false, 8, 8, 4, 1, 0)     /* 4 */      \
+  X(32, 192, 32, 1, true, true, 8, 16, 4, 1, 0)     /* 5-6 */    \
+  X(32, 192, 64, 2, true, false, 8, 8, 4, 1, 0)     /* 7 */      \
+  X(64, 384, 64, 1, true, true, 8, 16, 8, 2, 1)     /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 16, 8, 2, 1)    /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 8, 8, 2, 1)      /* 12-13 */  \
+  X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
+  X(160, 960, 160, 1, true, true, 8, 8, 8, 2, 1)    /* 15-16 */  \
+  X(160, 960, 320, 1, true, false, 8, 8, 8, 4, 2)   /* 17 */
+
+template <typename K>
+static hipError_t x2_set_lds(K k, int lds) {   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
+  if (lds <= 65536) return hipSuccess;
+  return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
+}
+
+template <int CIN, int HID, int COUT, int S, bool EXPAND, bool RES, int TH, int TW, int NW, int WCO, int KIND>
 static hipError_t x2_irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
                             const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                             hipStream_t s) {
-  using G = X2Geom<CIN, HID, COUT, S, TH, TW, EXPAND, NW, WCO>;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  auto k = x2_irb_kernel<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
-  static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
-  if (!attr_set && G::LDS_BYTES > 65536) {
-    hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
-    if (e != hipSuccess) return e;
-    attr_set = true;
+  static bool attr_set = false;
+  if constexpr (KIND == 0) {
+    using G = X2Geom<CIN, HID, COUT, S, TH, TW, EXPAND, NW, WCO>;
+    auto k = x2_irb_kernel<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
+    if (!attr_set) {
+      hipError_t e = x2_set_lds(k, G::LDS_BYTES);
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+    k<<<nwg, NW * 64, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
+                                        (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
+  } else {
+    static_assert(EXPAND && NW == 8, "role-split blocks expand, 4 + 4 waves");
+    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND == 1>;
+    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND == 1>;
+    if (!attr_set) {
+      hipError_t e = x2_set_lds(k, G::LDS_BYTES);
+      if (e != hipSuccess) return e;
+      attr_set = true;
+    }
+    k<<<nwg, 512, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
+                                    (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   }
-  k<<<nwg, NW * 64, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
-                                      (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   return hipGetLastError();
 }
 
 bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res) {
-#define SPEF_X2_HAS(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_) \
+#define SPEF_X2_HAS(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_) \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS) return true;
   SPEF_X2_TABLE(SPEF_X2_HAS)
 #undef SPEF_X2_HAS
@@ -330,9 +755,11 @@ bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool 
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
                          int B, int H, int W, int OH, int OW, hipStream_t s) {
-#define SPEF_X2_CASE(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_)                                          \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                  \
-    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s);
+  if (!x || !y || !wd || !bd || !wp || !bp || (expand && (!we || !be))) return hipErrorInvalidValue;
+#define SPEF_X2_CASE(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                         \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                      \
+    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, \
+                                                                     s);
   SPEF_X2_TABLE(SPEF_X2_CASE)
 #undef SPEF_X2_CASE
   return hipErrorNotSupported;

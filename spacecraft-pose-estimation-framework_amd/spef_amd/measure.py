@@ -14,13 +14,20 @@ from . import _lib as L
 
 
 def measure_peaks(device: int = 0, reps: int = 2) -> dict:
-    out = (C.c_double * 6)()
+    out = (C.c_double * 8)()
     L.check(L.load().spef_measure_peaks(int(device), int(reps), out))
+
+    def cfg(v):
+        v = int(v)
+        return {'workgroups_per_cu': v // 100, 'loads_in_flight_per_thread': (v // 10) % 10, 'nontemporal': bool(v % 10)}
     return {'fp16_mfma_tflops': round(out[0], 1), 'int8_mfma_tops': round(out[1], 1),
             'hbm_copy_gbs': round(out[2], 1), 'hbm_read_gbs': round(out[3], 1),
             'sclk_mhz_fp16_loop': round(out[4], 1), 'sclk_mhz_int8_loop': round(out[5], 1),
+            'hbm_copy_config': cfg(out[6]), 'hbm_read_config': cfg(out[7]),
             'method': 'csrc/k_ubench.hip: best of %d timed launches after a warm-up; MFMA loops on random operands, '
-                      '8 chains per wave, 2 waves per SIMD; HBM: 1 GiB buffers (copy counts read + write bytes)' % reps}
+                      '8 chains per wave, 4 waves per SIMD; HBM: 1 GiB buffers (copy counts read + write bytes), '
+                      'contiguous 16-32 KiB blocks per workgroup iteration, best of 4/8/16 workgroups per CU x 4/8 '
+                      '16-B loads in flight per thread x plain/nontemporal' % reps}
 
 
 class ClockProbe:

@@ -1,0 +1,17 @@
+#!/bin/bash
+# SQ counter passes (timing breakdown, instruction mix, waves) over tools/fwd_only.py for one blob dtype.
+# GPU box, repo root: DT=fp16x2 bash tools/pmc_dt.sh <tag>  -> gpurun_out/pmc_<tag>/pmc_<n>/, table in pmc_<tag>.txt
+export TMPDIR=/tmp
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+T=${1:-dt}
+set -e
+rm -rf $R/gpurun_out/pmc_$T; mkdir -p $R/gpurun_out/pmc_$T
+i=0
+for set in "SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_VMEM" \
+           "SQ_INSTS_VALU SQ_INSTS_LDS SQ_INSTS_MFMA SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_VALU_MFMA_BUSY_CYCLES" \
+           "SQ_WAVES SQ_INSTS_SALU SQ_ACTIVE_INST_SCA SQ_WAIT_INST_LDS GRBM_GUI_ACTIVE"; do
+  i=$((i+1))
+  (cd /tmp && timeout -s KILL 150 rocprofv3 --pmc $set -d $R/gpurun_out/pmc_$T/pmc_$i -o run --output-format csv -- python3 $R/tools/fwd_only.py 2) > $R/gpurun_out/pmc_$T/pass_$i.log 2>&1 || { echo "pass $i failed"; tail -5 $R/gpurun_out/pmc_$T/pass_$i.log; exit 1; }
+  echo "pass $i ok"
+done
+python3 $R/tools/pmc_table.py $R/gpurun_out/pmc_$T > $R/gpurun_out/pmc_$T.txt
