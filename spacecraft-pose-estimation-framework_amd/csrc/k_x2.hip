@@ -765,6 +765,227 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
   return hipErrorNotSupported;
 }
 
+// ------------------------------------------------------------------------------------------ front: stem + block 1
+// uint8 NHWC frames -> stem ConvBnAct 3 -> 32, 3x3 / 2 (mobilenet_v2.py:252-254; ToTensor's /255 folded into the
+// weights) -> block 1 (depthwise 3x3 + project 32 -> 16, pytorch_layers.py:65-98) -> fp32 block-1 output, one kernel:
+// the 32-channel stem map (8.4 MB/img at 512^2 in fp32) never reaches HBM. A u8 pixel is exact in fp16, so the stem is
+// two MFMAs per product (W_hi x + W_lo x, the blob's split /255-folded operand x0). Its K runs over the 3 input rows
+// of the stencil, one K step per row ky with k = 4 kx + ci (ci padded to 4; k >= 12 zero), so a lane's B fragment is
+// one 16-B (kg 0) or 8-B (kg 1) LDS read of the staged input tile [row][col][4] (fp16). The stem map of the output
+// tile + halo goes to the fp32 slab (zero outside the image: the depthwise's padding), then block 1 runs as in
+// x2_irb_kernel.
+template <int TH, int TW>
+struct X2FrontGeom {
+  static constexpr int NW = 4;
+  static constexpr int PH = TH + 2, PW = TW + 2;        // stem pixels of the tile (+ block-1 halo)
+  static constexpr int PIN = PH * PW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
+  static constexpr int IRW = 2 * PH + 1, ICL = 2 * PW + 1;   // input rows / columns of the stem stencil
+  static constexpr int ICS = (ICL * 4 + 8 + 7) / 8 * 8;   // halves per staged input row (16-B rows; zero tail)
+  using SL = X2Slab<1, PINP>;
+  static constexpr int POUT16 = TH * TW / 16, QPW = POUT16 / NW;
+  static constexpr int EPT = (PIN16 + NW - 1) / NW;
+  static constexpr int XI_H = (IRW * ICS + 7) / 8 * 8;   // staged input (halves)
+  static constexpr int DWS = 9 * 32 + 32;               // block-1 depthwise weights + bias (floats)
+  static constexpr int LDS_BYTES = XI_H * 2 + (SL::FLOATS + DWS) * 4;
+  static_assert(TW == 16 && POUT16 % NW == 0 && EPT <= 32, "front tile");
+};
+
+template <int TH, int TW>
+__global__ __launch_bounds__(256) void x2_front_kernel(
+    const uint8_t* __restrict__ X, const _Float16* __restrict__ Wsx, const float* __restrict__ bs,
+    const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
+    const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
+    uint32_t nwg) {
+  using G = X2FrontGeom<TH, TW>;
+  using SL = typename G::SL;
+  constexpr int NW = G::NW;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  _Float16* Xi = reinterpret_cast<_Float16*>(smem);                     // [IRW][ICS] input tile, fp16
+  float* Sl = reinterpret_cast<float*>(smem + G::XI_H * 2);             // stem map of the tile (+halo), plane layout
+  float* Ds = Sl + SL::FLOATS;                                          // [9][32] depthwise weights, [32] bias
+
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int tx = (int)(L % (uint32_t)tiles_x);
+  L /= (uint32_t)tiles_x;
+  const int ty = (int)(L % (uint32_t)tiles_y);
+  const int b = (int)(L / (uint32_t)tiles_y);
+  const int oy0 = ty * TH, ox0 = tx * TW;
+  const int sy0 = oy0 - 1, sx0 = ox0 - 1;              // stem pixel of tile position (0, 0)
+  const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;      // input pixel of staged position (0, 0)
+
+  // ---- staging: input pixels (3 bytes each, zero outside the frame) -> fp16 [row][col][4]; block-1 depthwise
+  {
+    constexpr int NPX = G::IRW * G::ICL;
+    constexpr int NIT = (NPX + NW * 64 - 1) / (NW * 64);
+    const uint8_t* Xb = X + (size_t)b * H * W * 3;
+    uint32_t v[NIT][3];
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int u = tid + NW * 64 * i;
+      const int r = u / G::ICL, cc = u - r * G::ICL;
+      const int iy = iy0 + r, ix = ix0 + cc;
+      v[i][0] = v[i][1] = v[i][2] = 0;
+      if (u < NPX && iy >= 0 && iy < H && ix >= 0 && ix < W) {
+        const uint8_t* p = Xb + ((size_t)iy * W + ix) * 3;
+        v[i][0] = p[0];
+        v[i][1] = p[1];
+        v[i][2] = p[2];
+      }
+    }
+    float4 dwv[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + NW * 64 * i;   // 72 pieces of the [9][32] weights, 8 of the bias
+      dwv[i] = u < 72 ? *reinterpret_cast<const float4*>(Wd + 4 * u)
+                      : u < 80 ? *reinterpret_cast<const float4*>(bd + 4 * (u - 72)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      const int u = tid + NW * 64 * i;
+      if (u >= NPX) break;
+      const int r = u / G::ICL, cc = u - r * G::ICL;
+      *reinterpret_cast<uint2*>(Xi + r * G::ICS + 4 * cc) =
+          make_uint2(pack_h2((_Float16)(float)v[i][0], (_Float16)(float)v[i][1]), pack_h2((_Float16)(float)v[i][2],
+                                                                                          (_Float16)0.0f));
+    }
+    if (tid < G::IRW) *reinterpret_cast<uint2*>(Xi + tid * G::ICS + 4 * G::ICL) = make_uint2(0, 0);
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + NW * 64 * i;
+      if (u < 80) *reinterpret_cast<float4*>(Ds + 4 * u) = dwv[i];
+    }
+  }
+  // stem A fragments for the 3 K steps (ky) and 2 channel halves: lane (r16 = output channel, kg) holds k = 8kg + e,
+  // k = 4 kx + ci. The blob's x0 is already in this order: [2 planes][3 ky][32 ch][32 k] (spef_blob.hpp).
+  f16x8 sah[2][3], sal[2][3];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const int off = (ky * 32 + 16 * h + r16) * 32 + 8 * kg;
+      sah[h][ky] = *reinterpret_cast<const f16x8*>(Wsx + off);
+      sal[h][ky] = *reinterpret_cast<const f16x8*>(Wsx + 3 * 32 * 32 + off);
+    }
+  float sb[2][4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float4 t = *reinterpret_cast<const float4*>(bs + 16 * h + 4 * kg);
+    sb[h][0] = t.x; sb[h][1] = t.y; sb[h][2] = t.z; sb[h][3] = t.w;
+  }
+  __syncthreads();
+
+  // ---- stem of the tile's stem pixels p = 16 pt + r16 -> slab (ReLU; zero outside the stem map)
+#pragma unroll
+  for (int j = 0; j < G::EPT; ++j) {
+    const int pt = wave + NW * j;
+    if (pt >= G::PIN16) break;
+    const int p = pt * 16 + r16;
+    const int pc = p < G::PIN ? p : G::PIN - 1;
+    const int py = pc / G::PW, px = pc - (pc / G::PW) * G::PW;
+    const int sy = sy0 + py, sx = sx0 + px;
+    const bool ok = p < G::PIN && sy >= 0 && sy < OH && sx >= 0 && sx < OW;
+    f32x4 e[2];
+#pragma unroll
+    for (int h = 0; h < 2; ++h) e[h] = f32x4{sb[h][0], sb[h][1], sb[h][2], sb[h][3]};
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const _Float16* xr = Xi + (2 * py + ky) * G::ICS + 8 * px;   // stem pixel px reads input cols 2px .. 2px + 2
+      f16x8 bx;
+      if (kg == 0) {
+        bx = *reinterpret_cast<const f16x8*>(xr);
+      } else if (kg == 1) {
+        const uint2 t = *reinterpret_cast<const uint2*>(xr + 8);
+        bx = __builtin_bit_cast(f16x8, make_uint4(t.x, t.y, 0u, 0u));
+      } else {
+        bx = __builtin_bit_cast(f16x8, make_uint4(0u, 0u, 0u, 0u));
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        e[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sah[h][ky], bx, e[h], 0, 0, 0);
+        e[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sal[h][ky], bx, e[h], 0, 0, 0);
+      }
+    }
+    if (p < G::PINP) {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        float4 o;
+        o.x = ok ? fmaxf(e[h][0], 0.f) : 0.f;
+        o.y = ok ? fmaxf(e[h][1], 0.f) : 0.f;
+        o.z = ok ? fmaxf(e[h][2], 0.f) : 0.f;
+        o.w = ok ? fmaxf(e[h][3], 0.f) : 0.f;
+        *reinterpret_cast<float4*>(Sl + SL::at(p, 4 * h + kg)) = o;
+      }
+    }
+  }
+  __syncthreads();
+
+  // ---- block 1: depthwise 3x3 (fp32, kx outer / ky inner) + BN + ReLU -> hi / lo -> project 32 -> 16
+  float a[G::QPW][8];
+  int pbase[G::QPW];
+  {
+    const float4 d0 = *reinterpret_cast<const float4*>(Ds + 288 + 8 * kg);
+    const float4 d1 = *reinterpret_cast<const float4*>(Ds + 288 + 8 * kg + 4);
+#pragma unroll
+    for (int q = 0; q < G::QPW; ++q) {
+      a[q][0] = d0.x; a[q][1] = d0.y; a[q][2] = d0.z; a[q][3] = d0.w;
+      a[q][4] = d1.x; a[q][5] = d1.y; a[q][6] = d1.z; a[q][7] = d1.w;
+      const int o = (wave * G::QPW + q) * 16 + r16;
+      pbase[q] = (o / TW) * G::PW + (o % TW);
+    }
+  }
+#pragma unroll
+  for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+    for (int ky = 0; ky < 3; ++ky) {
+      const float* wt = Ds + (ky * 3 + kx) * 32 + 8 * kg;
+      const float4 w0 = *reinterpret_cast<const float4*>(wt), w1 = *reinterpret_cast<const float4*>(wt + 4);
+      const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+#pragma unroll
+      for (int q = 0; q < G::QPW; ++q) {
+        const int p = pbase[q] + ky * G::PW + kx;
+        const float4 x0 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
+        const float4 x1 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
+        const float x8[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
+#pragma unroll
+        for (int e = 0; e < 8; ++e) a[q][e] = fmaf(x8[e], w8[e], a[q][e]);
+      }
+    }
+  const f16x8 ph = *reinterpret_cast<const f16x8*>(Wp + r16 * 32 + 8 * kg);
+  const f16x8 pl = *reinterpret_cast<const f16x8*>(Wp + 16 * 32 + r16 * 32 + 8 * kg);
+  const float4 bb = *reinterpret_cast<const float4*>(bp + 4 * kg);
+#pragma unroll
+  for (int q = 0; q < G::QPW; ++q) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) a[q][e] = fmaxf(a[q][e], 0.f);
+    f16x8 bh, bl;
+    split8(a[q], bh, bl);
+    const f32x4 v = mfma_x2(ph, pl, bh, bl, f32x4{bb.x, bb.y, bb.z, bb.w});
+    const int o = (wave * G::QPW + q) * 16 + r16;
+    const int gy = oy0 + o / TW, gx = ox0 + o % TW;
+    if (gy < OH && gx < OW)
+      *reinterpret_cast<float4*>(Y + (((size_t)b * OH + gy) * OW + gx) * 16 + 4 * kg) = make_float4(v[0], v[1], v[2], v[3]);
+  }
+}
+
+hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
+                           const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
+                           hipStream_t s) {
+  constexpr int TH = 8, TW = 16;
+  using G = X2FrontGeom<TH, TW>;
+  if (!x || !wsx || !bs || !wd || !bd || !wp || !bp || !y) return hipErrorInvalidValue;
+  const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
+  const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
+  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+  const uint32_t nwg = (uint32_t)nwg64;
+  static_assert(G::LDS_BYTES <= 65536, "front kernel LDS");
+  x2_front_kernel<TH, TW><<<nwg, 256, G::LDS_BYTES, s>>>((const uint8_t*)x, (const _Float16*)wsx, bs, wd, bd,
+                                                        (const _Float16*)wp, bp, (float*)y, H, W, OH, OW, tiles_x,
+                                                        tiles_y, nwg);
+  return hipGetLastError();
+}
+
 // ------------------------------------------------------------------------------------------ 1x1 conv, fp32 I/O
 // C^T = W X^T as pw_kernel: a wave owns NT output-channel tiles x MT pixel tiles; 4 waves on 64 MT consecutive
 // pixels; channel chunks fastest-varying so one pixel block's chunks share an XCD L2. B fragments: 8 fp32 values

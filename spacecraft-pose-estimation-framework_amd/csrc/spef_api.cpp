@@ -269,6 +269,26 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const bool front = !f32 && !x2 && c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx && nx->kind == OP_IRB &&
                          nx->cin == 32 && nx->hidden == 32 && nx->cout == 16 && nx->expand == 1 && nx->stride == 1 &&
                          op.cout == 32 && op.x0 != kAbsent;
+      const bool front_x2 = x2 && c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx &&
+                            nx->kind == OP_IRB && nx->cin == 32 && nx->hidden == 32 && nx->cout == 16 &&
+                            nx->expand == 1 && nx->stride == 1 && op.cout == 32 && op.x0 != kAbsent;
+      if (front_x2) {   // fp16x2: stem (MFMA, exact u8 operand) + block 1 in one kernel, fp32 output
+        void* y = c->buf[0];
+        const double px = (double)B * OH * OW;
+        HIP_TRY(prof_launch(c, s, "x2_front_kernel<stem+block1>", (double)B * h * w * 3 + px * 16 * 4,
+                            px * (2 * 27 * 32 + 18 * 32 + 2 * 32 * 16), [&] {
+          return launch_x2_front(input, ptr<void>(c, op.x0), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
+                                 ptr<float>(c, nx->b1), ptr<void>(c, nx->w2), ptr<float>(c, nx->b2), y, B, h, w, OH,
+                                 OW, s);
+        }));
+        cur = y;
+        h = OH;
+        w = OW;
+        ch = (int)nx->cout;
+        skip_next = true;
+        ++op_index;
+        continue;
+      }
       if (front) {
         void* y = c->buf[0];
         const double px = (double)B * OH * OW;
@@ -719,7 +739,7 @@ static void op_extents(const OpDesc& op, uint32_t dtype, uint64_t ext[9]) {
   const uint64_t ci = op.cin, co = op.cout, h = op.hidden;
   if (dtype == DT_X2) {   // fp16x2: 1x1 weights as [2][rows][Kp] fp16 planes (hi, lo); depthwise / biases padded to 32
     switch (op.kind) {
-      case OP_STEM: ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * co * 32 * 2; break;
+      case OP_STEM: ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * 3 * co * 32 * 2; break;
       case OP_IRB:
         if (op.expand != 1) { ext[0] = 2 * r32(h) * r32(ci) * 2; ext[1] = r32(h) * 4; }
         ext[2] = 9 * r32(h) * 4; ext[3] = r32(h) * 4;

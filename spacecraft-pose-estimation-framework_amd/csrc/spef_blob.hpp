@@ -31,6 +31,9 @@
 //   OP_QFC   [0] fully_connected bias width (signed)
 // act = the activation storage type (fp16, bf16 or fp32 -- dtype 4, whose depthwise weights are fp32 as in bf16
 // blobs and whose stem x0 is fp32 hi + zero lo); Kp = K rounded up to 32, Np = N rounded up to 16, padding 0.
+// fp16x2 blob (dtype 5, k_x2.hip; fp32 activations): every 1x1 weight is [2][rows][Kp] fp16 (hi plane = fp16(w), lo
+// plane = fp16(w - hi)), expand rows padded to H32 = hidden rounded up to 32; depthwise fp32 [9][H32], expand and
+// depthwise biases fp32 [H32]; stem x0 = [2][3 ky][32 ch][32 k] fp16 hi / lo of the /255-folded weights, k = 4 kx + ci.
 // BatchNorm (eps 1e-5) is folded: w' = w*g/sqrt(v+eps), b' = beta - mean*g/sqrt(v+eps).
 #pragma once
 #include <stdint.h>

@@ -88,6 +88,9 @@ bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool 
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
                          int B, int H, int W, int OH, int OW, hipStream_t s);
+// uint8 NHWC frames -> stem + block 1 -> fp32 [B][OH][OW][16] (x2_front_kernel); wsx: blob OP_STEM x0 of dtype 5.
+hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
+                           const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
 // 1x1 conv + BN + ReLU on fp32 activations X [M][K] with wt [2][Np][Kp] fp16 (hi, lo) -> fp32 Y [M][N]; Np % 64 == 0.
 hipError_t launch_x2_pw_relu(const void* x, const void* wt, const float* bias, float* y, int64_t M, int K, int N,
                              hipStream_t s);

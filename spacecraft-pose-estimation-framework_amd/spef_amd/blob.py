@@ -14,7 +14,8 @@ Depthwise weights are fp16 in fp16 blobs (fp32 in bf16 blobs); stem, bias and he
 ``fp16x2`` (dtype 5, the fp32-accurate fused schedule of csrc/k_x2.hip): every 1x1 weight is stored as two fp16
 planes [2][rows][Kp], hi = fp16(w) and lo = fp16(w - hi) of the float64 folded weight (22 significant bits), expand
 rows padded to 32; depthwise weights fp32 [9][H32] and the hidden-width biases padded to H32 = hidden rounded up to
-32 (zeros), so the kernel never masks a channel.
+32 (zeros), so the kernel never masks a channel; the stem's /255-folded MFMA operand x0 as [2][3 ky][32][32] hi / lo
+planes with k = 4 kx + ci (the front kernel's fragment order).
 """
 from __future__ import annotations
 
@@ -164,9 +165,13 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
                 hi[:, k] = w255[ky * 9 + j]
     else:
         hi[:, :27] = w255.T
-    if dtype == 'fp16x2':
-        sp = split_f16(hi)
-        x0 = np.concatenate(sp).tobytes()
+    if dtype == 'fp16x2':   # x2_front_kernel's operand: [plane][ky][32 ch][32 k], k = 4 kx + ci (k >= 12 zero)
+        a = np.zeros((3, arch.stem.cout, 32), np.float64)
+        for ky in range(3):
+            for kx in range(3):
+                for ci in range(3):
+                    a[ky, :, 4 * kx + ci] = w255[ky * 9 + kx * 3 + ci]
+        x0 = np.concatenate(split_f16(a)).tobytes()
     else:
         hi_r = _round_act(hi, dtype)
         x0 = _to_act(np.concatenate([hi_r, _round_act(hi - hi_r, dtype)]), dtype)
