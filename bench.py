@@ -61,10 +61,11 @@ def pmc_traffic(kernel_key: str, path: str):
     if kernel_key in kernels:
         return kernels[kernel_key]['hbm_bytes_per_launch']
     import re
-    m = re.fullmatch(r'(ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
-    if m:   # fused block key -> the one template instantiation profiled for that geometry
+    m = re.fullmatch(r'(x2_irb_kernel|ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
+    if m:   # fused block key -> the one template instantiation profiled for that geometry (fp16x2: slab or role-split)
         geo = ','.join(m.groups()[1:]) + ','
-        hits = [v for k, v in kernels.items() if re.match(m.group(1) + r'<B?F16,' + re.escape(geo), k)]
+        kind = r'x2_ir[bw]_kernel<' if m.group(1).startswith('x2') else m.group(1) + r'<B?F16,'
+        hits = [v for k, v in kernels.items() if re.match(kind + re.escape(geo), k)]
     else:   # e.g. front_kernel<stem+block1> -> front_kernel<...> or its fp16 form front_vp_kernel<...>
         base = kernel_key.split('<')[0]
         prefixes = (base + '<', base.replace('_kernel', '_vp_kernel') + '<')

@@ -791,7 +791,7 @@ struct X2FrontGeom {
 };
 
 template <int TH, int TW>
-__global__ __launch_bounds__(256) void x2_front_kernel(
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void x2_front_kernel(
     const uint8_t* __restrict__ X, const _Float16* __restrict__ Wsx, const float* __restrict__ bs,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
@@ -815,23 +815,33 @@ __global__ __launch_bounds__(256) void x2_front_kernel(
   const int sy0 = oy0 - 1, sx0 = ox0 - 1;              // stem pixel of tile position (0, 0)
   const int iy0 = 2 * sy0 - 1, ix0 = 2 * sx0 - 1;      // input pixel of staged position (0, 0)
 
-  // ---- staging: input pixels (3 bytes each, zero outside the frame) -> fp16 [row][col][4]; block-1 depthwise
+  // ---- staging: the input rows of the stencil as aligned dword loads (a row segment is 3 ICL bytes at any byte
+  // alignment), bytes scattered to fp16 [row][col][4] over a zero-filled tile (zero outside the frame: the stem's
+  // padding; the ci = 3 pad); block-1 depthwise weights + bias
   {
-    constexpr int NPX = G::IRW * G::ICL;
-    constexpr int NIT = (NPX + NW * 64 - 1) / (NW * 64);
-    const uint8_t* Xb = X + (size_t)b * H * W * 3;
-    uint32_t v[NIT][3];
+    constexpr int NDW = (3 * G::ICL + 3 + 3) / 4 + 1;   // dwords covering one row segment at any alignment
+    constexpr int NPC = G::IRW * NDW;
+    constexpr int NIT = (NPC + NW * 64 - 1) / (NW * 64);
+    constexpr int NZ = G::XI_H / 8;                     // 16-B pieces of the staged tile
+    const size_t img = (size_t)b * H * W * 3;
+    uint32_t v[NIT];
+    bool ld[NIT];
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       const int u = tid + NW * 64 * i;
-      const int r = u / G::ICL, cc = u - r * G::ICL;
-      const int iy = iy0 + r, ix = ix0 + cc;
-      v[i][0] = v[i][1] = v[i][2] = 0;
-      if (u < NPX && iy >= 0 && iy < H && ix >= 0 && ix < W) {
-        const uint8_t* p = Xb + ((size_t)iy * W + ix) * 3;
-        v[i][0] = p[0];
-        v[i][1] = p[1];
-        v[i][2] = p[2];
+      const int r = u / NDW, j = u - r * NDW;
+      const int iy = iy0 + r;
+      v[i] = 0;
+      ld[i] = false;
+      if (u < NPC && iy >= 0 && iy < H) {
+        const int64_t rb = (int64_t)(img + (size_t)iy * W * 3);
+        const int64_t vs = rb + 3 * (int64_t)(ix0 > 0 ? ix0 : 0);
+        const int64_t ve = rb + 3 * (int64_t)(ix0 + G::ICL < W ? ix0 + G::ICL : W);
+        const int64_t a = ((rb + 3 * (int64_t)ix0) & ~(int64_t)3) + 4 * j;   // may start left of the frame row
+        if (a + 4 > vs && a < ve) {
+          v[i] = *reinterpret_cast<const uint32_t*>(X + a);
+          ld[i] = true;
+        }
       }
     }
     float4 dwv[2];
@@ -841,33 +851,38 @@ __global__ __launch_bounds__(256) void x2_front_kernel(
       dwv[i] = u < 72 ? *reinterpret_cast<const float4*>(Wd + 4 * u)
                       : u < 80 ? *reinterpret_cast<const float4*>(bd + 4 * (u - 72)) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
-#pragma unroll
-    for (int i = 0; i < NIT; ++i) {
-      const int u = tid + NW * 64 * i;
-      if (u >= NPX) break;
-      const int r = u / G::ICL, cc = u - r * G::ICL;
-      *reinterpret_cast<uint2*>(Xi + r * G::ICS + 4 * cc) =
-          make_uint2(pack_h2((_Float16)(float)v[i][0], (_Float16)(float)v[i][1]), pack_h2((_Float16)(float)v[i][2],
-                                                                                          (_Float16)0.0f));
-    }
-    if (tid < G::IRW) *reinterpret_cast<uint2*>(Xi + tid * G::ICS + 4 * G::ICL) = make_uint2(0, 0);
+    for (int u = tid; u < NZ; u += NW * 64) reinterpret_cast<uint4*>(Xi)[u] = make_uint4(0, 0, 0, 0);
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int u = tid + NW * 64 * i;
       if (u < 80) *reinterpret_cast<float4*>(Ds + 4 * u) = dwv[i];
     }
+    __syncthreads();
+    // dword j's first byte is segment byte 4 j - off (off = the segment start's offset in its dword); valid bytes:
+    // segment bytes [rlo, rhi), the frame row's part of the segment
+#pragma unroll
+    for (int i = 0; i < NIT; ++i) {
+      if (!ld[i]) continue;
+      const int u = tid + NW * 64 * i;
+      const int r = u / NDW, j = u - r * NDW;
+      const int64_t rb = (int64_t)(img + (size_t)(iy0 + r) * W * 3);
+      const int off = (int)((rb + 3 * (int64_t)ix0) & 3);      // segment start within its dword
+      const int rlo = ix0 < 0 ? -3 * ix0 : 0, rhi = 3 * ((ix0 + G::ICL < W ? ix0 + G::ICL : W) - ix0);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int rel = 4 * j + k - off;   // byte of the segment: column rel / 3, channel rel % 3
+        if (rel < rlo || rel >= rhi) continue;
+        Xi[r * G::ICS + 4 * (rel / 3) + rel % 3] = (_Float16)(float)((v[i] >> (8 * k)) & 0xffu);
+      }
+    }
   }
   // stem A fragments for the 3 K steps (ky) and 2 channel halves: lane (r16 = output channel, kg) holds k = 8kg + e,
   // k = 4 kx + ci. The blob's x0 is already in this order: [2 planes][3 ky][32 ch][32 k] (spef_blob.hpp).
-  f16x8 sah[2][3], sal[2][3];
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int ky = 0; ky < 3; ++ky) {
-      const int off = (ky * 32 + 16 * h + r16) * 32 + 8 * kg;
-      sah[h][ky] = *reinterpret_cast<const f16x8*>(Wsx + off);
-      sal[h][ky] = *reinterpret_cast<const f16x8*>(Wsx + 3 * 32 * 32 + off);
-    }
+  auto stem_a = [&](int h, int ky, f16x8& ah, f16x8& al) {
+    const int off = (ky * 32 + 16 * h + r16) * 32 + 8 * kg;
+    ah = *reinterpret_cast<const f16x8*>(Wsx + off);
+    al = *reinterpret_cast<const f16x8*>(Wsx + 3 * 32 * 32 + off);
+  };
   float sb[2][4];
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -876,46 +891,62 @@ __global__ __launch_bounds__(256) void x2_front_kernel(
   }
   __syncthreads();
 
-  // ---- stem of the tile's stem pixels p = 16 pt + r16 -> slab (ReLU; zero outside the stem map)
+  // ---- stem of the tile's stem pixels p = 16 pt + r16 -> slab (ReLU; zero outside the stem map); K steps (ky)
+  // outermost so one (ky, half) A fragment pair is live at a time
+  {
+    f32x4 e[G::EPT][2];
+    int xo[G::EPT];
+    bool ok[G::EPT];
 #pragma unroll
-  for (int j = 0; j < G::EPT; ++j) {
-    const int pt = wave + NW * j;
-    if (pt >= G::PIN16) break;
-    const int p = pt * 16 + r16;
-    const int pc = p < G::PIN ? p : G::PIN - 1;
-    const int py = pc / G::PW, px = pc - (pc / G::PW) * G::PW;
-    const int sy = sy0 + py, sx = sx0 + px;
-    const bool ok = p < G::PIN && sy >= 0 && sy < OH && sx >= 0 && sx < OW;
-    f32x4 e[2];
+    for (int j = 0; j < G::EPT; ++j) {
+      const int p = (wave + NW * j) * 16 + r16;
+      const int pc = p < G::PIN ? p : G::PIN - 1;
+      const int py = pc / G::PW, px = pc - (pc / G::PW) * G::PW;
+      const int sy = sy0 + py, sx = sx0 + px;
+      ok[j] = p < G::PIN && sy >= 0 && sy < OH && sx >= 0 && sx < OW;
+      xo[j] = 2 * py * G::ICS + 8 * px + (kg == 1 ? 8 : 0);   // stem pixel px reads input cols 2px .. 2px + 2
 #pragma unroll
-    for (int h = 0; h < 2; ++h) e[h] = f32x4{sb[h][0], sb[h][1], sb[h][2], sb[h][3]};
+      for (int h = 0; h < 2; ++h) e[j][h] = f32x4{sb[h][0], sb[h][1], sb[h][2], sb[h][3]};
+    }
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
-      const _Float16* xr = Xi + (2 * py + ky) * G::ICS + 8 * px;   // stem pixel px reads input cols 2px .. 2px + 2
-      f16x8 bx;
-      if (kg == 0) {
-        bx = *reinterpret_cast<const f16x8*>(xr);
-      } else if (kg == 1) {
-        const uint2 t = *reinterpret_cast<const uint2*>(xr + 8);
-        bx = __builtin_bit_cast(f16x8, make_uint4(t.x, t.y, 0u, 0u));
-      } else {
-        bx = __builtin_bit_cast(f16x8, make_uint4(0u, 0u, 0u, 0u));
+      f16x8 bx[G::EPT];
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        const _Float16* xr = Xi + xo[j] + ky * G::ICS;
+        if (kg == 0) {
+          bx[j] = *reinterpret_cast<const f16x8*>(xr);
+        } else if (kg == 1) {
+          const uint2 t = *reinterpret_cast<const uint2*>(xr);
+          bx[j] = __builtin_bit_cast(f16x8, make_uint4(t.x, t.y, 0u, 0u));
+        } else {
+          bx[j] = __builtin_bit_cast(f16x8, make_uint4(0u, 0u, 0u, 0u));
+        }
       }
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        e[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sah[h][ky], bx, e[h], 0, 0, 0);
-        e[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(sal[h][ky], bx, e[h], 0, 0, 0);
+        f16x8 ah, al;
+        stem_a(h, ky, ah, al);
+#pragma unroll
+        for (int j = 0; j < G::EPT; ++j) {
+          if (wave + NW * j >= G::PIN16) break;
+          e[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bx[j], e[j][h], 0, 0, 0);
+          e[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bx[j], e[j][h], 0, 0, 0);
+        }
       }
     }
-    if (p < G::PINP) {
+#pragma unroll
+    for (int j = 0; j < G::EPT; ++j) {
+      const int pt = wave + NW * j;
+      if (pt >= G::PIN16) break;
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
         float4 o;
-        o.x = ok ? fmaxf(e[h][0], 0.f) : 0.f;
-        o.y = ok ? fmaxf(e[h][1], 0.f) : 0.f;
-        o.z = ok ? fmaxf(e[h][2], 0.f) : 0.f;
-        o.w = ok ? fmaxf(e[h][3], 0.f) : 0.f;
-        *reinterpret_cast<float4*>(Sl + SL::at(p, 4 * h + kg)) = o;
+        o.x = ok[j] ? fmaxf(e[j][h][0], 0.f) : 0.f;
+        o.y = ok[j] ? fmaxf(e[j][h][1], 0.f) : 0.f;
+        o.z = ok[j] ? fmaxf(e[j][h][2], 0.f) : 0.f;
+        o.w = ok[j] ? fmaxf(e[j][h][3], 0.f) : 0.f;
+        *reinterpret_cast<float4*>(Sl + SL::at(pt * 16 + r16, 4 * h + kg)) = o;
       }
     }
   }
@@ -935,7 +966,7 @@ __global__ __launch_bounds__(256) void x2_front_kernel(
       pbase[q] = (o / TW) * G::PW + (o % TW);
     }
   }
-#pragma unroll
+#pragma unroll 1   // (one kernel column in flight: fully unrolled, the 36 tap loads hoist and cost an occupancy step)
   for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
     for (int ky = 0; ky < 3; ++ky) {
@@ -989,8 +1020,11 @@ hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, cons
 // ------------------------------------------------------------------------------------------ 1x1 conv, fp32 I/O
 // C^T = W X^T as pw_kernel: a wave owns NT output-channel tiles x MT pixel tiles; 4 waves on 64 MT consecutive
 // pixels; channel chunks fastest-varying so one pixel block's chunks share an XCD L2. B fragments: 8 fp32 values
-// per lane from HBM / L2, split once and used by all NT channel tiles.
-template <int NT, int MT>
+// per lane from HBM / L2, split once and used by all NT channel tiles. POOL (URSONetHead's x.mean([2,3]),
+// ursonet.py:30, when HW % 64 == 0): the 1280-channel map is never stored -- each wave sums the ReLU'd outputs of its
+// 64 pixels (one image) over its pixel tiles and then over the 16 pixel lanes (xor shuffles, fixed order) into
+// Y = partial [M / 64][N]; x2_pool_reduce_kernel adds an image's partials in order and divides by HW.
+template <int NT, int MT, bool POOL>
 __global__ __launch_bounds__(256) void x2_pw_kernel(const float* __restrict__ X, const _Float16* __restrict__ Wt,
                                                     const float* __restrict__ bias, float* __restrict__ Y, int64_t M,
                                                     int K, int N, int Np, int Kp, int n_chunks, uint32_t nwg) {
@@ -1040,6 +1074,25 @@ __global__ __launch_bounds__(256) void x2_pw_kernel(const float* __restrict__ X,
       for (int m = 0; m < MT; ++m) acc[a][m] = mfma_x2(ah, al, bh[m], bl[m], acc[a][m]);
     }
   }
+  if constexpr (POOL) {   // MT = 4: the wave's 64 pixels m0 .. m0 + 63, all valid (M % 64 == 0)
+#pragma unroll
+    for (int a = 0; a < NT; ++a) {
+      float sm[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < MT; ++m) t += fmaxf(acc[a][m][r], 0.f);
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+        sm[r] = t;
+      }
+      const int i = n0 + 16 * a + 4 * kg;
+      if (r16 == 0 && i < N)
+        *reinterpret_cast<float4*>(Y + (size_t)(m0 / 64) * N + i) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+    }
+    return;
+  }
 #pragma unroll
   for (int a = 0; a < NT; ++a) {
     const int i = n0 + 16 * a + 4 * kg;
@@ -1055,6 +1108,18 @@ __global__ __launch_bounds__(256) void x2_pw_kernel(const float* __restrict__ X,
   }
 }
 
+// pooled[b][c] = (sum over the image's HW / 64 wave partials, in order) / HW
+__global__ __launch_bounds__(256) void x2_pool_reduce_kernel(const float* __restrict__ part, float* __restrict__ pooled,
+                                                             int B, int nblk, int N, float inv_hw) {
+  const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (int64_t)B * N) return;
+  const int b = (int)(i / N), c = (int)(i % N);
+  const float* p = part + (size_t)b * nblk * N + c;
+  float t = 0.f;
+  for (int j = 0; j < nblk; ++j) t += p[(size_t)j * N];
+  pooled[i] = t * inv_hw;
+}
+
 hipError_t launch_x2_pw_relu(const void* x, const void* wt, const float* bias, float* y, int64_t M, int K, int N,
                              hipStream_t s) {
   if (M <= 0) return hipSuccess;
@@ -1065,8 +1130,29 @@ hipError_t launch_x2_pw_relu(const void* x, const void* wt, const float* bias, f
   const int64_t nwg64 = (M + 64 * MT - 1) / (64 * MT) * n_chunks;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  x2_pw_kernel<NT, MT><<<nwg, 256, 0, s>>>((const float*)x, (const _Float16*)wt, bias, y, M, K, N, Np, Kp, n_chunks,
-                                           nwg);
+  x2_pw_kernel<NT, MT, false><<<nwg, 256, 0, s>>>((const float*)x, (const _Float16*)wt, bias, y, M, K, N, Np, Kp,
+                                                  n_chunks, nwg);
+  return hipGetLastError();
+}
+
+bool x2_pw_pool_supported(int HW, int N) { return HW % 64 == 0 && N % 64 == 0; }
+
+hipError_t launch_x2_pw_pool(const void* x, const void* wt, const float* bias, float* part, float* pooled, int B,
+                             int HW, int K, int N, hipStream_t s) {
+  const int Kp = (K + 31) & ~31, Np = (N + 15) & ~15;
+  if ((K & 7) || !x2_pw_pool_supported(HW, N) || B <= 0) return hipErrorInvalidValue;
+  constexpr int NT = 4, MT = 4;
+  const int64_t M = (int64_t)B * HW;
+  const int n_chunks = Np / (16 * NT);
+  const int64_t nwg64 = (M + 64 * MT - 1) / (64 * MT) * n_chunks;
+  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+  const uint32_t nwg = (uint32_t)nwg64;
+  x2_pw_kernel<NT, MT, true><<<nwg, 256, 0, s>>>((const float*)x, (const _Float16*)wt, bias, part, M, K, N, Np, Kp,
+                                                 n_chunks, nwg);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  x2_pool_reduce_kernel<<<(unsigned)(((int64_t)B * N + 255) / 256), 256, 0, s>>>(part, pooled, B, HW / 64, N,
+                                                                                 1.0f / (float)HW);
   return hipGetLastError();
 }
 

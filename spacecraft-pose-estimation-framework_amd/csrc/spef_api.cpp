@@ -410,7 +410,15 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         ch = (int)op.cout;
       }
     } else if (op.kind == OP_LAST) {
-      if (x2) {   // fp32 map (keypoint head input, feature export, or the URSONet mean's input)
+      if (x2 && mode == 0 && x2_pw_pool_supported(h * w, (int)op.cout)) {   // last conv + mean, map never stored
+        float* part = (float*)pick({cur});
+        const double M3 = (double)B * h * w;
+        HIP_TRY(prof_launch(c, s, "x2_pw_kernel<pool>", M3 * op.cin * 4 + (double)op.cout * (op.cin * 4 + 4) +
+                            (double)B * op.cout * 4, 2.0 * M3 * op.cin * op.cout, [&] {
+          return launch_x2_pw_pool(cur, ptr<void>(c, op.w0), ptr<float>(c, op.b0), part, c->pooled, B, h * w,
+                                   (int)op.cin, (int)op.cout, s);
+        }));
+      } else if (x2) {   // fp32 map (keypoint head input, feature export, or the URSONet mean's input)
         float* y = (mode == 2 && feat_f32) ? feat_f32 : (float*)pick({cur});
         const double M3 = (double)B * h * w;
         HIP_TRY(prof_launch(c, s, "x2_pw_kernel<4,4>", M3 * (op.cin + op.cout) * 4 + (double)op.cout * (op.cin * 4 + 4),

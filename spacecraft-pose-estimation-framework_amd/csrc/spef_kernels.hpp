@@ -94,6 +94,10 @@ hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, cons
 // 1x1 conv + BN + ReLU on fp32 activations X [M][K] with wt [2][Np][Kp] fp16 (hi, lo) -> fp32 Y [M][N]; Np % 64 == 0.
 hipError_t launch_x2_pw_relu(const void* x, const void* wt, const float* bias, float* y, int64_t M, int K, int N,
                              hipStream_t s);
+// Same conv fused with URSONetHead's mean over HW (HW % 64 == 0, N % 64 == 0): part = workspace [B * HW / 64][N].
+bool x2_pw_pool_supported(int HW, int N);
+hipError_t launch_x2_pw_pool(const void* x, const void* wt, const float* bias, float* part, float* pooled, int B,
+                             int HW, int K, int N, hipStream_t s);
 // URSONetHead mean([2,3]) over an fp32 NHWC map: pooled [B][C].
 hipError_t launch_mean_hw(const float* x, float* pooled, int B, int HW, int C, hipStream_t s);
 

@@ -28,9 +28,10 @@ ORI_TOL_DEG = 0.1     # < 0.1 deg
 LOGIT_TOL = 1e-3
 
 
+@pytest.mark.parametrize('dtype', ['fp16', 'fp16x2'])
 @pytest.mark.parametrize('layout', ['f32_nchw', 'u8_nhwc'])
 @pytest.mark.parametrize('name', sorted(PREDICT_CASES))
-def test_predict_matches_reference_spetorch(golden, name, layout):
+def test_predict_matches_reference_spetorch(golden, name, layout, dtype):
     from spef_amd.spe.spe_utils import SPEUtils
     from spef_amd.spe_mi355x import SPEMi355x
     su_args, (n_ori, n_pos), wargs, _ = PREDICT_CASES[name]
@@ -39,7 +40,7 @@ def test_predict_matches_reference_spetorch(golden, name, layout):
     assert state_dict_digest(sd) == str(g['digest'])          # the fixture's weights, regenerated bit for bit
     su = SPEUtils(None, *su_args)
     assert su.orientation.n_bins == n_ori or su.ori_mode == 'regression'
-    tgt = SPEMi355x(Bl.pack(sd, dtype='fp16'), 'cuda:0', su)
+    tgt = SPEMi355x(Bl.pack(sd, dtype=dtype), 'cuda:0', su)
     try:
         fr = g['frames']
         x = M.u8_nhwc_to_nchw_f32(fr) if layout == 'f32_nchw' else torch.from_numpy(fr)
@@ -54,11 +55,14 @@ def test_predict_matches_reference_spetorch(golden, name, layout):
     assert dpos < POS_TOL_M, dpos
     if su.ori_mode == 'regression':                           # L2 normalise keeps the raw sign: compare values
         assert np.abs(pose['ori'] - g['pose_ori']).max() < 1e-3
-    # Probabilities, compared in log space: |d log p| <= 2 max|d logit|. The logit bound is the north_star's 1e-3 at
-    # the reference Linear init (std 0.01, pytorch_layers.py:25-27), scaled with the head's weight scale (the
-    # logit error is W . d(pooled features), linear in W): these fixtures use sharper heads for peaked histograms.
-    ori_tol = LOGIT_TOL * wargs.get('head_std', 0.01) / 0.01
-    pos_tol = LOGIT_TOL * wargs.get('pos_std', wargs.get('head_std', 0.01)) / 0.01
+    # Probabilities, compared in log space: |d log p| <= 2 max|d logit|. fp16x2 (fp32 activations, hi + lo operands)
+    # holds the north star's absolute 1e-3 at every head scale. The fp16 schedule holds it at the reference Linear init
+    # (std 0.01, pytorch_layers.py:25-27) only: its logit error is W . d(pooled features), linear in W, and these
+    # fixtures use sharper heads for peaked histograms -- measured 1.5e-2 at std 0.3 (test_gpu_x2.py::
+    # test_sharp_head_logits_absolute, bench pose_err_vs_fp32_sharp_head), so for fp16 the bound scales with the head.
+    scale = (lambda std: std / 0.01) if dtype == 'fp16' else (lambda std: 1.0)
+    ori_tol = LOGIT_TOL * scale(wargs.get('head_std', 0.01))
+    pos_tol = LOGIT_TOL * scale(wargs.get('pos_std', wargs.get('head_std', 0.01)))
     if 'ori_soft' in pose:
         dl = np.abs(np.log(pose['ori_soft'].astype(np.float64)) - np.log(g['pose_ori_soft'].astype(np.float64)))
         assert dl.max() < 2 * ori_tol, (dl.max(), ori_tol)
