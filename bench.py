@@ -44,7 +44,7 @@ INT8_TOLERANCE = ('int8 contract: bit-exact vs the integer oracle (oracle/int8_r
                   'section 5), not the fp16 1e-3 / 0.1 deg / 1 mm')
 INT8_BOUND = (0.05, 0.030, 0.25)   # logits, position (m), orientation (deg)
 # committed rocprofv3 FETCH_SIZE / WRITE_SIZE summaries, newest first (profiles/)
-FP16_TRAFFIC = ['r03f_pmc_traffic.json', 'r03e_pmc_traffic.json']
+FP16_TRAFFIC = ['r04_pmc_traffic.json', 'r03f_pmc_traffic.json']
 INT8_TRAFFIC = ['r03_int8_pmc_traffic.json']
 X2_TRAFFIC = ['r04_x2_pmc_traffic.json']
 

@@ -89,8 +89,14 @@ def evaluate_variants(sd, cfg, arch, out_dir: str, variants, calib_frames=None, 
             d = np.abs(np.sum(qa * qb, axis=1)) / (np.linalg.norm(qa, axis=1) * np.linalg.norm(qb, axis=1))
             rec['vs_fp32_variant']['ori_max_deg'] = float(np.degrees(2 * np.arccos(np.clip(d, 0, 1))).max())
             rec['vs_fp32_variant']['pos_max_m'] = float(np.linalg.norm(poses[v]['pos'] - poses[base]['pos'], axis=1).max())
+            # the north star's bound (raw outputs 1e-3, pose 0.1 deg / 1 mm) against the fp32 variant on these frames:
+            # fp16 storage error scales with the output range, so a trained head may fail it
+            vs = rec['vs_fp32_variant']
+            rec['within_north_star'] = bool(vs['max_abs'] < 1e-3 and vs['ori_max_deg'] < 0.1 and vs['pos_max_m'] < 1e-3)
         if ref_out is not None:
             rec['vs_reference'] = feature_stats(outs[v], ref_out)
+    if base:
+        summary['within_north_star'] = [base] + [v for v in outs if summary['variants'][v].get('within_north_star')]
     with open(os.path.join(ed, 'variants.json'), 'w') as f:
         json.dump(summary, f, indent=1)
     return summary
@@ -172,6 +178,11 @@ def main(argv=None):
             info['eval_host'] = evaluate_variants(sd, cfg, arch_from_state_dict(sd, residual=cfg.MODEL.BACKBONE.RESIDUAL),
                                                   out, variants, calib, bit_width, n_batches=a.eval_batches,
                                                   camera=camera)
+            ok = info['eval_host'].get('within_north_star')
+            if ok is not None and dtype not in ok and dtype != 'int8':
+                info['warning'] = (f'the built {dtype} blob exceeds the 1e-3 / 0.1 deg / 1 mm bound against the fp32 '
+                                   f'variant on the evaluation frames; variants within it: {ok}')
+                print('warning:', info['warning'], file=sys.stderr)
         else:
             info['eval_host'] = 'skipped: no GPU visible (run the build on the MI355X box to evaluate the variants)'
         with open(os.path.join(out, 'build.json'), 'w') as f:

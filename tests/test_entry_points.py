@@ -108,6 +108,7 @@ def test_build_tool_evaluates_precision_variants(tmp_path):
         assert name in v['variants']
     assert v['variants']['fp16']['vs_fp32_variant']['max_abs'] < 1e-3          # north-star logit bound
     assert v['variants']['fp16x2']['vs_fp32_variant']['max_abs'] < 1e-4        # fp32-accurate split schedule
+    assert 'fp16x2' in v['within_north_star'] and 'fp32' in v['within_north_star']
     assert v['variants']['bf16']['vs_fp32_variant']['max_abs'] < 6e-3          # test_gpu_c2_precision bound
     assert v['variants']['fp16']['vs_fp32_variant']['ori_max_deg'] < 0.1
     assert v['variants']['int8']['vs_fp32_variant']['max_abs'] < 0.05          # INT8_BOUND (bench.py)
