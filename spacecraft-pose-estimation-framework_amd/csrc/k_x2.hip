@@ -552,25 +552,39 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         }
       }
     };
+    // Stage data is loaded one iteration before it is stored: the pieces of expand chunk c + 2 and depthwise /
+    // project chunk c + 1 are fetched in iteration c - 1 (a whole chunk period of L2 latency hidden) and written to
+    // LDS at the start of iteration c (the same buffers and barriers as a load-and-store in iteration c).
+    uint4 v[G::NPIECE];
+    auto load_stage = [&](int c) {
+#pragma unroll
+      for (int i = 0; i < G::NPIECE; ++i) {
+        const void* src;
+        void* dst;
+        piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
+        v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+      }
+    };
+    auto store_stage = [&](int c) {
+#pragma unroll
+      for (int i = 0; i < G::NPIECE; ++i) {
+        const void* src;
+        void* dst;
+        piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
+        if (src) *reinterpret_cast<uint4*>(dst) = v[i];
+      }
+    };
+    load_stage(0);
     __syncthreads();                 // prologue stages visible
     expand(0);
     __syncthreads();                 // slab 0 visible
 #pragma unroll 1
     for (int c = 0; c < G::NCH; ++c) {
-      // stage expand chunk c + 2 and depthwise / project chunk c + 1 (loads issued before the expand)
-      uint4 v[G::NPIECE];
-      void* dst[G::NPIECE];
-#pragma unroll
-      for (int i = 0; i < G::NPIECE; ++i) {
-        const void* src;
-        piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst[i]);
-        v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
-        if (!src) dst[i] = nullptr;
+      store_stage(c);                // expand chunk c + 2, depthwise / project chunk c + 1
+      if (c + 1 < G::NCH) {
+        load_stage(c + 1);
+        expand(c + 1);
       }
-      if (c + 1 < G::NCH) expand(c + 1);
-#pragma unroll
-      for (int i = 0; i < G::NPIECE; ++i)
-        if (dst[i]) *reinterpret_cast<uint4*>(dst[i]) = v[i];
       __syncthreads();
     }
   } else {
