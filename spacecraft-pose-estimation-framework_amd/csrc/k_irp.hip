@@ -158,6 +158,9 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
     // expand A fragments of one hidden half: rows 32c + 16hh + r16, k = 32ks + 8kg
     x8 ea[G::KS];
     auto load_ea = [&](int c) {   // from L2, one step ahead
+#ifdef SPEF_KBENCH_IRW_NO_WLOAD   // tools/kbench timing ablation (wrong results): no weight loads after chunk 1
+      if (c > 1) return;
+#endif
       const T* w0 = We + (size_t)(32 * c + 16 * hh + r16) * CIN + 8 * kg;
 #pragma unroll
       for (int ks = 0; ks < G::KS; ++ks) ea[ks] = c < G::NCH ? load8<DT>(w0 + 32 * ks) : zero8<DT>();
@@ -165,6 +168,9 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
     // project A fragments: output-channel tiles wave + NM*t, hidden k = 32c + 8kg
     x8 pa[G::NCTW];
     auto load_pa = [&](int c) {
+#ifdef SPEF_KBENCH_IRW_NO_WLOAD
+      if (c > 1) return;
+#endif
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) {
         const int ct = wave + NM * t;
