@@ -505,7 +505,7 @@ __global__ __launch_bounds__(NW * 64) void front_vp_kernel(
         out[1] = (T)ac[1];
         out[2] = (T)ac[2];
         out[3] = (T)ac[3];
-        *reinterpret_cast<x4*>(yr + (size_t)h * SW_img * 16) = out;
+        SPEF_KB_YSTORE(*reinterpret_cast<x4*>(yr + (size_t)h * SW_img * 16) = out, out);
       }
     }
   }

@@ -283,7 +283,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       const int py = p / G::IW, px = p - py * G::IW;
       const int iy = iy0 + py, ix = ix0 + px;
       const bool ok = u < NU && p < G::PIN && g < CG && iy >= 0 && iy < H && ix >= 0 && ix < W;
-      xin[i] = load8<DT>(Xb + (ok ? ((size_t)iy * W + ix) * CIN + g * 8 : 0));
+      xin[i] = load8<DT>(Xb + (ok ? SPEF_KB_XOFF(((size_t)iy * W + ix) * CIN + g * 8) : 0));
       okm |= (uint32_t)ok << i;
     }
     const uint4 sl0 = slab_load(0);
@@ -906,7 +906,7 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (T)v[e];
-      *reinterpret_cast<x4*>(yr + co) = o;
+      SPEF_KB_YSTORE(*reinterpret_cast<x4*>(yr + co) = o, o);
     }
   }
   SPEF_TRACE(SPEF_TRACE_SLOTS - 1);

@@ -109,7 +109,7 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
         if (p < G::PIN) {
           const int py = p / G::IW, px = p - py * G::IW;
           const int iy = iy0 + py, ix = ix0 + px;
-          if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + ((size_t)iy * W + ix) * CIN + g * 8;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + SPEF_KB_XOFF(((size_t)iy * W + ix) * CIN + g * 8);
         }
       } else if ((u -= NXP) < NDP) {
         const int tap = u / DPR, g = u - tap * DPR;
@@ -307,7 +307,7 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
         x4 o4;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o4[e] = (T)v[e];
-        *reinterpret_cast<x4*>(yr + co) = o4;
+        SPEF_KB_YSTORE(*reinterpret_cast<x4*>(yr + co) = o4, o4);
       }
     }
   } else {

@@ -145,7 +145,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
         if (p < G::PIN && g < CG) {
           const int py = p / G::IW, px = p - py * G::IW;
           const int iy = iy0 + py, ix = ix0 + px;
-          if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + ((size_t)iy * W + ix) * CIN + g * 8;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + SPEF_KB_XOFF(((size_t)iy * W + ix) * CIN + g * 8);
         }
       } else if ((u -= NXP) < NDP) {
         const int tap = u / DPR, g = u - tap * DPR;
@@ -620,7 +620,7 @@ __global__ __launch_bounds__((NE + ND) * 64) void irw_kernel(
         x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) o[e] = (T)v[e];
-        *reinterpret_cast<x4*>(yr + co) = o;
+        SPEF_KB_YSTORE(*reinterpret_cast<x4*>(yr + co) = o, o);
       }
     }
   }

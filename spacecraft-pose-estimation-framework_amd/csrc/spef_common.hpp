@@ -221,4 +221,19 @@ __device__ unsigned long long* spef_ktrace;
 #define SPEF_TRACE(slot) ((void)0)
 #endif
 
+// Timing ablations of the kernel harness (tools/kbench/ablate.sh; wrong results, never in the library):
+// SPEF_KBENCH_NO_XLOAD points every input-tile load of the fused blocks at the image's first pixels (the same
+// instructions, served from L2: no HBM input traffic); SPEF_KBENCH_NO_YSTORE drops the output stores of the fused
+// blocks and the front kernel (values kept live).
+#ifdef SPEF_KBENCH_NO_XLOAD
+#define SPEF_KB_XOFF(off) ((size_t)0 * (off))
+#else
+#define SPEF_KB_XOFF(off) (off)
+#endif
+#ifdef SPEF_KBENCH_NO_YSTORE
+#define SPEF_KB_YSTORE(store, v) asm volatile("" ::"v"(v))
+#else
+#define SPEF_KB_YSTORE(store, v) store
+#endif
+
 }  // namespace spef

@@ -7,6 +7,8 @@ F="-O3 -std=c++17 --offload-arch=gfx950 -fno-honor-nans -fno-slp-vectorize -mllv
 for v in "$@"; do
   case $v in
     base) D="" ;;
+    no_xload|no_ystore) D="-DSPEF_KBENCH_${v^^}" ;;
+    no_mem) D="-DSPEF_KBENCH_NO_XLOAD -DSPEF_KBENCH_NO_YSTORE" ;;
     *) D="-DSPEF_KBENCH_IRW_${v^^}" ;;
   esac
   /opt/rocm/bin/hipcc $F $D tools/kbench/blk_trace.hip -o tools/kbench/abl/blk_$v &

@@ -5,12 +5,14 @@
 //   hipcc -O3 -std=c++17 --offload-arch=gfx950 -fno-honor-nans -fno-slp-vectorize -mllvm -amdgpu-mfma-vgpr-form \
 //     -I include -I spacecraft-pose-estimation-framework_amd/csrc tools/kbench/blk_trace.hip -o tools/kbench/blk_trace
 //   ./tools/kbench/blk_trace irb|irw|irp CIN HID COUT STRIDE RES H W [B=64] [variant=0] [iters=50] [xscale=2]
+//   ./tools/kbench/blk_trace front 3 32 16 2 0 H W [B=64] ...   (fp16 stem + block 1 on uint8 frames; timing only)
 #ifndef SPEF_KBENCH_TIMING_ONLY   // -DSPEF_KBENCH_TIMING_ONLY: same harness, probes compiled out (timing only)
 #define SPEF_KTRACE
 #endif
 #include "k_irb.hip"
 #include "k_irp.hip"
 #include "k_irw.hip"
+#include "k_front.hip"
 
 
 #include <algorithm>
@@ -53,8 +55,8 @@ int main(int argc, char** argv) {
     fprintf(stderr, "usage: %s irb|irw|irp CIN HID COUT STRIDE RES H W [B] [variant] [iters] [xscale]\n", argv[0]);
     return 2;
   }
-  const bool irp = argv[1][2] == 'p', irb = argv[1][2] == 'b';
-  const char* kname = irb ? "irb" : irp ? "irp" : "irw";
+  const bool irp = argv[1][2] == 'p', irb = argv[1][2] == 'b', front = argv[1][0] == 'f';
+  const char* kname = front ? "front" : irb ? "irb" : irp ? "irp" : "irw";
   ++argv;
   --argc;
   const int cin = atoi(argv[1]), hid = atoi(argv[2]), cout = atoi(argv[3]), st = atoi(argv[4]);
@@ -88,7 +90,9 @@ int main(int argc, char** argv) {
   hipStream_t s;
   CK(hipStreamCreate(&s));
   auto go = [&]() {
-    if (irb)
+    if (front)
+      CK(launch_front(DT_F16, x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s));
+    else if (irb)
       CK(launch_irb(variant, DT_F16, cin, hid, cout, st, true, res, x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, s));
     else
       CK((irp ? launch_irp : launch_irw)(variant, DT_F16, cin, hid, cout, st, res, x, we, be, wd, bd, wp, bp, y, B, H,
@@ -106,6 +110,10 @@ int main(int argc, char** argv) {
   CK(hipEventElapsedTime(&ms, e0, e1));
   const double us = 1e3 * ms / iters;
 
+  if (front) {   // no probes in the front kernel
+    printf("%s avg launch %.2f us (%d iters)\n", kname, us, iters);
+    return 0;
+  }
 #ifndef SPEF_KTRACE
   printf("%s avg launch %.2f us (%d iters, no probes)\n", kname, us, iters);
   return 0;

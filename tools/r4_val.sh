@@ -5,7 +5,7 @@ bash tools/x2run.sh || exit $?
 timeout -k 10 400 python -u -m pytest tests/test_gpu_c2_precision.py -m gpu -x -q -s --timeout 200 --timeout-method thread > gpurun_out/c2.log 2>&1; rc=$?
 grep -E "^C2|passed|failed" gpurun_out/c2.log
 [ $rc -eq 0 ] || exit $rc
-if [ -x kbrun/blk_base ]; then
+if false; then
   for pass in 1 2; do
     for v in base no_wload; do
       for g in "irp 160 960 160 1 1 16 16" "irp 96 576 160 2 0 32 32" "irp 160 960 320 1 0 16 16"; do
@@ -14,3 +14,4 @@ if [ -x kbrun/blk_base ]; then
     done
   done
 fi
+bash tools/r4_abl.sh
