@@ -717,6 +717,11 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 2, 1)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 4, 2)   /* 17 */
+// Smaller tiles for maps whose primary tiling leaves CUs idle (fewer workgroups than the 256 CUs; the role-split
+// kernels run one workgroup per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64).
+#define SPEF_X2_SMALL_TABLE(X)                                   \
+  X(160, 960, 160, 1, true, true, 4, 8, 8, 2, 1)    /* 15-16 */  \
+  X(160, 960, 320, 1, true, false, 4, 8, 8, 4, 2)   /* 17 */
 
 template <typename K>
 static hipError_t x2_set_lds(K k, int lds) {   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
@@ -770,6 +775,26 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
                          int B, int H, int W, int OH, int OW, hipStream_t s) {
   if (!x || !y || !wd || !bd || !wp || !bp || (expand && (!we || !be))) return hipErrorInvalidValue;
+  int num_cu = 0;
+  {
+    static int cus = 0;   // (first call per process; the library runs on one device type)
+    if (!cus) {
+      int dev = 0;
+      if (hipGetDevice(&dev) != hipSuccess ||
+          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        cus = 256;
+    }
+    num_cu = cus;
+  }
+#define SPEF_X2_TILES(TH_, TW_) ((int64_t)((OW + (TW_)-1) / (TW_)) * ((OH + (TH_)-1) / (TH_)) * B)
+#define SPEF_X2_SMALL(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                        \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS &&                    \
+      SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) <= num_cu)                                      \
+    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, \
+                                                                     s);
+  SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
+#undef SPEF_X2_SMALL
+#undef SPEF_X2_TILES
 #define SPEF_X2_CASE(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                         \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                      \
     return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, \

@@ -14,4 +14,5 @@ if false; then
     done
   done
 fi
-bash tools/r4_abl.sh
+bash tools/r4_abl.sh && \
+bash tools/x2_ab.sh A B C D
