@@ -704,6 +704,12 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
 // (mobilenet_v2.py:240-249). kind 0: slab kernel with `waves` waves (tiles keep the hi / lo input tile + fp32 slab at
 // 2+ workgroups per CU where the geometry allows); kind 1: role-split kernel (4 + 4 waves) with the project weights
 // staged in LDS; kind 2: role-split, project weights from L2 (block 17: no two depthwise waves share a channel tile).
+// Cout groups: with g groups the depthwise waves split into g sets that each run the whole depthwise for their pixels
+// and project onto 1/g of the output channels, so g > 1 computes the depthwise g times. Interleaved A/B at B = 64
+// (tools/x2_ab.sh, per launch): blocks 8-10 81 -> 54 us and block 11 84 -> 59 us with g 2 -> 1; blocks 12-13 158
+// (8x8, g 2) -> 125 (8x16, g 2) -> 89 us (8x16, g 1); blocks 15-16 93 -> 91 us (g 2 -> 1); block 17 142 us at g 4,
+// 125 at g 2, 322 at g 1 (80 accumulator registers per wave: spills). URSONet step 2.11 -> 1.85 ms, keypoint mode
+// 1.27 -> 1.05 ms (with the small-map table below).
 #define SPEF_X2_TABLE(X)                                         \
   X(32, 32, 16, 1, false, false, 8, 16, 4, 1, 0)    /* 1 */      \
   X(16, 96, 24, 2, true, false, 8, 8, 4, 1, 0)      /* 2 */      \
@@ -711,12 +717,12 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   X(24, 144, 32, 2, true, false, 8, 8, 4, 1, 0)     /* 4 */      \
   X(32, 192, 32, 1, true, true, 8, 16, 4, 1, 0)     /* 5-6 */    \
   X(32, 192, 64, 2, true, false, 8, 8, 4, 1, 0)     /* 7 */      \
-  X(64, 384, 64, 1, true, true, 8, 16, 8, 2, 1)     /* 8-10 */   \
-  X(64, 384, 96, 1, true, false, 8, 16, 8, 2, 1)    /* 11 */     \
-  X(96, 576, 96, 1, true, true, 8, 8, 8, 2, 1)      /* 12-13 */  \
+  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, 1)     /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, 1)    /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, 1)     /* 12-13 */  \
   X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
-  X(160, 960, 160, 1, true, true, 8, 8, 8, 2, 1)    /* 15-16 */  \
-  X(160, 960, 320, 1, true, false, 8, 8, 8, 4, 2)   /* 17 */
+  X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1)    /* 15-16 */  \
+  X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
 // Smaller tiles for maps whose primary tiling leaves CUs idle (fewer workgroups than the 256 CUs; the role-split
 // kernels run one workgroup per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64).
 #define SPEF_X2_SMALL_TABLE(X)                                   \
