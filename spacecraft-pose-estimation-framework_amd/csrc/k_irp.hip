@@ -25,6 +25,10 @@
 
 namespace spef {
 
+#ifndef SPEF_IRP_EARLY
+#define SPEF_IRP_EARLY 1
+#endif
+
 template <int CIN, int HID, int COUT, int S, int TH, int TW, int NM, int NV, int DWB>
 struct IrpGeom {
   static constexpr int NW = NM + NV;
@@ -205,7 +209,10 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
             bx[jj][ks] = *reinterpret_cast<const x8*>(Xs + (pt * 16 + r16) * G::XS + 32 * ks + 8 * kg);
       }
     };
-    auto step = [&](int ce, int cp, bool do_e, bool do_p) {
+    // ld_e / ld_p >= 0: the next expand / project fragments (chunks ld_e / ld_p) are issued inside the step, right after
+    // the MFMAs that read the current ones, so their L2 latency overlaps the rest of the step and the barrier wait
+    // (issued after the step, only the barrier wait covered it; the MFMA waves are the critical role).
+    auto step = [&](int ce, int cp, bool do_e, bool do_p, int ld_e, int ld_p) {
       x8 bq[G::POUT16];
       if (!G::BXR && do_e) read_bx();
       if (do_p) {
@@ -224,6 +231,7 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
           for (int jj = 0; jj < G::EPT; ++jj)
             if (eg + G::NG * jj < G::PIN16) e[jj] = DT::mfma(ea[ks], bx[jj][ks], e[jj]);
       }
+      if (SPEF_IRP_EARLY && ld_e >= 0) load_ea(ld_e);
       if (do_p) {
 #pragma unroll
         for (int q = 0; q < G::POUT16; ++q)
@@ -231,6 +239,7 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
           for (int t = 0; t < G::NCTW; ++t)
             if (wave + NM * t < G::NCT) acc[q][t] = DT::mfma(pa[t], bq[q], acc[q][t]);   // wave-uniform
       }
+      if (SPEF_IRP_EARLY && ld_p >= 0) load_pa(ld_p);
       if (do_e) {
         T* Ew = Es0 + (ce & 1) * G::PINP * G::ES;
 #pragma unroll
@@ -256,34 +265,36 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
     SPEF_TRACE(3);
     __builtin_amdgcn_s_waitcnt(0x0F70);                // vmcnt(0): no load in flight across the role loop's header
     if (G::BXR) read_bx();
-    step(0, 0, true, false);
-    load_ea(1);
+    step(0, 0, true, false, SPEF_IRP_EARLY ? 1 : -1, -1);
+    if (!SPEF_IRP_EARLY) load_ea(1);
     SPEF_TRACE(4);
     __syncthreads();                                   // B1: Es[0] complete
     SPEF_TRACE(5);
     // iteration 0: E(1) while the depthwise waves run V(0)
-    step(1, 0, true, false);
-    load_ea(2);
+    step(1, 0, true, false, SPEF_IRP_EARLY ? 2 : -1, -1);
+    if (!SPEF_IRP_EARLY) load_ea(2);
     SPEF_TRACE(6);
     __syncthreads();
     SPEF_TRACE(7);
     // iterations 1 .. NCH-2: E(i+1) and P(i-1)
 #pragma unroll 1
     for (int i = 1; i + 1 < G::NCH; ++i) {
-      step(i + 1, i - 1, true, true);
-      load_ea(i + 2);
-      load_pa(i);
+      step(i + 1, i - 1, true, true, SPEF_IRP_EARLY ? i + 2 : -1, SPEF_IRP_EARLY ? i : -1);
+      if (!SPEF_IRP_EARLY) {
+        load_ea(i + 2);
+        load_pa(i);
+      }
       SPEF_TRACE(6 + 2 * i);
       __syncthreads();
       SPEF_TRACE(7 + 2 * i);
     }
     // iteration NCH-1: P(NCH-2); iteration NCH: P(NCH-1)
-    step(0, G::NCH - 2, false, true);
-    load_pa(G::NCH - 1);
+    step(0, G::NCH - 2, false, true, -1, SPEF_IRP_EARLY ? G::NCH - 1 : -1);
+    if (!SPEF_IRP_EARLY) load_pa(G::NCH - 1);
     SPEF_TRACE(6 + 2 * (G::NCH - 1));
     __syncthreads();
     SPEF_TRACE(7 + 2 * (G::NCH - 1));
-    step(0, G::NCH - 1, false, true);
+    step(0, G::NCH - 1, false, true, -1, -1);
 
     // ---- epilogue: + residual from the staged input tile -> y (NHWC)
 #pragma unroll

@@ -541,15 +541,23 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
           q_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, op.expand != 1)) {
         void* y = pick({x});
         const std::array<int64_t, 3>& r3 = c->q8_res[&op - c->ops.data()];
+        // role-split form for blocks 8-16 unless SPEF_OPT_WAVESPEC = 0 (bit-identical either way)
+        const bool qw = c->wavespec && op.expand != 1 &&
+                        q_irw_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res);
         char key[96];
-        snprintf(key, sizeof(key), "q_irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
+        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", qw ? "q_irw_kernel" : "q_irb_kernel", op.cin, op.hidden,
+                 op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, (double)M * op.cin + (double)M2 * op.cout + (double)op.hidden * (op.cin + op.cout + 9),
                             2.0 * M * op.cin * op.hidden + 18.0 * M2 * op.hidden + 2.0 * M2 * op.hidden * op.cout, [&] {
+          const QBits qb{qbits(op, 0), qbits(op, 1), qbits(op, 2)};
+          if (qw)
+            return launch_q_irw((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, (op.flags & 4u) != 0,
+                                (const int8_t*)x, ptr<int8_t>(c, op.w0), ptr<int8_t>(c, op.w2), ptr<int32_t>(c, op.x0),
+                                ptr<uint8_t>(c, op.x2), r3[0], r3[1], (int)r3[2], qb, (int8_t*)y, B, h, w, OH, OW, s);
           return launch_q_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, op.expand != 1,
                               (op.flags & 4u) != 0, (const int8_t*)x,
                               ptr<int8_t>(c, op.w0), ptr<int8_t>(c, op.w2), ptr<int32_t>(c, op.x0),
-                              ptr<uint8_t>(c, op.x2), r3[0], r3[1], (int)r3[2],
-                              QBits{qbits(op, 0), qbits(op, 1), qbits(op, 2)}, (int8_t*)y, B, h, w, OH, OW, s);
+                              ptr<uint8_t>(c, op.x2), r3[0], r3[1], (int)r3[2], qb, (int8_t*)y, B, h, w, OH, OW, s);
         }));
         cur = y;
         h = OH;

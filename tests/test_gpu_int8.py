@@ -54,6 +54,24 @@ def test_int8_head_outputs_bit_exact(q8, b, h, w):
     np.testing.assert_array_equal(p.cpu().numpy(), rp)
 
 
+@pytest.mark.parametrize('b,h,w', [(2, 64, 64), (1, 100, 136), (2, 512, 512)])
+def test_int8_role_split_blocks_bit_identical_to_slab(q8, b, h, w):
+    """Blocks 8-16 run the role-split kernel (k_q8irw.hip) by default; SPEF_OPT_WAVESPEC 0 selects the slab kernel
+    (k_q8irb.hip). Every late-block output is bit-identical (ragged maps included)."""
+    from spef_amd import _lib as L
+    eng, sd, qp = q8
+    x = torch.from_numpy(synth_frames(b, h, w, 21)).cuda()
+    try:
+        for op in range(8, 18):
+            outs = []
+            for mode in (2, 0):
+                eng.set_option(L.OPT_WAVESPEC, mode)
+                outs.append(eng.probe(x, op).cpu().numpy())
+            np.testing.assert_array_equal(outs[0], outs[1], err_msg=f'op {op}')
+    finally:
+        eng.set_option(L.OPT_WAVESPEC, 2)
+
+
 def test_int8_f32_input_matches_u8(q8):
     """NCHW float32 [0,1] input (the reference `images['torch']`) quantises to the same codes as the u8 LUT."""
     eng, sd, qp = q8

@@ -9,6 +9,7 @@ for v in "$@"; do
     base) D="" ;;
     no_xload|no_ystore) D="-DSPEF_KBENCH_${v^^}" ;;
     no_mem) D="-DSPEF_KBENCH_NO_XLOAD -DSPEF_KBENCH_NO_YSTORE" ;;
+    irp_late) D="-DSPEF_IRP_EARLY=0" ;;
     *) D="-DSPEF_KBENCH_IRW_${v^^}" ;;
   esac
   /opt/rocm/bin/hipcc $F $D tools/kbench/blk_trace.hip -o tools/kbench/abl/blk_$v &

@@ -1,0 +1,11 @@
+# irp fragment-load placement A/B (kbrun/ binaries from tools/kbench/ablate.sh base irp_late no_wload)
+R=${GRAFT_REPO_ROOT:-$(pwd)}
+cd $R
+for pass in 1 2 3; do
+  for g in "irp 96 576 160 2 0 32 32" "irp 160 960 160 1 1 16 16" "irp 160 960 320 1 0 16 16"; do
+    L="base irp_late no_wload"; [ $pass = 2 ] && L="no_wload irp_late base"
+    for v in $L; do
+      printf "%-9s %-28s " $v "$g"; timeout -k 5 60 ./kbrun/blk_$v $g || exit $?
+    done
+  done
+done

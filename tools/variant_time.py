@@ -1,5 +1,5 @@
 """Per-kernel timing of one precision variant (GPU box): python tools/variant_time.py [dtype] [head] [B].
-dtype fp16 | bf16 | fp32 | fp16x2; head ursonet (512x512) | keypoints (240x384, forward + sigmoid + EPnP)."""
+dtype fp16 | bf16 | fp32 | fp16x2 | int8 (URSONet only); head ursonet (512x512) | keypoints (240x384, forward + sigmoid + EPnP)."""
 import os
 import sys
 import time
@@ -27,7 +27,14 @@ def main():
     else:
         arch, (H, W) = mobilenet_v2('ursonet', 1728, 3), (512, 512)
         sd = synthetic_state_dict(arch, seed=1001)
-    eng = Engine(Bl.pack(sd, arch, dtype=dt), 'cuda:0')
+    if dt == 'int8':   # the C5 path, scales calibrated on random frames (timing only)
+        from spef_amd.blob_q8 import pack_int8
+        from spef_amd.quant import calibrate
+        cal = np.random.Generator(np.random.PCG64(9)).integers(0, 256, (4, 128, 128, 3), dtype=np.uint8)
+        blob = pack_int8(sd, calibrate(sd, cal))
+    else:
+        blob = Bl.pack(sd, arch, dtype=dt)
+    eng = Engine(blob, 'cuda:0')
     if head == 'keypoints':
         g = np.load(os.path.join(ROOT, 'tests', 'golden', 'keypoints.npz'))
         eng.set_keypoints(g['kp3d'], g['K'], float(g['nu']), float(g['nv']))
