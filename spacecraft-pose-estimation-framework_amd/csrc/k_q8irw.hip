@@ -1,5 +1,5 @@
 // Role-split fused INT8 inverted-residual block (QInvertedResidual, src/modeling/common/brevitas_layers.py:57-136)
-// for the low-resolution MobileNet-V2 blocks 8-16 (32x32 and 16x16 maps, 384-960 hidden channels). Integer
+// for the low-resolution MobileNet-V2 blocks 8-17 (32x32 and 16x16 maps, 384-960 hidden channels). Integer
 // semantics of oracle/int8_ref.py, identical to the slab kernel (k_q8irb.hip) and the unfused k_q8.hip kernels.
 //
 // The slab kernel runs expand, barrier, depthwise + project on every wave in lock step, with every wave fetching the
@@ -385,13 +385,18 @@ hipError_t q_irw_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
   return hipGetLastError();
 }
 
-// (cin, hidden, cout, stride, TH, TW, residual, expand waves, depthwise waves): MobileNet-V2 blocks 8-16
+// (cin, hidden, cout, stride, TH, TW, residual, expand waves, depthwise waves): MobileNet-V2 blocks 8-17.
+// Interleaved A/B against the slab kernel (tools/i8_ab.sh, per launch at B = 64): blocks 8-10 34.3 -> 32.8 us,
+// block 11 38.1 -> 35.5, blocks 12-13 56.1 -> 49.8, block 14 46.8 -> 33.8, blocks 15-16 57.8 -> 47.6, block 17 73.8 ->
+// 70.2; int8 kernel sum 1.28 -> 1.22 ms. 8x16 tiles for blocks 8-13 (512 workgroups; 134-170 VGPRs, so still one
+// workgroup per CU): +3 to +5 us per launch.
 #define SPEF_QIRW_TABLE(X)                                                  \
   X(64, 384, 64, 1, 16, 16, true, 4, 4)       /* blocks 8-10  */           \
   X(64, 384, 96, 1, 16, 16, false, 4, 4)      /* block 11     */           \
   X(96, 576, 96, 1, 16, 16, true, 4, 4)       /* blocks 12-13 */           \
   X(96, 576, 160, 2, 8, 8, false, 4, 4)       /* block 14     */           \
-  X(160, 960, 160, 1, 8, 8, true, 4, 4)       /* blocks 15-16 */
+  X(160, 960, 160, 1, 8, 8, true, 4, 4)       /* blocks 15-16 */ \
+  X(160, 960, 320, 1, 8, 8, false, 4, 4)      /* block 17     */
 
 }  // namespace
 

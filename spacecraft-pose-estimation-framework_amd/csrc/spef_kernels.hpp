@@ -173,7 +173,7 @@ struct QBits {
 hipError_t launch_q_irb(int cin, int hid, int cout, int stride, bool res, bool expand, bool sh32, const int8_t* x, const int8_t* we,
                         const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm, int64_t rb, int rs,
                         QBits qb, int8_t* y, int B, int H, int W, int OH, int OW, hipStream_t s);
-// Role-split form of the same block for MobileNet-V2 blocks 8-16 (k_q8irw.hip; bit-identical, same arguments).
+// Role-split form of the same block for MobileNet-V2 blocks 8-17 (k_q8irw.hip; bit-identical, same arguments).
 bool q_irw_supported(int cin, int hid, int cout, int stride, bool res);
 hipError_t launch_q_irw(int cin, int hid, int cout, int stride, bool res, bool sh32, const int8_t* x, const int8_t* we,
                         const int8_t* wp, const int32_t* pinit, const uint8_t* tabs, int64_t rm, int64_t rb, int rs,

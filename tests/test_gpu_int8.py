@@ -56,7 +56,7 @@ def test_int8_head_outputs_bit_exact(q8, b, h, w):
 
 @pytest.mark.parametrize('b,h,w', [(2, 64, 64), (1, 100, 136), (2, 512, 512)])
 def test_int8_role_split_blocks_bit_identical_to_slab(q8, b, h, w):
-    """Blocks 8-16 run the role-split kernel (k_q8irw.hip) by default; SPEF_OPT_WAVESPEC 0 selects the slab kernel
+    """Blocks 8-17 run the role-split kernel (k_q8irw.hip) by default; SPEF_OPT_WAVESPEC 0 selects the slab kernel
     (k_q8irb.hip). Every late-block output is bit-identical (ragged maps included)."""
     from spef_amd import _lib as L
     eng, sd, qp = q8
