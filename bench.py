@@ -269,6 +269,15 @@ def run_int8(args, sd, dev, frames, ref, peaks=None):
     return run_variant(args, blob, 'int8', dev, frames, ref, peaks)
 
 
+def set_wavespec(pipe, args) -> None:
+    """--wavespec / --q8-rolesplit: the late-block schedule of every engine in the pipeline (A/B aids)."""
+    from spef_amd import _lib as L
+    for opt, val in ((L.OPT_WAVESPEC, args.wavespec), (L.OPT_Q8_ROLESPLIT, args.q8_rolesplit)):
+        if val is not None:
+            for e in pipe.engines:
+                e.set_option(opt, val)
+
+
 def run_variant(args, blob, dtype, dev, frames, ref, peaks=None):
     """A precision variant's sub-record at the headline workload and timing protocol (N=1): int8 (C5) or fp16x2
     (the fp32-accurate split-fp16 schedule)."""
@@ -278,6 +287,7 @@ def run_variant(args, blob, dtype, dev, frames, ref, peaks=None):
     from spef_amd.spe.spe_utils import SPEUtils
     su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
     pipe = StreamPipeline(blob, dev, depth=max(1, args.inflight), ori_bins=su.orientation.histogram)
+    set_wavespec(pipe, args)
     B, S = args.batch, args.size
     pipe.reserve(B, S, S)
 
@@ -440,6 +450,12 @@ def main():
     ap.add_argument('--size', type=int, default=512)
     ap.add_argument('--dtype', default='fp16', choices=['fp16', 'bf16', 'int8'],
                     help='int8 = the Brevitas-mirroring C5 path (calibrated activation scales) as the headline')
+    ap.add_argument('--wavespec', type=int, default=None,
+                    help='late-block schedule (SPEF_OPT_WAVESPEC): 0 slab kernels, 1 wave-specialised, 2 three-stage '
+                         '(fp16 blocks 14-17; A/B aid; default: the library\'s)')
+    ap.add_argument('--q8-rolesplit', type=int, default=None,
+                    help='int8 blocks 8-17 as role-split kernels (SPEF_OPT_Q8_ROLESPLIT 1) or slab kernels (0, the '
+                         'library default)')
     ap.add_argument('--inflight', type=int, default=3,
                     help='batches in flight: consecutive steps alternate over this many HIP streams (spef_amd.pipeline)')
     ap.add_argument('--frame-buffers', type=int, default=6,
@@ -520,6 +536,7 @@ def main():
             comm = RcclComm(dev)
         su = SPEUtils(None, 'classification', 12, 3, False, 'regression')
         pipe = StreamPipeline(blob, dev, depth=max(1, args.inflight), ori_bins=su.orientation.histogram, comm=comm)
+        set_wavespec(pipe, args)
         eng = pipe.engine
         frames = device_batches(stop - first, S, first, max(1, args.frame_buffers), dev)
         pipe.reserve(B, S, S)

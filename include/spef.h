@@ -132,10 +132,14 @@ int spef_preprocess(spef_ctx* ctx, const uint8_t* frames, int B, int Hin, int Wi
  * SPEF_OPT_WAVESPEC (default 2): role-split fused kernels for the low-resolution blocks. 2 = three-stage pipeline
  *   (MFMA waves expand + project, VALU waves depthwise); 1 = two-stage (expand waves, depthwise + project waves);
  *   0 = LDS-slab fused kernels everywhere.
+ * SPEF_OPT_Q8_ROLESPLIT (default 0): int8 blobs run blocks 8-17 as role-split kernels (expand waves vs depthwise +
+ *   project waves) instead of the LDS-slab kernels: faster with one batch in flight, slower when several batches
+ *   share the GPU (the role-split workgroups hold a CU's LDS; DESIGN.md section 3, INT8 path).
  * (Kernel-tuning knobs used by the sweep tools are internal: csrc/spef_tuning.hpp.) */
 enum spef_option {
   SPEF_OPT_FUSE_BLOCKS = 1,
-  SPEF_OPT_WAVESPEC = 6
+  SPEF_OPT_WAVESPEC = 6,
+  SPEF_OPT_Q8_ROLESPLIT = 7
 };
 int spef_set_option(spef_ctx* ctx, int option, int value);
 

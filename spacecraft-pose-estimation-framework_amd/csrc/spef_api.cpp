@@ -76,6 +76,7 @@ struct spef_ctx {
   int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
   int irb_variant = 0;       // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps)
   int wavespec = 2;          // SPEF_OPT_WAVESPEC: 2 = pipelined (k_irp.hip), 1 = wave-specialised (k_irw.hip)
+  int q8_rolesplit = 0;      // SPEF_OPT_Q8_ROLESPLIT: int8 blocks 8-17 role-split (k_q8irw.hip)
   int test_fail_bcast = 0;   // SPEF_OPT_TEST_FAIL_BCAST (spef_tuning.hpp): failure injection in spef_bcast_weights
   // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
   std::vector<double> q8_sw, q8_bias;
@@ -541,8 +542,8 @@ int run_backbone_q8(spef_ctx* c, const void* input, int layout, int B, int H, in
           q_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, op.expand != 1)) {
         void* y = pick({x});
         const std::array<int64_t, 3>& r3 = c->q8_res[&op - c->ops.data()];
-        // role-split form for blocks 8-16 unless SPEF_OPT_WAVESPEC = 0 (bit-identical either way)
-        const bool qw = c->wavespec && op.expand != 1 &&
+        // role-split form for blocks 8-17 with SPEF_OPT_Q8_ROLESPLIT (bit-identical either way)
+        const bool qw = c->q8_rolesplit && op.expand != 1 &&
                         q_irw_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res);
         char key[96];
         snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", qw ? "q_irw_kernel" : "q_irb_kernel", op.cin, op.hidden,
@@ -1684,6 +1685,11 @@ int spef_set_option(spef_ctx* c, int option, int value) {
   }
   if (option == SPEF_OPT_PW_GEMM) {
     c->gemm = value != 0;
+    return SPEF_OK;
+  }
+  if (option == SPEF_OPT_Q8_ROLESPLIT) {
+    if (value < 0 || value > 1) return fail(SPEF_ERR_ARG, "SPEF_OPT_Q8_ROLESPLIT: 0 or 1");
+    c->q8_rolesplit = value;
     return SPEF_OK;
   }
   if (option == SPEF_OPT_WAVESPEC) {

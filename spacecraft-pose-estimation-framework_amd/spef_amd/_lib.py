@@ -14,7 +14,7 @@ IN_U8_NHWC, IN_F32_NCHW = 0, 1
 REGRESSION, CLASSIFICATION, KEYPOINTS = 0, 1, 2
 ABI_VERSION = 3
 COMM_ID_BYTES = 128
-OPT_FUSE_BLOCKS, OPT_WAVESPEC = 1, 6                          # public schedule options (include/spef.h)
+OPT_FUSE_BLOCKS, OPT_WAVESPEC, OPT_Q8_ROLESPLIT = 1, 6, 7     # public schedule options (include/spef.h)
 OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT, OPT_TEST_FAIL_BCAST = 2, 3, 4, 5   # internal (csrc/spef_tuning.hpp)
 
 # name -> (restype, argtypes); keep in sync with include/spef.h (tests/test_abi.py checks the header)

@@ -56,7 +56,7 @@ def test_int8_head_outputs_bit_exact(q8, b, h, w):
 
 @pytest.mark.parametrize('b,h,w', [(2, 64, 64), (1, 100, 136), (2, 512, 512)])
 def test_int8_role_split_blocks_bit_identical_to_slab(q8, b, h, w):
-    """Blocks 8-17 run the role-split kernel (k_q8irw.hip) by default; SPEF_OPT_WAVESPEC 0 selects the slab kernel
+    """SPEF_OPT_Q8_ROLESPLIT 1 runs blocks 8-17 as role-split kernels (k_q8irw.hip), 0 (default) as slab kernels
     (k_q8irb.hip). Every late-block output is bit-identical (ragged maps included)."""
     from spef_amd import _lib as L
     eng, sd, qp = q8
@@ -64,12 +64,12 @@ def test_int8_role_split_blocks_bit_identical_to_slab(q8, b, h, w):
     try:
         for op in range(8, 18):
             outs = []
-            for mode in (2, 0):
-                eng.set_option(L.OPT_WAVESPEC, mode)
+            for mode in (1, 0):
+                eng.set_option(L.OPT_Q8_ROLESPLIT, mode)
                 outs.append(eng.probe(x, op).cpu().numpy())
             np.testing.assert_array_equal(outs[0], outs[1], err_msg=f'op {op}')
     finally:
-        eng.set_option(L.OPT_WAVESPEC, 2)
+        eng.set_option(L.OPT_Q8_ROLESPLIT, 0)
 
 
 def test_int8_f32_input_matches_u8(q8):
@@ -100,10 +100,13 @@ def test_int8_general_shift_kernels_bit_exact(q8):
     fr = synth_frames(2, 96, 64, 13)
     e = Engine(pack_int8(sd, qp, shift32=False), 'cuda:0')
     try:
-        o, p = e.forward(torch.from_numpy(fr).cuda())
         ro, rp = Q.int8_forward(fr, sd, qp)
-        np.testing.assert_array_equal(o.cpu().numpy(), ro)
-        np.testing.assert_array_equal(p.cpu().numpy(), rp)
+        from spef_amd import _lib as L
+        for rolesplit in (0, 1):   # slab and role-split late blocks, general-shift requant
+            e.set_option(L.OPT_Q8_ROLESPLIT, rolesplit)
+            o, p = e.forward(torch.from_numpy(fr).cuda())
+            np.testing.assert_array_equal(o.cpu().numpy(), ro)
+            np.testing.assert_array_equal(p.cpu().numpy(), rp)
     finally:
         e.close()
 
@@ -154,11 +157,17 @@ def test_low_bit_head_outputs_bit_exact(q8low):
     np.testing.assert_array_equal(of.cpu().numpy(), ro)
     np.testing.assert_array_equal(pf.cpu().numpy(), rp)
     e = Engine(pack_int8(sd, qp, shift32=False), 'cuda:0')
+    from spef_amd import _lib as L
     try:
-        o2, p2 = e.forward(torch.from_numpy(fr).cuda())
-        np.testing.assert_array_equal(o2.cpu().numpy(), ro)
-        np.testing.assert_array_equal(p2.cpu().numpy(), rp)
+        for rolesplit in (0, 1):   # low-bit quantizers through the role-split late blocks as well
+            e.set_option(L.OPT_Q8_ROLESPLIT, rolesplit)
+            eng.set_option(L.OPT_Q8_ROLESPLIT, rolesplit)
+            for en in (e, eng):
+                o2, p2 = en.forward(torch.from_numpy(fr).cuda())
+                np.testing.assert_array_equal(o2.cpu().numpy(), ro)
+                np.testing.assert_array_equal(p2.cpu().numpy(), rp)
     finally:
+        eng.set_option(L.OPT_Q8_ROLESPLIT, 0)
         e.close()
 
 
