@@ -229,28 +229,29 @@ static int measure_peaks_on(int device, int reps, double* out) {
   }
   const size_t n16 = hbm_bytes / 16;
   double best_copy = 0.0, best_read = 0.0, cfg_copy = 0.0, cfg_read = 0.0;
-  for (int wpc : {4, 8, 16}) {          // workgroups (of 4 waves) per CU
+  for (int wpc : {4, 8, 16, 0}) {       // workgroups (of 4 waves) per CU; 0: one workgroup per block (no grid stride)
     for (int ui = 0; ui < 4; ++ui) {    // (loads in flight, nontemporal)
       const int U = ui < 2 ? 4 : 8;
       const bool nt = ui & 1;
       const double cfg = wpc * 100 + U * 10 + (nt ? 1 : 0);
+      const size_t grid = wpc ? (size_t)cus * wpc : n16 / (256 * (size_t)U);
       auto copy = [&] {
         const u32x4* a = (const u32x4*)sc.p[3];
         u32x4* d = (u32x4*)sc.p[4];
-        if (ui == 0) hbm_copy_kernel<4, false><<<cus * wpc, 256>>>(a, d, n16);
-        else if (ui == 1) hbm_copy_kernel<4, true><<<cus * wpc, 256>>>(a, d, n16);
-        else if (ui == 2) hbm_copy_kernel<8, false><<<cus * wpc, 256>>>(a, d, n16);
-        else hbm_copy_kernel<8, true><<<cus * wpc, 256>>>(a, d, n16);
+        if (ui == 0) hbm_copy_kernel<4, false><<<grid, 256>>>(a, d, n16);
+        else if (ui == 1) hbm_copy_kernel<4, true><<<grid, 256>>>(a, d, n16);
+        else if (ui == 2) hbm_copy_kernel<8, false><<<grid, 256>>>(a, d, n16);
+        else hbm_copy_kernel<8, true><<<grid, 256>>>(a, d, n16);
       };
       auto read = [&] {
         const u32x4* a = (const u32x4*)sc.p[4];
         uint32_t* k = (uint32_t*)sc.p[1];
-        if (ui == 0) hbm_read_kernel<4, false><<<cus * wpc, 256>>>(a, n16, k);
-        else if (ui == 1) hbm_read_kernel<4, true><<<cus * wpc, 256>>>(a, n16, k);
-        else if (ui == 2) hbm_read_kernel<8, false><<<cus * wpc, 256>>>(a, n16, k);
-        else hbm_read_kernel<8, true><<<cus * wpc, 256>>>(a, n16, k);
+        if (ui == 0) hbm_read_kernel<4, false><<<grid, 256>>>(a, n16, k);
+        else if (ui == 1) hbm_read_kernel<4, true><<<grid, 256>>>(a, n16, k);
+        else if (ui == 2) hbm_read_kernel<8, false><<<grid, 256>>>(a, n16, k);
+        else hbm_read_kernel<8, true><<<grid, 256>>>(a, n16, k);
       };
-      for (int r = 0; r < reps + 1; ++r) {
+      for (int r = 0; r < reps + 3; ++r) {   // streams: best of reps + 2 (the copy's spread is a few %)
         float ms = 0.f;
         int rc = time_launch(copy, &ms);
         if (rc) return rc;

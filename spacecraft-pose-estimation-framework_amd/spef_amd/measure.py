@@ -19,15 +19,17 @@ def measure_peaks(device: int = 0, reps: int = 2) -> dict:
 
     def cfg(v):
         v = int(v)
-        return {'workgroups_per_cu': v // 100, 'loads_in_flight_per_thread': (v // 10) % 10, 'nontemporal': bool(v % 10)}
+        return {'workgroups_per_cu': (v // 100) or 'one per 16-32 KiB block (no grid stride)',
+                'loads_in_flight_per_thread': (v // 10) % 10, 'nontemporal': bool(v % 10)}
     return {'fp16_mfma_tflops': round(out[0], 1), 'int8_mfma_tops': round(out[1], 1),
             'hbm_copy_gbs': round(out[2], 1), 'hbm_read_gbs': round(out[3], 1),
             'sclk_mhz_fp16_loop': round(out[4], 1), 'sclk_mhz_int8_loop': round(out[5], 1),
             'hbm_copy_config': cfg(out[6]), 'hbm_read_config': cfg(out[7]),
             'method': 'csrc/k_ubench.hip: best of %d timed launches after a warm-up; MFMA loops on random operands, '
                       '8 chains per wave, 4 waves per SIMD; HBM: 1 GiB buffers (copy counts read + write bytes), '
-                      'contiguous 16-32 KiB blocks per workgroup iteration, best of 4/8/16 workgroups per CU x 4/8 '
-                      '16-B loads in flight per thread x plain/nontemporal' % reps}
+                      'contiguous 16-32 KiB blocks per workgroup iteration, best of %d launches of each of 4/8/16 '
+                      'workgroups per CU or one workgroup per block x 4/8 16-B loads in flight per thread x '
+                      'plain/nontemporal' % (reps, reps + 2)}
 
 
 class ClockProbe:
