@@ -70,6 +70,32 @@ class StreamPipeline:
         dec['event'] = ev
         return dec
 
+    def set_keypoints(self, kp3d: np.ndarray, K: np.ndarray, nu: float, nv: float, dist=None) -> None:
+        for e in self.engines:
+            e.set_keypoints(kp3d, K, nu, nv, dist)
+
+    def submit_keypoints(self, frames: torch.Tensor) -> dict:
+        """Keypoint mode: forward (KeypointRegressionHead) + sigmoid + batched EPnP of one batch on the next stream;
+        returns the decode dict of Engine.decode_keypoints plus 'raw' and 'event' (as submit())."""
+        i = self._next
+        self._next = (i + 1) % self.depth
+        eng, s = self.engines[i], self.streams[i]
+        B = frames.shape[0]
+        buf = self._bufs[i]
+        if buf is None or buf[0].shape[0] != B:
+            buf = (torch.empty((B, eng.n_out0), dtype=torch.float32, device=self.device), None)
+            self._bufs[i] = buf
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            frames.record_stream(s)
+            raw, _ = eng.forward(frames, buf[0])
+            dec = eng.decode_keypoints(raw)
+            ev = torch.cuda.Event()
+            ev.record(s)
+        dec['raw'] = raw
+        dec['event'] = ev
+        return dec
+
     def synchronize(self) -> None:
         for s in self.streams:
             s.synchronize()
