@@ -80,15 +80,10 @@ class StreamPipeline:
         i = self._next
         self._next = (i + 1) % self.depth
         eng, s = self.engines[i], self.streams[i]
-        B = frames.shape[0]
-        buf = self._bufs[i]
-        if buf is None or buf[0].shape[0] != B:
-            buf = (torch.empty((B, eng.n_out0), dtype=torch.float32, device=self.device), None)
-            self._bufs[i] = buf
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             frames.record_stream(s)
-            raw, _ = eng.forward(frames, buf[0])
+            raw, _ = eng.forward(frames)   # allocated on s: every returned tensor belongs to this batch alone
             dec = eng.decode_keypoints(raw)
             ev = torch.cuda.Event()
             ev.record(s)

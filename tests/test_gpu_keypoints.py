@@ -190,3 +190,27 @@ def test_predict_keypoint_mode(kp_engine, golden):
     chk = eng.decode_keypoints(torch.from_numpy(pose['keypoints']).cuda(), apply_sigmoid=False)
     np.testing.assert_array_equal(chk['ori'].cpu().numpy(), pose['ori'])
     np.testing.assert_array_equal(chk['pos'].cpu().numpy(), pose['pos'])
+
+
+def test_stream_pipeline_keypoint_mode_matches_single_engine(kp_sd, golden):
+    """StreamPipeline.submit_keypoints (the bench's keypoint timing path: batches on three streams, each with its own
+    context) gives every batch the same raw outputs, poses and status as one engine on one stream."""
+    from spef_amd.pipeline import StreamPipeline
+    g = golden('keypoints.npz')
+    rng = np.random.Generator(np.random.PCG64(31))
+    batches = [torch.from_numpy(rng.integers(0, 256, (3, 240, 384, 3), dtype=np.uint8)).cuda() for _ in range(4)]
+    pipe = StreamPipeline(Bl.pack(kp_sd, mobilenet_v2('keypoints'), dtype='fp16x2'), 'cuda:0', depth=3)
+    try:
+        pipe.set_keypoints(g['kp3d'], g['K'], float(g['nu']), float(g['nv']))
+        outs = [pipe.submit_keypoints(x) for x in batches]
+        pipe.synchronize()
+        ref = pipe.engines[0]
+        for x, o in zip(batches, outs):
+            raw, _ = ref.forward(x)
+            r = ref.decode_keypoints(raw)
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(o['raw'].cpu().numpy(), raw.cpu().numpy())
+            for k in ('keypoints', 'ori', 'pos', 'status'):
+                np.testing.assert_array_equal(o[k].cpu().numpy(), r[k].cpu().numpy(), err_msg=k)
+    finally:
+        pipe.close()
