@@ -272,7 +272,8 @@ def run_int8(args, sd, dev, frames, ref, peaks=None):
 def set_wavespec(pipe, args) -> None:
     """--wavespec / --q8-rolesplit: the late-block schedule of every engine in the pipeline (A/B aids)."""
     from spef_amd import _lib as L
-    for opt, val in ((L.OPT_WAVESPEC, args.wavespec), (L.OPT_Q8_ROLESPLIT, args.q8_rolesplit)):
+    extra = [tuple(int(v) for v in o.split('=')) for o in args.set_option]
+    for opt, val in [(L.OPT_WAVESPEC, args.wavespec), (L.OPT_Q8_ROLESPLIT, args.q8_rolesplit)] + extra:
         if val is not None:
             for e in pipe.engines:
                 e.set_option(opt, val)
@@ -464,6 +465,9 @@ def main():
     ap.add_argument('--wavespec', type=int, default=None,
                     help='late-block schedule (SPEF_OPT_WAVESPEC): 0 slab kernels, 1 wave-specialised, 2 three-stage '
                          '(fp16 blocks 14-17; A/B aid; default: the library\'s)')
+    ap.add_argument('--set-option', action='append', default=[], metavar='OPT=VALUE',
+                    help='spef_set_option(OPT, VALUE) on every engine (schedule / tuning A/B aid; include/spef.h, '
+                         'csrc/spef_tuning.hpp)')
     ap.add_argument('--q8-rolesplit', type=int, default=None,
                     help='int8 blocks 8-17 as role-split kernels (SPEF_OPT_Q8_ROLESPLIT 1) or slab kernels (0, the '
                          'library default)')
