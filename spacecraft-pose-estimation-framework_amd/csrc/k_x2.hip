@@ -352,7 +352,7 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
 // Stage buffers (double-buffered, written one iteration before use): expand weights + expand bias of chunk k in
 // iteration k - 2, depthwise weights + bias and project weights of chunk k in iteration k - 1. Same arithmetic and
 // rounding as x2_irb_kernel (bit-identical results).
-template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST, int P = 1>
 struct X2wGeom {
   static constexpr int NE = 4, ND = 4, NW = NE + ND;
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
@@ -362,6 +362,7 @@ struct X2wGeom {
   static constexpr int WPS = 48;                        // staged project row (halves, 32 used)
   using SL = X2Slab<S, PINP>;
   static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
+  static constexpr int NCL = NCH / P;                   // chunks of this workgroup's hidden part
   static constexpr int NCT = (COUT + 15) / 16, NPC = NCT * 16;
   static constexpr int POUT16 = TH * TW / 16;
   static constexpr int WP = ND / WCO, QPW = POUT16 / WP, NCTW = NCT / WCO;
@@ -378,23 +379,30 @@ struct X2wGeom {
   static constexpr int NPIECE = (NPE + NPD + NPP + NE * 64 - 1) / (NE * 64);
   static_assert(CIN % 8 == 0 && COUT % 4 == 0 && HID % 8 == 0, "channel counts");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
-  static_assert(EPT <= 32 && NCH >= 2, "validity mask / pipeline depth");
+  static_assert(EPT <= 32 && NCH % P == 0 && NCL >= 2, "validity mask / hidden parts / pipeline depth");
   static_assert(SE_B % 16 == 0 && SD_B % 16 == 0 && SP_B % 16 == 0 && SLAB_B % 16 == 0, "16-B aligned stages");
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST>
+// P > 1 (hidden split): the P workgroups of a tile each run NCH / P consecutive hidden chunks and store their
+// project partial sums (no bias, no residual) to Y + part * pstride; x2_split_reduce_kernel adds the P parts in order,
+// the bias and the residual. Small maps get P times the workgroups while every workgroup streams only 1 / P of the
+// block's weights.
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1>
 __global__ __launch_bounds__(512) void x2_irw_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
-    uint32_t nwg) {
-  using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST>;
+    uint32_t nwg, size_t pstride) {
+  using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST, P>;
   using SL = typename G::SL;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
   uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int part = (int)(L % (uint32_t)P);        // hidden part (the parts of a tile share an XCD)
+  L /= (uint32_t)P;
+  const int cb = part * G::NCL;                    // first hidden chunk of this part
   const int tx = (int)(L % (uint32_t)tiles_x);
   L /= (uint32_t)tiles_x;
   const int ty = (int)(L % (uint32_t)tiles_y);
@@ -412,37 +420,37 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     src = nullptr;
     dst = nullptr;
     if (u < G::NPE) {
-      if (ke >= G::NCH) return;
+      if (ke >= G::NCL) return;
       if (u < G::NPE - 8) {
         constexpr int PPR = G::CINP / 8;
         const int pl = u / (32 * PPR), rr = (u / PPR) % 32, g = u % PPR;
-        src = We + (size_t)pl * G::HIDP * G::CINP + (size_t)(32 * ke + rr) * G::CINP + 8 * g;
+        src = We + (size_t)pl * G::HIDP * G::CINP + (size_t)(32 * (cb + ke) + rr) * G::CINP + 8 * g;
         dst = se(ke & 1) + ((pl * 32 + rr) * G::WES + 8 * g) * 2;
       } else {
         const int g = u - (G::NPE - 8);
-        src = be + 32 * ke + 4 * g;
+        src = be + 32 * (cb + ke) + 4 * g;
         dst = se(ke & 1) + 2 * 32 * G::WES * 2 + 16 * g;
       }
       return;
     }
     u -= G::NPE;
     if (u < G::NPD) {
-      if (kd >= G::NCH) return;
+      if (kd >= G::NCL) return;
       if (u < 72) {
         const int tap = u >> 3, g = u & 7;
-        src = Wd + (size_t)tap * G::HIDP + 32 * kd + 4 * g;
+        src = Wd + (size_t)tap * G::HIDP + 32 * (cb + kd) + 4 * g;
         dst = sd(kd & 1) + tap * 32 + 4 * g;
       } else {
-        src = bd + 32 * kd + 4 * (u - 72);
+        src = bd + 32 * (cb + kd) + 4 * (u - 72);
         dst = sd(kd & 1) + 288 + 4 * (u - 72);
       }
       return;
     }
     u -= G::NPD;
     if (PST && u < G::NPP) {
-      if (kd >= G::NCH) return;
+      if (kd >= G::NCL) return;
       const int pl = u / (G::NPC * 4), rr = (u >> 2) % G::NPC, q = u & 3;
-      src = Wp + (size_t)pl * G::NPC * G::HIDP + (size_t)rr * G::HIDP + 32 * kd + 8 * q;
+      src = Wp + (size_t)pl * G::NPC * G::HIDP + (size_t)rr * G::HIDP + 32 * (cb + kd) + 8 * q;
       dst = sp(kd & 1) + (pl * G::NPC + rr) * G::WPS + 8 * q;
     }
   };
@@ -458,7 +466,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       int u = tid + G::NW * 64 * i;
       const void* src = nullptr;
       dst[i] = nullptr;
-      if (u < G::NPE) piece(u, 1, G::NCH, src, dst[i]);                     // expand chunk 1
+      if (u < G::NPE) piece(u, 1, G::NCL, src, dst[i]);                     // expand chunk 1
       else if (u < NP0) piece(u - G::NPE, 0, 0, src, dst[i]);               // expand / dw / project chunk 0
       v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
     }
@@ -579,9 +587,9 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     expand(0);
     __syncthreads();                 // slab 0 visible
 #pragma unroll 1
-    for (int c = 0; c < G::NCH; ++c) {
+    for (int c = 0; c < G::NCL; ++c) {
       store_stage(c);                // expand chunk c + 2, depthwise / project chunk c + 1
-      if (c + 1 < G::NCH) {
+      if (c + 1 < G::NCL) {
         load_stage(c + 1);
         expand(c + 1);
       }
@@ -593,8 +601,9 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     const int wp = d % G::WP, wc = d / G::WP;
     f32x4 acc[G::QPW][G::NCTW];
 #pragma unroll
-    for (int t = 0; t < G::NCTW; ++t) {
-      const float4 bb = *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg);
+    for (int t = 0; t < G::NCTW; ++t) {   // (P > 1: the bias is added once, by the reduce)
+      const float4 bb = P == 1 ? *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
       for (int q = 0; q < G::QPW; ++q) acc[q][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
     }
@@ -611,7 +620,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       if constexpr (!PST) {
 #pragma unroll
         for (int t = 0; t < G::NCTW; ++t) {
-          const size_t off = (size_t)((wc * G::NCTW + t) * 16 + r16) * G::HIDP + 32 * k + 8 * kg;
+          const size_t off = (size_t)((wc * G::NCTW + t) * 16 + r16) * G::HIDP + 32 * (cb + k) + 8 * kg;
           pgh[t] = *reinterpret_cast<const f16x8*>(Wp + off);
           pgl[t] = *reinterpret_cast<const f16x8*>(WpLo + off);
         }
@@ -621,7 +630,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     __syncthreads();
     __syncthreads();
 #pragma unroll 1
-    for (int c = 0; c < G::NCH; ++c) {
+    for (int c = 0; c < G::NCL; ++c) {
       const float* Sl = slab(c & 1);
       const float* D = sd(c & 1);
       float a[G::QPW][8];
@@ -659,12 +668,12 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         split8(a[q], bh[q], bl[q]);
       }
       if constexpr (PST) {
-        const _Float16* P = sp(c & 1);
+        const _Float16* Ps = sp(c & 1);
 #pragma unroll
         for (int t = 0; t < G::NCTW; ++t) {
           const int row = (wc * G::NCTW + t) * 16 + r16;
-          const f16x8 ph = *reinterpret_cast<const f16x8*>(P + row * G::WPS + 8 * kg);
-          const f16x8 pl = *reinterpret_cast<const f16x8*>(P + (G::NPC + row) * G::WPS + 8 * kg);
+          const f16x8 ph = *reinterpret_cast<const f16x8*>(Ps + row * G::WPS + 8 * kg);
+          const f16x8 pl = *reinterpret_cast<const f16x8*>(Ps + (G::NPC + row) * G::WPS + 8 * kg);
 #pragma unroll
           for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(ph, pl, bh[q], bl[q], acc[q][t]);
         }
@@ -673,7 +682,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         for (int t = 0; t < G::NCTW; ++t)
 #pragma unroll
           for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(pgh[t], pgl[t], bh[q], bl[q], acc[q][t]);
-        if (c + 1 < G::NCH) load_pg(c + 1);   // next chunk's fragments: in flight across the barrier and its depthwise
+        if (c + 1 < G::NCL) load_pg(c + 1);   // next chunk's fragments: in flight across the barrier and its depthwise
       }
       __syncthreads();
     }
@@ -690,6 +699,10 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
         if (co >= COUT) continue;
         f32x4 v = acc[q][t];
+        if constexpr (P > 1) {   // partial sum of this hidden part
+          *reinterpret_cast<float4*>(Y + part * pstride + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
+          continue;
+        }
         if constexpr (RES) {
           const float4 r = *reinterpret_cast<const float4*>(X + pix * CIN + co);
           v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
@@ -698,6 +711,29 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       }
     }
   }
+}
+
+// Hidden-split join: y = ((part 0 + part 1) + ...) + bias (+ residual), in that order, 4 channels per thread.
+template <int P, bool RES>
+__global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __restrict__ parts, size_t pstride,
+                                                              const float* __restrict__ bias,
+                                                              const float* __restrict__ X, float* __restrict__ Y,
+                                                              size_t n4, int cout4) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n4) return;
+  float4 v = reinterpret_cast<const float4*>(parts)[i];
+#pragma unroll
+  for (int p = 1; p < P; ++p) {
+    const float4 u = reinterpret_cast<const float4*>(parts + p * pstride)[i];
+    v.x += u.x; v.y += u.y; v.z += u.z; v.w += u.w;
+  }
+  const float4 bb = reinterpret_cast<const float4*>(bias)[i % (size_t)cout4];
+  v.x += bb.x; v.y += bb.y; v.z += bb.z; v.w += bb.w;
+  if constexpr (RES) {
+    const float4 r = reinterpret_cast<const float4*>(X)[i];
+    v.x += r.x; v.y += r.y; v.z += r.z; v.w += r.w;
+  }
+  reinterpret_cast<float4*>(Y)[i] = v;
 }
 
 // (cin, hidden, cout, stride, expand, residual, TH, TW, waves, cout groups, kind): MobileNet-V2's 17 blocks
@@ -723,11 +759,12 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
-// Smaller tiles for maps whose primary tiling leaves CUs idle (fewer workgroups than the 256 CUs; the role-split
-// kernels run one workgroup per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64).
-#define SPEF_X2_SMALL_TABLE(X)                                   \
-  X(160, 960, 160, 1, true, true, 4, 8, 8, 2, 1)    /* 15-16 */  \
-  X(160, 960, 320, 1, true, false, 4, 8, 8, 4, 2)   /* 17 */
+// Maps whose primary tiling leaves CUs idle (fewer workgroups than CUs; the role-split kernels run one workgroup
+// per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64) split the hidden dimension over P
+// workgroups per tile (last field; partial sums joined by x2_split_reduce_kernel in the caller's scratch).
+#define SPEF_X2_SMALL_TABLE(X)                                      \
+  X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1, 2)    /* 15-16 */  \
+  X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2, 2)   /* 17 */
 
 template <typename K>
 static hipError_t x2_set_lds(K k, int lds) {   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
@@ -735,12 +772,13 @@ static hipError_t x2_set_lds(K k, int lds) {   // > 64 KiB dynamic LDS needs the
   return hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
 }
 
-template <int CIN, int HID, int COUT, int S, bool EXPAND, bool RES, int TH, int TW, int NW, int WCO, int KIND>
+template <int CIN, int HID, int COUT, int S, bool EXPAND, bool RES, int TH, int TW, int NW, int WCO, int KIND,
+          int P = 1>
 static hipError_t x2_irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
                             const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
-                            hipStream_t s) {
+                            hipStream_t s, float* scratch = nullptr) {
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
-  const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
+  const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B * P;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   static bool attr_set = false;
@@ -756,15 +794,23 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
                                         (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
   } else {
     static_assert(EXPAND && NW == 8, "role-split blocks expand, 4 + 4 waves");
-    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND == 1>;
-    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND == 1>;
+    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND == 1, P>;
+    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND == 1, P>;
     if (!attr_set) {
       hipError_t e = x2_set_lds(k, G::LDS_BYTES);
       if (e != hipSuccess) return e;
       attr_set = true;
     }
+    const size_t pstride = (size_t)B * OH * OW * COUT;   // floats per hidden part (16-B multiple: COUT % 4 == 0)
+    if (P > 1 && !scratch) return hipErrorInvalidValue;
     k<<<nwg, 512, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
-                                    (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
+                                    P > 1 ? scratch : (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg, pstride);
+    if constexpr (P > 1) {
+      const size_t n4 = pstride / 4;
+      x2_split_reduce_kernel<P, RES><<<(unsigned)((n4 + 255) / 256), 256, 0, s>>>(scratch, pstride, bp,
+                                                                                   (const float*)x, (float*)y, n4,
+                                                                                   COUT / 4);
+    }
   }
   return hipGetLastError();
 }
@@ -779,7 +825,7 @@ bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool 
 
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
-                         int B, int H, int W, int OH, int OW, hipStream_t s) {
+                         int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch) {
   if (!x || !y || !wd || !bd || !wp || !bp || (expand && (!we || !be))) return hipErrorInvalidValue;
   int num_cu = 0;
   {
@@ -793,11 +839,11 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
     num_cu = cus;
   }
 #define SPEF_X2_TILES(TH_, TW_) ((int64_t)((OW + (TW_)-1) / (TW_)) * ((OH + (TH_)-1) / (TH_)) * B)
-#define SPEF_X2_SMALL(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                        \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS &&                    \
-      SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) <= num_cu)                                      \
-    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, \
-                                                                     s);
+#define SPEF_X2_SMALL(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_)                                    \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && scratch &&         \
+      SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)                                 \
+    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
+                                                                         OW, s, scratch);
   SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
 #undef SPEF_X2_SMALL
 #undef SPEF_X2_TILES

@@ -338,9 +338,11 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         char key[96];
         snprintf(key, sizeof(key), "x2_irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
+          // a third activation buffer (each holds the largest map) is the hidden-split form's partial-sum scratch
           return launch_x2_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
                                ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
-                               ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
+                               ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s,
+                               (float*)pick({x, y}));
         }));
         cur = y;
         h = OH;

@@ -85,9 +85,10 @@ const char* gemm_f32_key(int N);
 // operands (3 MFMAs per product). we: [2][r32(hid)][r32(cin)] fp16 (hi plane, lo plane), be fp32 [r32(hid)],
 // wd fp32 [9][r32(hid)], bd fp32 [r32(hid)], wp [2][r16(cout)][r32(hid)] fp16, bp fp32 [r16(cout)]; zero padded.
 bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
+// scratch (nullable): B * OH * OW * cout * 2 floats for the hidden-split form of the late blocks on small maps.
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
-                         int B, int H, int W, int OH, int OW, hipStream_t s);
+                         int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch = nullptr);
 // uint8 NHWC frames -> stem + block 1 -> fp32 [B][OH][OW][16] (x2_front_kernel); wsx: blob OP_STEM x0 of dtype 5.
 hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
                            const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
