@@ -77,6 +77,22 @@ def test_block_outputs_vs_oracle(x2, sd, b, h, w):
         assert err < 5e-5, (op, err)
 
 
+def test_hidden_split_blocks_vs_oracle(x2, sd):
+    """B=24 at 240x384 (the keypoint head's input size): blocks 15-17 on 8x12 maps run the hidden-split form (two
+    workgroups per 8x8 tile, ordered partial-sum join); their outputs, and those of the blocks before them, within the
+    block-output bound of test_block_outputs_vs_oracle."""
+    fr = _frames(24, 240, 384, 41)
+    x = M.u8_nhwc_to_nchw_f32(fr)
+    xg = torch.from_numpy(fr).cuda()
+    torch.set_num_threads(16)
+    for op in (8, 10, 15, 17):
+        ref = M.backbone(x, sd, upto=op).permute(0, 2, 3, 1).numpy()
+        got = x2.probe(xg, op).cpu().numpy()
+        assert got.shape == ref.shape, (op, got.shape, ref.shape)
+        err = np.abs(got - ref).max() / max(1e-6, np.abs(ref).max())
+        assert err < 5e-5, (op, err)
+
+
 def test_sharp_head_logits_absolute(golden):
     """the bench weights with a sharp orientation head (head_std 0.3: logits up to ~20, peaked
     histograms) at 512x512 -- max |d logit| against the FP32 oracle at the north star's absolute 1e-3.
