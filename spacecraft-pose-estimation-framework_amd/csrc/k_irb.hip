@@ -114,6 +114,7 @@ struct IrbGeom {
   static constexpr int EPT = (PIN16 + NW - 1) / NW;   // expand pixel tiles per wave
   static constexpr int NCH = (HID + 31) / 32;
   static constexpr int HIDP = NCH * 32;        // project K (blob pads to 32)
+  static constexpr bool NT_Y = S == 2 && COUT == 64;   // nontemporal output stores (block 7)
   static constexpr int POUT = TH * TW;
   static constexpr int POUT16 = POUT / 16;
   static constexpr int WP = NW / WCO;          // pixel-tile groups in the depthwise/project phase
@@ -906,7 +907,10 @@ __global__ __launch_bounds__(NW * 64) void irb_kernel(
       x4 o;
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (T)v[e];
-      SPEF_KB_YSTORE(*reinterpret_cast<x4*>(yr + co) = o, o);
+      if constexpr (G::NT_Y)   // (block 7: measured -4 us; elsewhere the consumer reads the map from the caches)
+        SPEF_KB_YSTORE(__builtin_nontemporal_store(o, reinterpret_cast<x4*>(yr + co)), o);
+      else
+        SPEF_KB_YSTORE(*reinterpret_cast<x4*>(yr + co) = o, o);
     }
   }
   SPEF_TRACE(SPEF_TRACE_SLOTS - 1);
