@@ -909,7 +909,51 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
   // ---- staging: the input rows of the stencil as aligned dword loads (a row segment is 3 ICL bytes at any byte
   // alignment), bytes scattered to fp16 [row][col][4] over a zero-filled tile (zero outside the frame: the stem's
   // padding; the ci = 3 pad); block-1 depthwise weights + bias
-  {
+  // Interior tiles (every staged row and column inside the frame, 4-byte aligned rows): the row's dwords load one per
+  // lane, and lane c builds stem pixel column c from two of them (two lane shuffles + one v_alignbyte), converts the
+  // three bytes exactly to fp16 (0x6400 | byte = 1024 + byte, minus 1024) and writes its 4 halves with one 8-B store.
+  const bool fast = (W & 3) == 0 && ix0 >= 0 && ix0 + G::ICL <= W && iy0 >= 0 && iy0 + G::IRW <= H;
+  if (fast) {
+    constexpr int RPW = (G::IRW + NW - 1) / NW;
+    static_assert(G::ICL <= 64 && (3 * G::ICL + 3 + 3) / 4 < 64, "one row per wave");
+    const int off = (3 * ix0) & 3;                      // rows start `off` bytes into their dword (W % 4 == 0)
+    const int nl = (off + 3 * G::ICL + 3) / 4;          // dwords holding the row segment
+    const uint8_t* Xb = X + (size_t)b * H * W * 3;
+    uint32_t v[RPW];
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = wave + NW * i;
+      v[i] = 0;
+      if (r < G::IRW && lane < nl)
+        v[i] = *reinterpret_cast<const uint32_t*>(Xb + (((size_t)(iy0 + r) * W + ix0) * 3 - off) + 4 * lane);
+    }
+    float4 dwv[2];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + NW * 64 * i;   // 72 pieces of the [9][32] weights, 8 of the bias
+      dwv[i] = u < 72 ? *reinterpret_cast<const float4*>(Wd + 4 * u)
+                      : u < 80 ? *reinterpret_cast<const float4*>(bd + 4 * (u - 72)) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    const int q = 3 * lane + off, d = q >> 2, sh = q & 3;   // lane c = pixel column c: segment bytes q .. q + 2
+    const f16x2 k1024 = {(_Float16)1024.0f, (_Float16)1024.0f};
+#pragma unroll
+    for (int i = 0; i < RPW; ++i) {
+      const int r = wave + NW * i;
+      const uint32_t lo = __shfl(v[i], d, 64), hi = __shfl(v[i], d + 1 < 64 ? d + 1 : 63, 64);
+      if (r < G::IRW && lane < G::ICL) {
+        const uint32_t by = __builtin_amdgcn_alignbyte(hi, lo, sh);   // bytes ci 0, 1, 2 of the pixel
+        const f16x2 h01 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(0u, by, 0x0c010c00u) | 0x64006400u) - k1024;
+        const f16x2 h2 = __builtin_bit_cast(f16x2, __builtin_amdgcn_perm(0u, by, 0x0c0c0c02u) | 0x64006400u) - k1024;
+        *reinterpret_cast<uint2*>(Xi + r * G::ICS + 4 * lane) =
+            make_uint2(__builtin_bit_cast(uint32_t, h01), __builtin_bit_cast(uint32_t, h2));
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int u = tid + NW * 64 * i;
+      if (u < 80) *reinterpret_cast<float4*>(Ds + 4 * u) = dwv[i];
+    }
+  } else {
     constexpr int NDW = (3 * G::ICL + 3 + 3) / 4 + 1;   // dwords covering one row segment at any alignment
     constexpr int NPC = G::IRW * NDW;
     constexpr int NIT = (NPC + NW * 64 - 1) / (NW * 64);
