@@ -865,9 +865,9 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
 // one 16-B (kg 0) or 8-B (kg 1) LDS read of the staged input tile [row][col][4] (fp16). The stem map of the output
 // tile + halo goes to the fp32 slab (zero outside the image: the depthwise's padding), then block 1 runs as in
 // x2_irb_kernel.
-template <int TH, int TW>
+template <int TH, int TW, int NW_ = 4>
 struct X2FrontGeom {
-  static constexpr int NW = 4;
+  static constexpr int NW = NW_;
   static constexpr int PH = TH + 2, PW = TW + 2;        // stem pixels of the tile (+ block-1 halo)
   static constexpr int PIN = PH * PW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
   static constexpr int IRW = 2 * PH + 1, ICL = 2 * PW + 1;   // input rows / columns of the stem stencil
@@ -881,13 +881,13 @@ struct X2FrontGeom {
   static_assert(TW == 16 && POUT16 % NW == 0 && EPT <= 32, "front tile");
 };
 
-template <int TH, int TW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) void x2_front_kernel(
+template <int TH, int TW, int NW_ = 4>
+__global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ == 4 ? 3 : 4, 8))) void x2_front_kernel(
     const uint8_t* __restrict__ X, const _Float16* __restrict__ Wsx, const float* __restrict__ bs,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
     uint32_t nwg) {
-  using G = X2FrontGeom<TH, TW>;
+  using G = X2FrontGeom<TH, TW, NW_>;
   using SL = typename G::SL;
   constexpr int NW = G::NW;
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1135,18 +1135,27 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3, 8))) voi
   }
 }
 
+#ifndef SPEF_X2_FRONT_TH
+#define SPEF_X2_FRONT_TH 16
+#define SPEF_X2_FRONT_NW 8
+#endif
 hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
                            const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                            hipStream_t s) {
-  constexpr int TH = 8, TW = 16;
-  using G = X2FrontGeom<TH, TW>;
+  constexpr int TH = SPEF_X2_FRONT_TH, TW = 16, NW = SPEF_X2_FRONT_NW;
+  using G = X2FrontGeom<TH, TW, NW>;
   if (!x || !wsx || !bs || !wd || !bd || !wp || !bp || !y) return hipErrorInvalidValue;
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  static_assert(G::LDS_BYTES <= 65536, "front kernel LDS");
-  x2_front_kernel<TH, TW><<<nwg, 256, G::LDS_BYTES, s>>>((const uint8_t*)x, (const _Float16*)wsx, bs, wd, bd,
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = x2_set_lds(x2_front_kernel<TH, TW, NW>, G::LDS_BYTES);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  x2_front_kernel<TH, TW, NW><<<nwg, NW * 64, G::LDS_BYTES, s>>>((const uint8_t*)x, (const _Float16*)wsx, bs, wd, bd,
                                                         (const _Float16*)wp, bp, (float*)y, H, W, OH, OW, tiles_x,
                                                         tiles_y, nwg);
   return hipGetLastError();
