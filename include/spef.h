@@ -179,7 +179,7 @@ int spef_profile_end(spef_ctx* ctx, char* buf, size_t cap, size_t* needed);
 /* On-box measurement (bench.py; SURVEY.md §8d "peaks re-measured by the build's own microbenchmark"), no model
  * involved. spef_measure_peaks runs, on `device`, `reps` timed launches (after one warm-up) of each of: a dense
  * v_mfma_f32_16x16x32_f16 loop, a v_mfma_i32_16x16x64_i8 loop (random operands, 8 independent chains per wave,
- * 4 waves per SIMD), a 1 GiB HBM copy and a 1 GiB HBM read, and writes the best rates: out[0] fp16 TFLOP/s,
+ * 4 waves per SIMD), a 4 GiB HBM copy and a 4 GiB HBM read, and writes the best rates: out[0] fp16 TFLOP/s,
  * out[1] int8 TOP/s, out[2] copy GB/s (read + write bytes), out[3] read GB/s, out[4] / out[5] the shader clock in
  * MHz held inside the fp16 / int8 loop (median over workgroups of delta s_memtime / delta s_memrealtime x 100),
  * out[6] / out[7] the stream configuration behind out[2] / out[3] (workgroups per CU x 100 + 16-B loads in flight

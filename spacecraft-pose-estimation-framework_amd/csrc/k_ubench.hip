@@ -169,7 +169,7 @@ static int measure_peaks_on(int device, int reps, double* out) {
   UB_TRY(hipGetDeviceProperties(&prop, device));
   const int cus = prop.multiProcessorCount;
   Scratch sc;
-  const size_t hbm_bytes = (size_t)1 << 30;   // 1 GiB per buffer: 4x the 256 MB Infinity Cache
+  const size_t hbm_bytes = (size_t)4 << 30;   // 4 GiB per buffer: 16x the 256 MB Infinity Cache, launch costs < 1 %
   UB_TRY(hipMalloc(&sc.p[0], 4096 * 16));
   UB_TRY(hipMalloc(&sc.p[1], (size_t)cus * 4 * 256 * sizeof(float)));
   UB_TRY(hipMalloc(&sc.p[2], (size_t)cus * 4 * 2 * sizeof(unsigned long long)));

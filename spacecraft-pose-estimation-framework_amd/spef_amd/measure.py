@@ -26,7 +26,7 @@ def measure_peaks(device: int = 0, reps: int = 2) -> dict:
             'sclk_mhz_fp16_loop': round(out[4], 1), 'sclk_mhz_int8_loop': round(out[5], 1),
             'hbm_copy_config': cfg(out[6]), 'hbm_read_config': cfg(out[7]),
             'method': 'csrc/k_ubench.hip: best of %d timed launches after a warm-up; MFMA loops on random operands, '
-                      '8 chains per wave, 4 waves per SIMD; HBM: 1 GiB buffers (copy counts read + write bytes), '
+                      '8 chains per wave, 4 waves per SIMD; HBM: 4 GiB buffers (copy counts read + write bytes), '
                       'contiguous 16-32 KiB blocks per workgroup iteration, best of %d launches of each of 4/8/16 '
                       'workgroups per CU or one workgroup per block x 4/8 16-B loads in flight per thread x '
                       'plain/nontemporal' % (reps, reps + 2)}
