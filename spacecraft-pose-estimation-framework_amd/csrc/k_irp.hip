@@ -162,23 +162,32 @@ __global__ __launch_bounds__((NM + NV) * 64) __attribute__((amdgpu_waves_per_eu(
     // expand A fragments of one hidden half: rows 32c + 16hh + r16, k = 32ks + 8kg
     x8 ea[G::KS];
     auto load_ea = [&](int c) {   // from L2, one step ahead
-#ifdef SPEF_KBENCH_IRW_NO_WLOAD   // tools/kbench timing ablation (wrong results): no weight loads after chunk 1
-      if (c > 1) return;
+#if defined(SPEF_KBENCH_IRW_NO_WLOAD) || defined(SPEF_KBENCH_IRW_NO_ELOAD)   // tools/kbench timing ablations (wrong
+      if (c > 1) return;                                                        // results): no weight loads after chunk 1
 #endif
+#ifdef SPEF_KBENCH_IRW_FIXED_WLOAD   // timing ablation: every chunk loads chunk 0's fragments (L1/L2-hot addresses)
+      const T* w0 = We + (size_t)(16 * hh + r16) * CIN + 8 * kg;
+#else
       const T* w0 = We + (size_t)(32 * c + 16 * hh + r16) * CIN + 8 * kg;
+#endif
 #pragma unroll
       for (int ks = 0; ks < G::KS; ++ks) ea[ks] = c < G::NCH ? load8<DT>(w0 + 32 * ks) : zero8<DT>();
     };
     // project A fragments: output-channel tiles wave + NM*t, hidden k = 32c + 8kg
     x8 pa[G::NCTW];
     auto load_pa = [&](int c) {
-#ifdef SPEF_KBENCH_IRW_NO_WLOAD
+#if defined(SPEF_KBENCH_IRW_NO_WLOAD) || defined(SPEF_KBENCH_IRW_NO_PLOAD)
       if (c > 1) return;
+#endif
+#ifdef SPEF_KBENCH_IRW_FIXED_WLOAD
+      const int cw = 0;
+#else
+      const int cw = c;
 #endif
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t) {
         const int ct = wave + NM * t;
-        pa[t] = (c < G::NCH && ct < G::NCT) ? load8<DT>(Wp + (size_t)(16 * ct + r16) * HID + 32 * c + 8 * kg)
+        pa[t] = (c < G::NCH && ct < G::NCT) ? load8<DT>(Wp + (size_t)(16 * ct + r16) * HID + 32 * cw + 8 * kg)
                                             : zero8<DT>();
       }
     };

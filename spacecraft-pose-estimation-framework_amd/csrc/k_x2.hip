@@ -759,6 +759,12 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
+// 16x16 tiles with 8 waves (2 workgroups per CU) where they tile the map exactly: blocks 3, 5-6 at 512^2 (interleaved
+// A/B: 165 -> 153 us and 119 -> 115 us per step); on maps they do not divide (60x96, 30x48 at 240x384) the partial
+// tiles cost more than the occupancy gains.
+#define SPEF_X2_EXACT_TABLE(X)                                      \
+  X(24, 144, 24, 1, true, true, 16, 16, 8, 1, 0)     /* 3 */      \
+  X(32, 192, 32, 1, true, true, 16, 16, 8, 1, 0)     /* 5-6 */
 // Maps whose primary tiling leaves CUs idle (fewer workgroups than CUs; the role-split kernels run one workgroup
 // per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64) split the hidden dimension over P
 // workgroups per tile (last field; partial sums joined by x2_split_reduce_kernel in the caller's scratch).
@@ -846,6 +852,13 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
                                                                          OW, s, scratch);
   SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
 #undef SPEF_X2_SMALL
+#define SPEF_X2_EXACT(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                        \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && OH % (TH_) == 0 &&  \
+      OW % (TW_) == 0)                                                                                        \
+    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, \
+                                                                     s);
+  SPEF_X2_EXACT_TABLE(SPEF_X2_EXACT)
+#undef SPEF_X2_EXACT
 #undef SPEF_X2_TILES
 #define SPEF_X2_CASE(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                         \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                      \
