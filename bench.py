@@ -273,6 +273,8 @@ def set_wavespec(pipe, args) -> None:
     """--wavespec / --q8-rolesplit: the late-block schedule of every engine in the pipeline (A/B aids)."""
     from spef_amd import _lib as L
     extra = [tuple(int(v) for v in o.split('=')) for o in args.set_option]
+    if getattr(args, 'graphs', False):
+        pipe.use_graphs()
     for opt, val in [(L.OPT_WAVESPEC, args.wavespec), (L.OPT_Q8_ROLESPLIT, args.q8_rolesplit)] + extra:
         if val is not None:
             for e in pipe.engines:
@@ -473,6 +475,8 @@ def main():
                          'library default)')
     ap.add_argument('--inflight', type=int, default=3,
                     help='batches in flight: consecutive steps alternate over this many HIP streams (spef_amd.pipeline)')
+    ap.add_argument('--graphs', action='store_true',
+                    help='replay each (stream, input batch) forward + decode as a recorded HIP graph (StreamPipeline.use_graphs)')
     ap.add_argument('--frame-buffers', type=int, default=6,
                     help='distinct device batches the timed steps rotate over (6 x 50 MB > 256 MB Infinity Cache)')
     ap.add_argument('--no-cpu-baseline', action='store_true')
