@@ -1265,6 +1265,156 @@ __global__ __launch_bounds__(256) void x2_pw_kernel(const float* __restrict__ X,
   }
 }
 
+// Staged form (the last conv, K = 320): 64 pixels x 256 output channels per workgroup. The 64 x K fp32 input block is
+// split into hi / lo fp16 once per workgroup and staged in LDS (80 KB at K = 320: two workgroups per CU), instead of
+// once per wave and 64-channel chunk from L2 as above (4x the split VALU and 4x the activation reads); the four waves
+// take 64 channels each and stream their hi / lo weight fragments from L2 one K step ahead. Same products, same
+// accumulation order, same pool partials as x2_pw_kernel<4, 4, POOL> (bit-identical). LDS rows of Kp halves with the
+// 16-B granule index XOR-ed by (row & 7): the 8 rows a ds_read_b128 lane group reads hit disjoint banks.
+#ifndef SPEF_X2_PWS
+#define SPEF_X2_PWS 1
+#endif
+template <bool POOL>
+__global__ __launch_bounds__(256) void x2_pws_kernel(const float* __restrict__ X, const _Float16* __restrict__ Wt,
+                                                     const float* __restrict__ bias, float* __restrict__ Y, int64_t M,
+                                                     int K, int N, int Np, int Kp, int n_chunks, uint32_t nwg) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  _Float16* Xh = reinterpret_cast<_Float16*>(smem);   // [64][Kp] hi halves (swizzled granules)
+  _Float16* Xl = Xh + 64 * Kp;                         // [64][Kp] lo halves
+  const uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const int chunk = (int)(L % (uint32_t)n_chunks);
+  const int64_t m0 = (int64_t)(L / (uint32_t)n_chunks) * 64;
+  const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
+  const int r16 = lane & 15, kg = lane >> 4;
+  const int n0 = chunk * 256 + wave * 64;
+  const _Float16* Wlo = Wt + (size_t)Np * Kp;
+  // ---- stage: 64 rows x Kp / 8 granules, 8 fp32 -> hi / lo per piece (batches of 5 pieces per thread, loads first)
+  {
+    const int GP = Kp >> 3, NP = 64 * GP;
+    for (int u0 = 0; u0 < NP; u0 += 256 * 5) {
+      float4 v[5][2];
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int u = u0 + tid + 256 * i;
+        const int px = u / GP, g = u - px * GP;
+        const int64_t p = m0 + px;
+        v[i][0] = v[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        if (u < NP && p < M && 8 * g < K) {
+          const float* xp = X + (size_t)p * K + 8 * g;
+          v[i][0] = *reinterpret_cast<const float4*>(xp);
+          v[i][1] = *reinterpret_cast<const float4*>(xp + 4);
+        }
+      }
+#pragma unroll
+      for (int i = 0; i < 5; ++i) {
+        const int u = u0 + tid + 256 * i;
+        if (u >= NP) break;
+        const int px = u / GP, g = u - px * GP;
+        const float f[8] = {v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w};
+        f16x8 hi, lo;
+        split8(f, hi, lo);
+        const int o = px * Kp + 8 * (g ^ (px & 7));
+        *reinterpret_cast<f16x8*>(Xh + o) = hi;
+        *reinterpret_cast<f16x8*>(Xl + o) = lo;
+      }
+    }
+  }
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const float4 bb = *reinterpret_cast<const float4*>(bias + n0 + 16 * a + 4 * kg);
+#pragma unroll
+    for (int m = 0; m < 4; ++m) acc[a][m] = f32x4{bb.x, bb.y, bb.z, bb.w};
+  }
+  f16x8 ah[4], al[4];
+  auto load_a = [&](int k0) {
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      const size_t off = (size_t)(n0 + 16 * a + r16) * Kp + k0 + 8 * kg;
+      ah[a] = *reinterpret_cast<const f16x8*>(Wt + off);
+      al[a] = *reinterpret_cast<const f16x8*>(Wlo + off);
+    }
+  };
+  load_a(0);
+  __syncthreads();
+#pragma unroll 1
+  for (int k0 = 0; k0 < Kp; k0 += 32) {
+    f16x8 bh[4], bl[4];
+    const int g = (k0 >> 3) + kg;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int px = 16 * m + r16;
+      const int o = px * Kp + 8 * (g ^ (px & 7));
+      bh[m] = *reinterpret_cast<const f16x8*>(Xh + o);
+      bl[m] = *reinterpret_cast<const f16x8*>(Xl + o);
+    }
+    f16x8 ch[4], cl[4];
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      ch[a] = ah[a];
+      cl[a] = al[a];
+    }
+    if (k0 + 32 < Kp) load_a(k0 + 32);
+#pragma unroll
+    for (int a = 0; a < 4; ++a)
+#pragma unroll
+      for (int m = 0; m < 4; ++m) acc[a][m] = mfma_x2(ch[a], cl[a], bh[m], bl[m], acc[a][m]);
+  }
+  if constexpr (POOL) {   // the 64 pixels m0 .. m0 + 63, all valid (M % 64 == 0)
+#pragma unroll
+    for (int a = 0; a < 4; ++a) {
+      float sm[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        float t = 0.f;
+#pragma unroll
+        for (int m = 0; m < 4; ++m) t += fmaxf(acc[a][m][r], 0.f);
+#pragma unroll
+        for (int o = 1; o < 16; o <<= 1) t += __shfl_xor(t, o, 64);
+        sm[r] = t;
+      }
+      const int i = n0 + 16 * a + 4 * kg;
+      if (r16 == 0 && i < N)
+        *reinterpret_cast<float4*>(Y + (size_t)(m0 / 64) * N + i) = make_float4(sm[0], sm[1], sm[2], sm[3]);
+    }
+    return;
+  }
+#pragma unroll
+  for (int a = 0; a < 4; ++a) {
+    const int i = n0 + 16 * a + 4 * kg;
+    if (i >= N) continue;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      const int64_t p = m0 + 16 * m + r16;
+      if (p >= M) continue;
+      const f32x4 v = acc[a][m];
+      *reinterpret_cast<float4*>(Y + (size_t)p * N + i) =
+          make_float4(fmaxf(v[0], 0.f), fmaxf(v[1], 0.f), fmaxf(v[2], 0.f), fmaxf(v[3], 0.f));
+    }
+  }
+}
+
+static bool x2_pws_ok(int Kp, int Np) { return SPEF_X2_PWS && Kp % 64 == 0 && Kp <= 320 && Np % 256 == 0; }
+
+template <bool POOL>
+static hipError_t x2_pws_go(const void* x, const void* wt, const float* bias, float* y, int64_t M, int K, int N, int Np,
+                            int Kp, hipStream_t s) {
+  const int n_chunks = Np / 256;
+  const int64_t nwg64 = (M + 63) / 64 * n_chunks;
+  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+  const uint32_t nwg = (uint32_t)nwg64;
+  const int lds = 64 * Kp * 2 * (int)sizeof(_Float16);
+  static bool attr_set = false;
+  if (!attr_set) {
+    hipError_t e = x2_set_lds(x2_pws_kernel<POOL>, 64 * 320 * 2 * (int)sizeof(_Float16));   // the largest Kp
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  x2_pws_kernel<POOL><<<nwg, 256, lds, s>>>((const float*)x, (const _Float16*)wt, bias, y, M, K, N, Np, Kp, n_chunks,
+                                            nwg);
+  return hipGetLastError();
+}
+
 // pooled[b][c] = (sum over the image's HW / 64 wave partials, in order) / HW
 __global__ __launch_bounds__(256) void x2_pool_reduce_kernel(const float* __restrict__ part, float* __restrict__ pooled,
                                                              int B, int nblk, int N, float inv_hw) {
@@ -1282,6 +1432,7 @@ hipError_t launch_x2_pw_relu(const void* x, const void* wt, const float* bias, f
   if (M <= 0) return hipSuccess;
   const int Kp = (K + 31) & ~31, Np = (N + 15) & ~15;
   if ((K & 7) || (N & 3) || Np % 64) return hipErrorInvalidValue;
+  if (x2_pws_ok(Kp, Np)) return x2_pws_go<false>(x, wt, bias, y, M, K, N, Np, Kp, s);
   constexpr int NT = 4, MT = 4;
   const int n_chunks = Np / (16 * NT);
   const int64_t nwg64 = (M + 64 * MT - 1) / (64 * MT) * n_chunks;
@@ -1300,13 +1451,18 @@ hipError_t launch_x2_pw_pool(const void* x, const void* wt, const float* bias, f
   if ((K & 7) || !x2_pw_pool_supported(HW, N) || B <= 0) return hipErrorInvalidValue;
   constexpr int NT = 4, MT = 4;
   const int64_t M = (int64_t)B * HW;
-  const int n_chunks = Np / (16 * NT);
-  const int64_t nwg64 = (M + 64 * MT - 1) / (64 * MT) * n_chunks;
-  if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
-  const uint32_t nwg = (uint32_t)nwg64;
-  x2_pw_kernel<NT, MT, true><<<nwg, 256, 0, s>>>((const float*)x, (const _Float16*)wt, bias, part, M, K, N, Np, Kp,
-                                                 n_chunks, nwg);
-  hipError_t e = hipGetLastError();
+  hipError_t e;
+  if (x2_pws_ok(Kp, Np)) {
+    e = x2_pws_go<true>(x, wt, bias, part, M, K, N, Np, Kp, s);
+  } else {
+    const int n_chunks = Np / (16 * NT);
+    const int64_t nwg64 = (M + 64 * MT - 1) / (64 * MT) * n_chunks;
+    if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
+    const uint32_t nwg = (uint32_t)nwg64;
+    x2_pw_kernel<NT, MT, true><<<nwg, 256, 0, s>>>((const float*)x, (const _Float16*)wt, bias, part, M, K, N, Np, Kp,
+                                                   n_chunks, nwg);
+    e = hipGetLastError();
+  }
   if (e != hipSuccess) return e;
   x2_pool_reduce_kernel<<<(unsigned)(((int64_t)B * N + 255) / 256), 256, 0, s>>>(part, pooled, B, HW / 64, N,
                                                                                  1.0f / (float)HW);
