@@ -768,6 +768,9 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
 // Maps whose primary tiling leaves CUs idle (fewer workgroups than CUs; the role-split kernels run one workgroup
 // per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64) split the hidden dimension over P
 // workgroups per tile (last field; partial sums joined by x2_split_reduce_kernel in the caller's scratch).
+#ifndef SPEF_X2_SMALL_ALWAYS   // A/B aid: the hidden split on every map size
+#define SPEF_X2_SMALL_ALWAYS 0
+#endif
 #define SPEF_X2_SMALL_TABLE(X)                                      \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1, 2)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2, 2)   /* 17 */
@@ -847,7 +850,7 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
 #define SPEF_X2_TILES(TH_, TW_) ((int64_t)((OW + (TW_)-1) / (TW_)) * ((OH + (TH_)-1) / (TH_)) * B)
 #define SPEF_X2_SMALL(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_)                                    \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && scratch &&         \
-      SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)                                 \
+      (SPEF_X2_SMALL_ALWAYS || (SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)))     \
     return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
                                                                          OW, s, scratch);
   SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
