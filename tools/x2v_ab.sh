@@ -6,7 +6,7 @@ for pass in 1 2; do
   for v in $L; do
     for h in ursonet keypoints; do
       SPEF_LIB=$R/abx2/$v.so timeout -k 10 120 python tools/variant_time.py fp16x2 $h 64 > gpurun_out/x2v_$v$h$pass.log 2>&1 || exit 1
-      echo "$v $(grep -E '^==' gpurun_out/x2v_$v$h$pass.log)"; grep -E "fc_splitk|epnp" gpurun_out/x2v_$v$h$pass.log
+      echo "$v $(grep -E '^==' gpurun_out/x2v_$v$h$pass.log)"; grep -E "x2_pw" gpurun_out/x2v_$v$h$pass.log
     done
   done
 done
