@@ -48,11 +48,60 @@ __device__ __forceinline__ void split4(float4 v, uint2& hi, uint2& lo) {
   hi = make_uint2(pack_h2(h[0], h[1]), pack_h2(h[2], h[3]));
   lo = make_uint2(pack_h2(l[0], l[1]), pack_h2(l[2], l[3]));
 }
+// lo halves of a pair: fp16(a - hi.x), fp16(b - hi.y), each ONE v_fma_mix{lo,hi}_f16 (the difference is formed
+// exactly and rounded once, the same value as split8's fp32 residual + convert, which takes 1.5 ops per value)
+__device__ __forceinline__ uint32_t lo_pair(uint32_t hi2, float a, float b) {
+  uint32_t r;
+  asm("v_fma_mixlo_f16 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]\n\t"
+      "v_fma_mixhi_f16 %0, %1, -1.0, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "=&v"(r) : "v"(hi2), "v"(a), "v"(b));
+  return r;
+}
+// ReLU + hi / lo split of 8 fp32 values: 8 v_max + 4 v_cvt_pk + 8 v_fma_mix (bit-identical to max + split8)
+__device__ __forceinline__ void relu_split8(const f32x2 v[4], f16x8& hi, f16x8& lo) {
+  uint32_t h[4], l[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const float a = fmaxf(v[i].x, 0.f), b = fmaxf(v[i].y, 0.f);
+    h[i] = pack_h2((_Float16)a, (_Float16)b);
+    l[i] = lo_pair(h[i], a, b);
+  }
+  hi = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+  lo = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
+}
 // acc += (a_hi + a_lo)(b_hi + b_lo) without the lo*lo term
 __device__ __forceinline__ f32x4 mfma_x2(f16x8 ah, f16x8 al, f16x8 bh, f16x8 bl, f32x4 acc) {
   acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc, 0, 0, 0);
   acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, acc, 0, 0, 0);
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, acc, 0, 0, 0);
+}
+// acc += (a_hi + a_lo) b for an operand b that is exact in fp16 (fp16-stored activations: the fp16mx schedule)
+__device__ __forceinline__ f32x4 mfma_x2w(f16x8 ah, f16x8 al, f16x8 b, f32x4 acc) {
+  acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, b, acc, 0, 0, 0);
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(al, b, acc, 0, 0, 0);
+}
+// depthwise tap on 8 channels as 4 v_pk_fma_f32 (each channel's fma in the same order as scalar fmaf chains)
+__device__ __forceinline__ void dw_tap8(f32x2 a[4], float4 x0, float4 x1, const f32x2 w[4]) {
+  a[0] = __builtin_elementwise_fma(f32x2{x0.x, x0.y}, w[0], a[0]);
+  a[1] = __builtin_elementwise_fma(f32x2{x0.z, x0.w}, w[1], a[1]);
+  a[2] = __builtin_elementwise_fma(f32x2{x1.x, x1.y}, w[2], a[2]);
+  a[3] = __builtin_elementwise_fma(f32x2{x1.z, x1.w}, w[3], a[3]);
+}
+// block I/O element types (IO template bits): fp32, or fp16 where the fp16mx schedule stores a block output in fp16
+constexpr int IO_IN16 = 1, IO_OUT16 = 2;
+__device__ __forceinline__ float4 ld_act4(const void* p, size_t i, bool f16) {   // 4 channels at element i
+  if (f16) {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const _Float16*>(p) + i);
+    return make_float4(h_lo(u.x), h_hi(u.x), h_lo(u.y), h_hi(u.y));
+  }
+  return *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(p) + i);
+}
+__device__ __forceinline__ void st_act4(void* p, size_t i, f32x4 v, bool f16) {
+  if (f16)
+    *reinterpret_cast<uint2*>(reinterpret_cast<_Float16*>(p) + i) =
+        make_uint2(pack_h2((_Float16)v[0], (_Float16)v[1]), pack_h2((_Float16)v[2], (_Float16)v[3]));
+  else
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(p) + i) = make_float4(v[0], v[1], v[2], v[3]);
 }
 
 // Hidden-chunk slab in LDS (fp32): two planes per 32-channel chunk, plane h holding channels 8k + 4h .. 8k + 4h + 3
@@ -88,7 +137,11 @@ struct X2Geom {
   static constexpr int WP = NW / WCO, QPW = POUT16 / WP, NCTW = NCT / WCO;
   static constexpr int EPT = (PIN16 + NW - 1) / NW;   // expand pixel tiles per wave
   static constexpr int DWS = 11 * HIDP;               // staged floats: depthwise [9][HIDP], bias, expand bias
-  static constexpr int LDS_BYTES = (SL::FLOATS + DWS) * 4;
+  static constexpr int TRASH = EXPAND ? 16 * 24 : 0;   // dummy rows: expand stores of invalid input-tile pixels
+  static constexpr int LDS_BYTES = (SL::FLOATS + DWS + TRASH) * 4;
+  // waves per SIMD the LDS allows (workgroups per CU x NW / 4 SIMDs): the VGPR budget is held to it, so registers never
+  // cost occupancy (the 8-wave 16 x 16 tiles: 2 workgroups per CU = 4 waves per SIMD = 128 VGPRs)
+  static constexpr int WAVES_PER_EU = (163840 / LDS_BYTES) * NW / 4 > 8 ? 8 : (163840 / LDS_BYTES) * NW / 4;
   static_assert(CIN % 8 == 0 && COUT % 4 == 0 && HID % 8 == 0, "channel counts");
   static_assert(EXPAND || (CIN == HID && CIN == 32), "t == 1 blocks stage their 32-channel input as the hidden slab");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && NW % WCO == 0 && NCT % WCO == 0, "tile split");
@@ -96,14 +149,22 @@ struct X2Geom {
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO>
-__global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
-    const float* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
+// IO: IO_IN16 = fp16 block input (the fp16mx schedule's early block outputs; the expand's B operand is then exact
+// in fp16, two MFMAs per product), IO_OUT16 = fp16 block output. VALU per hidden value (the slab kernels are
+// VALU-issue bound): the expand epilogue is one v_max (invalid input-tile pixels -- the
+// depthwise's zero padding -- keep the zeros stored once at the start: their lanes store into a dummy LDS row), the
+// depthwise 4.5 v_pk_fma_f32 per 9 taps, ReLU + split 1.5 (v_cvt_pk + v_fma_mix{lo,hi}). Each channel's fma chain is
+// the same as with scalar fmaf, so the IO = 0 results equal the previous form bit for bit.
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, bool RES, int NW, int WCO, int IO = 0>
+__global__ __launch_bounds__(NW * 64) __attribute__((
+    amdgpu_waves_per_eu(X2Geom<CIN, HID, COUT, S, TH, TW, EXPAND, NW, WCO>::WAVES_PER_EU))) void x2_irb_kernel(
+    const void* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
-    const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
+    const float* __restrict__ bp, void* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
     uint32_t nwg) {
   using G = X2Geom<CIN, HID, COUT, S, TH, TW, EXPAND, NW, WCO>;
   using SL = typename G::SL;
+  constexpr bool IN16 = (IO & IO_IN16) != 0, OUT16 = (IO & IO_OUT16) != 0;
   extern __shared__ __attribute__((aligned(16))) char smem[];
   float* Sl = reinterpret_cast<float*>(smem);          // hidden chunk slab (plane layout)
   float* Ds = Sl + SL::FLOATS;                          // [9][HIDP] depthwise weights, [HIDP] bias, [HIDP] expand bias
@@ -117,13 +178,16 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
   const int b = (int)(L / (uint32_t)tiles_y);
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
-  const float* Xb = X + (size_t)b * H * W * CIN;
+  const size_t xb = (size_t)b * H * W * CIN;            // element offset of this image's input
 
   // ---- 1. staging: depthwise weights + biases of every chunk (LDS, once per workgroup); the input tile: B fragments
-  // of this wave's expand pixel tiles pt = wave + NW j (hi / lo, split once, in registers for every chunk), or for
-  // t = 1 the tile itself as the slab. All global loads are issued before the first LDS store.
-  f16x8 bxh[EXPAND ? G::EPT : 1][G::KS], bxl[EXPAND ? G::EPT : 1][G::KS];
+  // of this wave's expand pixel tiles pt = wave + NW j (fp32 input: hi / lo, split once; fp16 input: as loaded), in
+  // registers for every chunk, or for t = 1 the tile itself as the slab. All global loads are issued before the first
+  // LDS store.
+  constexpr int NBX = EXPAND ? G::EPT : 1;
+  f16x8 bxh[NBX][G::KS], bxl[IN16 ? 1 : NBX][G::KS];
   uint32_t pvmask = 0;
+  int soff[NBX];                                        // slab store offset of this lane's pixel (h = 0), or Tr
   {
     constexpr int NDP = G::DWS / 4;                       // float4 pieces of the depthwise stage
     constexpr int NTP = EXPAND ? 0 : G::PINP * 8;         // t = 1: float4 pieces of the 32-channel input tile
@@ -132,22 +196,22 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
       int u = tid + NW * 64 * i;
-      const float* src = nullptr;
+      v[i] = make_float4(0.f, 0.f, 0.f, 0.f);
       if (u < NDP) {
         const int part = u / (G::HIDP / 4), g = u - part * (G::HIDP / 4);
-        if (part < 10 || EXPAND) src = (part < 9 ? Wd + (size_t)part * G::HIDP : part == 9 ? bd : be) + 4 * g;   // t = 1: no be
+        if (part < 10 || EXPAND)                          // t = 1: no be
+          v[i] = *reinterpret_cast<const float4*>((part < 9 ? Wd + (size_t)part * G::HIDP : part == 9 ? bd : be) + 4 * g);
       } else if ((u -= NDP) < NTP) {
         const int p = u >> 3, g = u & 7;
         if (p < G::PIN) {
           const int py = p / G::IW, px = p - py * G::IW;
           const int iy = iy0 + py, ix = ix0 + px;
-          if (iy >= 0 && iy < H && ix >= 0 && ix < W) src = Xb + ((size_t)iy * W + ix) * CIN + 4 * g;
+          if (iy >= 0 && iy < H && ix >= 0 && ix < W) v[i] = ld_act4(X, xb + ((size_t)iy * W + ix) * CIN + 4 * g, IN16);
         }
       }
-      v[i] = src ? *reinterpret_cast<const float4*>(src) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
     if constexpr (EXPAND) {
-      float4 raw[G::EPT][G::KS][2];
+      uint4 raw[G::EPT][G::KS][IN16 ? 1 : 2];
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
         const int p = (wave + NW * j) * 16 + r16;
@@ -160,14 +224,20 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
           ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
         }
         if (ok) pvmask |= 1u << j;
+        soff[j] = ok ? SL::at(p, kg) : SL::FLOATS + G::DWS + r16 * 24 + 4 * kg;
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
           const int ch = 32 * ks + 8 * kg;
-          raw[j][ks][0] = raw[j][ks][1] = make_float4(0.f, 0.f, 0.f, 0.f);
+#pragma unroll
+          for (int u = 0; u < (IN16 ? 1 : 2); ++u) raw[j][ks][u] = make_uint4(0u, 0u, 0u, 0u);
           if (ok && ch < CIN) {
-            const float* src = Xb + ((size_t)iy * W + ix) * CIN + ch;
-            raw[j][ks][0] = *reinterpret_cast<const float4*>(src);
-            raw[j][ks][1] = *reinterpret_cast<const float4*>(src + 4);
+            const size_t e0 = xb + ((size_t)iy * W + ix) * CIN + ch;
+            if constexpr (IN16) {
+              raw[j][ks][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(X) + e0);
+            } else {
+              raw[j][ks][0] = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(X) + e0);
+              raw[j][ks][1] = *reinterpret_cast<const uint4*>(reinterpret_cast<const float*>(X) + e0 + 4);
+            }
           }
         }
       }
@@ -175,10 +245,27 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
       for (int j = 0; j < G::EPT; ++j)
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
-          const float4 a = raw[j][ks][0], c = raw[j][ks][1];
-          const float v8[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-          split8(v8, bxh[j][ks], bxl[j][ks]);
+          if constexpr (IN16) {
+            bxh[j][ks] = __builtin_bit_cast(f16x8, raw[j][ks][0]);
+          } else {
+            const float4 a = __builtin_bit_cast(float4, raw[j][ks][0]), c = __builtin_bit_cast(float4, raw[j][ks][1]);
+            const float v8[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+            split8(v8, bxh[j][ks], bxl[j][ks]);
+          }
         }
+      // invalid pixels (outside the image: the depthwise's zero padding) hold zeros for every chunk: stored once here,
+      // never overwritten (their lanes' expand stores go to the dummy row)
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        const int pt = wave + NW * j;
+        // (tiles past PIN16: the dummy tiles below, nothing to zero)
+        if (pt < G::PIN16 && !((pvmask >> j) & 1u)) {
+          const int p = pt * 16 + r16;
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            *reinterpret_cast<float4*>(Sl + SL::at(p, kg) + 8 * h) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+      }
     }
 #pragma unroll
     for (int i = 0; i < NIT; ++i) {
@@ -250,24 +337,22 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
       for (int ks = 0; ks < G::KS; ++ks)
 #pragma unroll
         for (int j = 0; j < G::EPT; ++j) {
-          if (wave + NW * j >= G::PIN16) break;
 #pragma unroll
-          for (int h = 0; h < 2; ++h) e[j][h] = mfma_x2(eah[h][ks], eal[h][ks], bxh[j][ks], bxl[j][ks], e[j][h]);
+          for (int h = 0; h < 2; ++h) {
+            if constexpr (IN16)
+              e[j][h] = mfma_x2w(eah[h][ks], eal[h][ks], bxh[j][ks], e[j][h]);
+            else
+              e[j][h] = mfma_x2(eah[h][ks], eal[h][ks], bxh[j][ks], bxl[IN16 ? 0 : j][ks], e[j][h]);
+          }
         }
       if (c + 1 < G::NCH) load_ea(c + 1);
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
-        const int pt = wave + NW * j;
-        if (pt >= G::PIN16) break;
-        const bool ok = (pvmask >> j) & 1u;
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          float4 o;
-          o.x = ok ? fmaxf(e[j][h][0], 0.f) : 0.f;
-          o.y = ok ? fmaxf(e[j][h][1], 0.f) : 0.f;
-          o.z = ok ? fmaxf(e[j][h][2], 0.f) : 0.f;
-          o.w = ok ? fmaxf(e[j][h][3], 0.f) : 0.f;
-          *reinterpret_cast<float4*>(Sl + SL::at(pt * 16 + r16, 4 * h + kg)) = o;
+          const float4 o = make_float4(fmaxf(e[j][h][0], 0.f), fmaxf(e[j][h][1], 0.f), fmaxf(e[j][h][2], 0.f),
+                                       fmaxf(e[j][h][3], 0.f));
+          *reinterpret_cast<float4*>(Sl + soff[j] + 8 * h) = o;
         }
       }
       __syncthreads();   // slab of chunk c complete
@@ -275,14 +360,14 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
 
     // ---- depthwise 3x3 (stride S, fp32, kx outer / ky inner) + BN + ReLU of this wave's output pixel tiles,
     // channels 32c + 8kg .. +7 -> hi / lo B fragments -> project accumulation
-    float a[G::QPW][8];
+    f32x2 a[G::QPW][4];
     {
       const float4 d0 = *reinterpret_cast<const float4*>(Ds + 9 * G::HIDP + 32 * c + 8 * kg);
       const float4 d1 = *reinterpret_cast<const float4*>(Ds + 9 * G::HIDP + 32 * c + 8 * kg + 4);
 #pragma unroll
       for (int q = 0; q < G::QPW; ++q) {
-        a[q][0] = d0.x; a[q][1] = d0.y; a[q][2] = d0.z; a[q][3] = d0.w;
-        a[q][4] = d1.x; a[q][5] = d1.y; a[q][6] = d1.z; a[q][7] = d1.w;
+        a[q][0] = f32x2{d0.x, d0.y}; a[q][1] = f32x2{d0.z, d0.w};
+        a[q][2] = f32x2{d1.x, d1.y}; a[q][3] = f32x2{d1.z, d1.w};
       }
     }
 #pragma unroll
@@ -291,24 +376,17 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
       for (int ky = 0; ky < 3; ++ky) {
         const float* wt = Ds + (ky * 3 + kx) * G::HIDP + 32 * c + 8 * kg;
         const float4 w0 = *reinterpret_cast<const float4*>(wt), w1 = *reinterpret_cast<const float4*>(wt + 4);
-        const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+        const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
 #pragma unroll
         for (int q = 0; q < G::QPW; ++q) {
           const int p = pbase[q] + ky * G::IW + kx;
-          const float4 x0 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
-          const float4 x1 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
-          const float x8[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-          for (int e = 0; e < 8; ++e) a[q][e] = fmaf(x8[e], w8[e], a[q][e]);
+          dw_tap8(a[q], *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg)),
+                  *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1)), w4);
         }
       }
     f16x8 bh[G::QPW], bl[G::QPW];
 #pragma unroll
-    for (int q = 0; q < G::QPW; ++q) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) a[q][e] = fmaxf(a[q][e], 0.f);
-      split8(a[q], bh[q], bl[q]);
-    }
+    for (int q = 0; q < G::QPW; ++q) relu_split8(a[q], bh[q], bl[q]);
 #pragma unroll
     for (int t = 0; t < G::NCTW; ++t)
 #pragma unroll
@@ -316,7 +394,7 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
     if (c + 1 < G::NCH) load_pa(c + 1);
   }
 
-  // ---- epilogue: + residual (fp32 block input, pytorch_layers.py:93-96, added after the BN bias) -> fp32 NHWC
+  // ---- epilogue: + residual (the block input, pytorch_layers.py:93-96, added after the BN bias) -> NHWC
 #pragma unroll
   for (int q = 0; q < G::QPW; ++q) {
     const int o = (wp * G::QPW + q) * 16 + r16;
@@ -330,10 +408,10 @@ __global__ __launch_bounds__(NW * 64) void x2_irb_kernel(
       if (co >= COUT) continue;
       f32x4 v = acc[q][t];
       if constexpr (RES) {
-        const float4 r = *reinterpret_cast<const float4*>(X + pix * CIN + co);
+        const float4 r = ld_act4(X, pix * CIN + co, IN16);
         v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
       }
-      *reinterpret_cast<float4*>(Y + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
+      st_act4(Y, pix * COUT + co, v, OUT16);
     }
   }
 }
@@ -373,7 +451,8 @@ struct X2wGeom {
   static constexpr int SD_B = (9 * 32 + 32) * 4;            // depthwise weights [9][32] + depthwise bias
   static constexpr int SP_B = PST ? 2 * NPC * WPS * 2 : 0;
   static constexpr int OFF_SE = 2 * SLAB_B, OFF_SD = OFF_SE + 2 * SE_B, OFF_SP = OFF_SD + 2 * SD_B;
-  static constexpr int LDS_BYTES = OFF_SP + 2 * SP_B;
+  static constexpr int OFF_TR = OFF_SP + 2 * SP_B;          // dummy rows: expand stores of invalid input pixels
+  static constexpr int LDS_BYTES = OFF_TR + 16 * 24 * 4;
   // 16-B stage pieces per chunk
   static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = 9 * 8 + 8, NPP = PST ? 2 * NPC * 4 : 0;
   static constexpr int NPIECE = (NPE + NPD + NPP + NE * 64 - 1) / (NE * 64);
@@ -481,6 +560,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     // this wave's input-tile pixel tiles pt = e + NE j: B fragments (hi / lo) for every K step, loaded and split once
     f16x8 bxh[G::EPT][G::KS], bxl[G::EPT][G::KS];
     uint32_t pvmask = 0;
+    int soff[G::EPT];   // slab store offset (floats) of this lane's pixel, or the dummy rows
     {
       const float* Xb = X + (size_t)b * H * W * CIN;
       float4 raw[G::EPT][G::KS][2];
@@ -496,6 +576,14 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
           ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
         }
         if (ok) pvmask |= 1u << j;
+        soff[j] = ok ? SL::at(p, kg) : G::OFF_TR / 4 + r16 * 24 + 4 * kg;
+        if (!ok && p < G::PINP) {   // zero padding of the depthwise: both slabs, once
+#pragma unroll
+          for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+            for (int h = 0; h < 2; ++h)
+              *reinterpret_cast<float4*>(slab(sb) + SL::at(p, kg) + 8 * h) = make_float4(0.f, 0.f, 0.f, 0.f);
+        }
 #pragma unroll
         for (int ks = 0; ks < G::KS; ++ks) {
           const int ch = 32 * ks + 8 * kg;
@@ -538,26 +626,20 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         }
 #pragma unroll
         for (int j = 0; j < G::EPT; ++j) {
-          if (e + G::NE * j >= G::PIN16) break;
 #pragma unroll
           for (int h = 0; h < 2; ++h) acc[j][h] = mfma_x2(ah[h], al[h], bxh[j][ks], bxl[j][ks], acc[j][h]);
         }
       }
-      float* Sl = slab(k & 1);
+      // valid pixels -> slab k & 1; invalid ones -> the dummy rows (slab offsets are relative to slab 0, the dummy
+      // rows' to the LDS base, which is slab 0)
+      float* Sl = reinterpret_cast<float*>(smem) + ((k & 1) ? G::SLAB_B / 4 : 0);
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
-        const int pt = e + G::NE * j;
-        if (pt >= G::PIN16) break;
-        const bool ok = (pvmask >> j) & 1u;
+        float* dst = ((pvmask >> j) & 1u) ? Sl + soff[j] : reinterpret_cast<float*>(smem) + soff[j];
 #pragma unroll
-        for (int h = 0; h < 2; ++h) {
-          float4 o;
-          o.x = ok ? fmaxf(acc[j][h][0], 0.f) : 0.f;
-          o.y = ok ? fmaxf(acc[j][h][1], 0.f) : 0.f;
-          o.z = ok ? fmaxf(acc[j][h][2], 0.f) : 0.f;
-          o.w = ok ? fmaxf(acc[j][h][3], 0.f) : 0.f;
-          *reinterpret_cast<float4*>(Sl + SL::at(pt * 16 + r16, 4 * h + kg)) = o;
-        }
+        for (int h = 0; h < 2; ++h)
+          *reinterpret_cast<float4*>(dst + 8 * h) = make_float4(fmaxf(acc[j][h][0], 0.f), fmaxf(acc[j][h][1], 0.f),
+                                                                fmaxf(acc[j][h][2], 0.f), fmaxf(acc[j][h][3], 0.f));
       }
     };
     // Stage data is loaded one iteration before it is stored: the pieces of expand chunk c + 2 and depthwise /
@@ -633,14 +715,14 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     for (int c = 0; c < G::NCL; ++c) {
       const float* Sl = slab(c & 1);
       const float* D = sd(c & 1);
-      float a[G::QPW][8];
+      f32x2 a[G::QPW][4];
       {
         const float4 d0 = *reinterpret_cast<const float4*>(D + 288 + 8 * kg);
         const float4 d1 = *reinterpret_cast<const float4*>(D + 288 + 8 * kg + 4);
 #pragma unroll
         for (int q = 0; q < G::QPW; ++q) {
-          a[q][0] = d0.x; a[q][1] = d0.y; a[q][2] = d0.z; a[q][3] = d0.w;
-          a[q][4] = d1.x; a[q][5] = d1.y; a[q][6] = d1.z; a[q][7] = d1.w;
+          a[q][0] = f32x2{d0.x, d0.y}; a[q][1] = f32x2{d0.z, d0.w};
+          a[q][2] = f32x2{d1.x, d1.y}; a[q][3] = f32x2{d1.z, d1.w};
         }
       }
 #pragma unroll
@@ -649,24 +731,17 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         for (int ky = 0; ky < 3; ++ky) {
           const float* wt = D + (ky * 3 + kx) * 32 + 8 * kg;
           const float4 w0 = *reinterpret_cast<const float4*>(wt), w1 = *reinterpret_cast<const float4*>(wt + 4);
-          const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+          const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
 #pragma unroll
           for (int q = 0; q < G::QPW; ++q) {
             const int p = pbase[q] + ky * G::IW + kx;
-            const float4 x0 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
-            const float4 x1 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
-            const float x8[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-            for (int e = 0; e < 8; ++e) a[q][e] = fmaf(x8[e], w8[e], a[q][e]);
+            dw_tap8(a[q], *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg)),
+                    *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1)), w4);
           }
         }
       f16x8 bh[G::QPW], bl[G::QPW];
 #pragma unroll
-      for (int q = 0; q < G::QPW; ++q) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a[q][e] = fmaxf(a[q][e], 0.f);
-        split8(a[q], bh[q], bl[q]);
-      }
+      for (int q = 0; q < G::QPW; ++q) relu_split8(a[q], bh[q], bl[q]);
       if constexpr (PST) {
         const _Float16* Ps = sp(c & 1);
 #pragma unroll
@@ -782,10 +857,13 @@ static hipError_t x2_set_lds(K k, int lds) {   // > 64 KiB dynamic LDS needs the
 }
 
 template <int CIN, int HID, int COUT, int S, bool EXPAND, bool RES, int TH, int TW, int NW, int WCO, int KIND,
-          int P = 1>
+          int P = 1, int IO = 0>
 static hipError_t x2_irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
                             const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
                             hipStream_t s, float* scratch = nullptr) {
+  if constexpr (KIND != 0 && IO != 0) {
+    return hipErrorNotSupported;   // fp16 block I/O: the slab kernels (the fp16mx schedule's blocks 1-7) only
+  }
   const int tiles_x = (OW + TW - 1) / TW, tiles_y = (OH + TH - 1) / TH;
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B * P;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
@@ -793,15 +871,15 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
   static bool attr_set = false;
   if constexpr (KIND == 0) {
     using G = X2Geom<CIN, HID, COUT, S, TH, TW, EXPAND, NW, WCO>;
-    auto k = x2_irb_kernel<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO>;
+    auto k = x2_irb_kernel<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, IO>;
     if (!attr_set) {
       hipError_t e = x2_set_lds(k, G::LDS_BYTES);
       if (e != hipSuccess) return e;
       attr_set = true;
     }
-    k<<<nwg, NW * 64, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
-                                        (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg);
-  } else {
+    k<<<nwg, NW * 64, G::LDS_BYTES, s>>>(x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp, y, H, W, OH, OW,
+                                        tiles_x, tiles_y, nwg);
+  } else if constexpr (IO == 0) {
     static_assert(EXPAND && NW == 8, "role-split blocks expand, 4 + 4 waves");
     using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND == 1, P>;
     auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND == 1, P>;
@@ -834,8 +912,8 @@ bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool 
 
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
-                         int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch) {
-  if (!x || !y || !wd || !bd || !wp || !bp || (expand && (!we || !be))) return hipErrorInvalidValue;
+                         int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch, int io) {
+  if (!x || !y || !wd || !bd || !wp || !bp || (expand && (!we || !be)) || io < 0 || io > 3) return hipErrorInvalidValue;
   int num_cu = 0;
   {
     static int cus = 0;   // (first call per process; the library runs on one device type)
@@ -847,9 +925,20 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
     }
     num_cu = cus;
   }
+#define SPEF_X2_IO_SWITCH(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                    \
+  switch (io) {                                                                                               \
+    case 0: return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, 1, 0>(x, we, be, wd, bd, wp, bp, y, \
+                                                                               B, H, W, OH, OW, s);           \
+    case 1: return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, 1, 1>(x, we, be, wd, bd, wp, bp, y, \
+                                                                               B, H, W, OH, OW, s);           \
+    case 2: return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, 1, 2>(x, we, be, wd, bd, wp, bp, y, \
+                                                                               B, H, W, OH, OW, s);           \
+    default: return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, 1, 3>(x, we, be, wd, bd, wp, bp, y, \
+                                                                                B, H, W, OH, OW, s);          \
+  }
 #define SPEF_X2_TILES(TH_, TW_) ((int64_t)((OW + (TW_)-1) / (TW_)) * ((OH + (TH_)-1) / (TH_)) * B)
 #define SPEF_X2_SMALL(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_)                                    \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && scratch &&         \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && scratch && !io &&  \
       (SPEF_X2_SMALL_ALWAYS || (SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)))     \
     return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
                                                                          OW, s, scratch);
@@ -858,17 +947,16 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
 #define SPEF_X2_EXACT(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                        \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && OH % (TH_) == 0 &&  \
       OW % (TW_) == 0)                                                                                        \
-    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, \
-                                                                     s);
+    SPEF_X2_IO_SWITCH(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)
   SPEF_X2_EXACT_TABLE(SPEF_X2_EXACT)
 #undef SPEF_X2_EXACT
 #undef SPEF_X2_TILES
 #define SPEF_X2_CASE(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                         \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                      \
-    return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, OW, \
-                                                                     s);
+    SPEF_X2_IO_SWITCH(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)
   SPEF_X2_TABLE(SPEF_X2_CASE)
 #undef SPEF_X2_CASE
+#undef SPEF_X2_IO_SWITCH
   return hipErrorNotSupported;
 }
 
@@ -893,15 +981,16 @@ struct X2FrontGeom {
   static constexpr int EPT = (PIN16 + NW - 1) / NW;
   static constexpr int XI_H = (IRW * ICS + 7) / 8 * 8;   // staged input (halves)
   static constexpr int DWS = 9 * 32 + 32;               // block-1 depthwise weights + bias (floats)
-  static constexpr int LDS_BYTES = XI_H * 2 + (SL::FLOATS + DWS) * 4;
+  static constexpr int TRASH = 16 * 24;                 // dummy rows: stem stores of pixels outside the stem map
+  static constexpr int LDS_BYTES = XI_H * 2 + (SL::FLOATS + DWS + TRASH) * 4;
   static_assert(TW == 16 && POUT16 % NW == 0 && EPT <= 32, "front tile");
 };
 
-template <int TH, int TW, int NW_ = 4>
+template <int TH, int TW, int NW_ = 4, bool OUT16 = false>
 __global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ == 4 ? 3 : 4, 8))) void x2_front_kernel(
     const uint8_t* __restrict__ X, const _Float16* __restrict__ Wsx, const float* __restrict__ bs,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
-    const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
+    const float* __restrict__ bp, void* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
     uint32_t nwg) {
   using G = X2FrontGeom<TH, TW, NW_>;
   using SL = typename G::SL;
@@ -1046,15 +1135,20 @@ __global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ ==
   // outermost so one (ky, half) A fragment pair is live at a time
   {
     f32x4 e[G::EPT][2];
-    int xo[G::EPT];
-    bool ok[G::EPT];
+    int xo[G::EPT], soff[G::EPT];
 #pragma unroll
     for (int j = 0; j < G::EPT; ++j) {
       const int p = (wave + NW * j) * 16 + r16;
       const int pc = p < G::PIN ? p : G::PIN - 1;
       const int py = pc / G::PW, px = pc - (pc / G::PW) * G::PW;
       const int sy = sy0 + py, sx = sx0 + px;
-      ok[j] = p < G::PIN && sy >= 0 && sy < OH && sx >= 0 && sx < OW;
+      const bool ok = p < G::PIN && sy >= 0 && sy < OH && sx >= 0 && sx < OW;
+      // pixels outside the stem map (the depthwise's zero padding) get zeros once; their stem results go to a dummy row
+      soff[j] = ok ? SL::at(p, kg) : SL::FLOATS + G::DWS + r16 * 24 + 4 * kg;
+      if (!ok && p < G::PIN) {
+        *reinterpret_cast<float4*>(Sl + SL::at(p, kg)) = make_float4(0.f, 0.f, 0.f, 0.f);
+        *reinterpret_cast<float4*>(Sl + SL::at(p, kg) + 8) = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
       xo[j] = 2 * py * G::ICS + 8 * px + (kg == 1 ? 8 : 0);   // stem pixel px reads input cols 2px .. 2px + 2
 #pragma unroll
       for (int h = 0; h < 2; ++h) e[j][h] = f32x4{sb[h][0], sb[h][1], sb[h][2], sb[h][3]};
@@ -1080,7 +1174,6 @@ __global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ ==
         stem_a(h, ky, ah, al);
 #pragma unroll
         for (int j = 0; j < G::EPT; ++j) {
-          if (wave + NW * j >= G::PIN16) break;
           e[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bx[j], e[j][h], 0, 0, 0);
           e[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bx[j], e[j][h], 0, 0, 0);
         }
@@ -1088,31 +1181,24 @@ __global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ ==
     }
 #pragma unroll
     for (int j = 0; j < G::EPT; ++j) {
-      const int pt = wave + NW * j;
-      if (pt >= G::PIN16) break;
 #pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        float4 o;
-        o.x = ok[j] ? fmaxf(e[j][h][0], 0.f) : 0.f;
-        o.y = ok[j] ? fmaxf(e[j][h][1], 0.f) : 0.f;
-        o.z = ok[j] ? fmaxf(e[j][h][2], 0.f) : 0.f;
-        o.w = ok[j] ? fmaxf(e[j][h][3], 0.f) : 0.f;
-        *reinterpret_cast<float4*>(Sl + SL::at(pt * 16 + r16, 4 * h + kg)) = o;
-      }
+      for (int h = 0; h < 2; ++h)
+        *reinterpret_cast<float4*>(Sl + soff[j] + 8 * h) = make_float4(
+            fmaxf(e[j][h][0], 0.f), fmaxf(e[j][h][1], 0.f), fmaxf(e[j][h][2], 0.f), fmaxf(e[j][h][3], 0.f));
     }
   }
   __syncthreads();
 
   // ---- block 1: depthwise 3x3 (fp32, kx outer / ky inner) + BN + ReLU -> hi / lo -> project 32 -> 16
-  float a[G::QPW][8];
+  f32x2 a[G::QPW][4];
   int pbase[G::QPW];
   {
     const float4 d0 = *reinterpret_cast<const float4*>(Ds + 288 + 8 * kg);
     const float4 d1 = *reinterpret_cast<const float4*>(Ds + 288 + 8 * kg + 4);
 #pragma unroll
     for (int q = 0; q < G::QPW; ++q) {
-      a[q][0] = d0.x; a[q][1] = d0.y; a[q][2] = d0.z; a[q][3] = d0.w;
-      a[q][4] = d1.x; a[q][5] = d1.y; a[q][6] = d1.z; a[q][7] = d1.w;
+      a[q][0] = f32x2{d0.x, d0.y}; a[q][1] = f32x2{d0.z, d0.w};
+      a[q][2] = f32x2{d1.x, d1.y}; a[q][3] = f32x2{d1.z, d1.w};
       const int o = (wave * G::QPW + q) * 16 + r16;
       pbase[q] = (o / TW) * G::PW + (o % TW);
     }
@@ -1123,15 +1209,12 @@ __global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ ==
     for (int ky = 0; ky < 3; ++ky) {
       const float* wt = Ds + (ky * 3 + kx) * 32 + 8 * kg;
       const float4 w0 = *reinterpret_cast<const float4*>(wt), w1 = *reinterpret_cast<const float4*>(wt + 4);
-      const float w8[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+      const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
 #pragma unroll
       for (int q = 0; q < G::QPW; ++q) {
         const int p = pbase[q] + ky * G::PW + kx;
-        const float4 x0 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
-        const float4 x1 = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
-        const float x8[8] = {x0.x, x0.y, x0.z, x0.w, x1.x, x1.y, x1.z, x1.w};
-#pragma unroll
-        for (int e = 0; e < 8; ++e) a[q][e] = fmaf(x8[e], w8[e], a[q][e]);
+        dw_tap8(a[q], *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg)),
+                *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1)), w4);
       }
     }
   const f16x8 ph = *reinterpret_cast<const f16x8*>(Wp + r16 * 32 + 8 * kg);
@@ -1139,15 +1222,12 @@ __global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ ==
   const float4 bb = *reinterpret_cast<const float4*>(bp + 4 * kg);
 #pragma unroll
   for (int q = 0; q < G::QPW; ++q) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) a[q][e] = fmaxf(a[q][e], 0.f);
     f16x8 bh, bl;
-    split8(a[q], bh, bl);
+    relu_split8(a[q], bh, bl);
     const f32x4 v = mfma_x2(ph, pl, bh, bl, f32x4{bb.x, bb.y, bb.z, bb.w});
     const int o = (wave * G::QPW + q) * 16 + r16;
     const int gy = oy0 + o / TW, gx = ox0 + o % TW;
-    if (gy < OH && gx < OW)
-      *reinterpret_cast<float4*>(Y + (((size_t)b * OH + gy) * OW + gx) * 16 + 4 * kg) = make_float4(v[0], v[1], v[2], v[3]);
+    if (gy < OH && gx < OW) st_act4(Y, (((size_t)b * OH + gy) * OW + gx) * 16 + 4 * kg, v, OUT16);
   }
 }
 
@@ -1155,9 +1235,10 @@ __global__ __launch_bounds__(NW_ * 64) __attribute__((amdgpu_waves_per_eu(NW_ ==
 #define SPEF_X2_FRONT_TH 16
 #define SPEF_X2_FRONT_NW 8
 #endif
-hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
-                           const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
-                           hipStream_t s) {
+template <bool OUT16>
+static hipError_t x2_front_go(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
+                              const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
+                              hipStream_t s) {
   constexpr int TH = SPEF_X2_FRONT_TH, TW = 16, NW = SPEF_X2_FRONT_NW;
   using G = X2FrontGeom<TH, TW, NW>;
   if (!x || !wsx || !bs || !wd || !bd || !wp || !bp || !y) return hipErrorInvalidValue;
@@ -1167,14 +1248,20 @@ hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, cons
   const uint32_t nwg = (uint32_t)nwg64;
   static bool attr_set = false;
   if (!attr_set) {
-    hipError_t e = x2_set_lds(x2_front_kernel<TH, TW, NW>, G::LDS_BYTES);
+    hipError_t e = x2_set_lds(x2_front_kernel<TH, TW, NW, OUT16>, G::LDS_BYTES);
     if (e != hipSuccess) return e;
     attr_set = true;
   }
-  x2_front_kernel<TH, TW, NW><<<nwg, NW * 64, G::LDS_BYTES, s>>>((const uint8_t*)x, (const _Float16*)wsx, bs, wd, bd,
-                                                        (const _Float16*)wp, bp, (float*)y, H, W, OH, OW, tiles_x,
-                                                        tiles_y, nwg);
+  x2_front_kernel<TH, TW, NW, OUT16><<<nwg, NW * 64, G::LDS_BYTES, s>>>((const uint8_t*)x, (const _Float16*)wsx, bs,
+                                                                      wd, bd, (const _Float16*)wp, bp, y, H, W, OH, OW,
+                                                                      tiles_x, tiles_y, nwg);
   return hipGetLastError();
+}
+hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
+                           const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
+                           hipStream_t s, bool out16) {
+  return out16 ? x2_front_go<true>(x, wsx, bs, wd, bd, wp, bp, y, B, H, W, OH, OW, s)
+               : x2_front_go<false>(x, wsx, bs, wd, bd, wp, bp, y, B, H, W, OH, OW, s);
 }
 
 // ------------------------------------------------------------------------------------------ 1x1 conv, fp32 I/O

@@ -78,6 +78,7 @@ struct spef_ctx {
   int wavespec = 2;          // SPEF_OPT_WAVESPEC: 2 = pipelined (k_irp.hip), 1 = wave-specialised (k_irw.hip)
   int q8_rolesplit = 0;      // SPEF_OPT_Q8_ROLESPLIT: int8 blocks 8-17 role-split (k_q8irw.hip)
   int test_fail_bcast = 0;   // SPEF_OPT_TEST_FAIL_BCAST (spef_tuning.hpp): failure injection in spef_bcast_weights
+  bool probe_f16 = false;    // run_backbone: the activation it stopped at is fp16 (fp16mx blocks 1-6)
   // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
   std::vector<double> q8_sw, q8_bias;
   std::vector<int32_t> q8_wsum;
@@ -194,7 +195,7 @@ static inline int q8_pool_shift(const spef_ctx* c, int hw) {
 }
 
 size_t elem_size(const spef_ctx* c) {   // int8 | fp16 / bf16 | fp32 activations (fp32 and fp16x2 schedules)
-  return c->hdr.dtype == DT_I8 ? 1 : (c->hdr.dtype == DT_F32 || c->hdr.dtype == DT_X2) ? 4 : 2;
+  return c->hdr.dtype == DT_I8 ? 1 : (c->hdr.dtype == DT_F32 || c->hdr.dtype == DT_X2 || c->hdr.dtype == DT_MX) ? 4 : 2;
 }
 
 // algorithmic HBM bytes of one pointwise launch: read X, write Y (+ read residual), weights + bias once
@@ -243,7 +244,12 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
                  int stop, void** out_buf, int* oc, int* oh, int* ow, float* feat_f32 = nullptr) {
   const int dt = (int)c->hdr.dtype;
   const bool f32 = dt == DT_F32;   // fp32 schedule: one kernel per conv (k_f32.hip), no fused kernels
-  const bool x2 = dt == DT_X2;     // fp16x2 schedule: fp32 activations, fused split-fp16 blocks (k_x2.hip)
+  const bool x2 = dt == DT_X2 || dt == DT_MX;   // fp16x2 kernels: fused split-fp16 blocks (k_x2.hip)
+  // fp16mx: the same kernels and weights; block outputs with <= 32 channels (blocks 1-6: the high-resolution maps,
+  // DESIGN.md section 5) are stored fp16, every other activation fp32
+  const bool mx = dt == DT_MX;
+  auto out16 = [&](const OpDesc& o) { return mx && o.cout <= 32; };
+  bool cur16 = false;                  // the current activation is fp16 (fp16mx early blocks)
   const double es = (f32 || x2) ? 4.0 : 2.0;   // activation bytes per element (profiler byte counts)
   void* cur = nullptr;
   int h = H, w = W, ch = 3;
@@ -273,16 +279,18 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
       const bool front_x2 = x2 && c->fuse && layout == IN_U8_NHWC && !(mode == 1 && stop == 0) && nx &&
                             nx->kind == OP_IRB && nx->cin == 32 && nx->hidden == 32 && nx->cout == 16 &&
                             nx->expand == 1 && nx->stride == 1 && op.cout == 32 && op.x0 != kAbsent;
-      if (front_x2) {   // fp16x2: stem (MFMA, exact u8 operand) + block 1 in one kernel, fp32 output
+      if (front_x2) {   // fp16x2: stem (MFMA, exact u8 operand) + block 1 in one kernel, fp32 (fp16mx: fp16) output
         void* y = c->buf[0];
         const double px = (double)B * OH * OW;
-        HIP_TRY(prof_launch(c, s, "x2_front_kernel<stem+block1>", (double)B * h * w * 3 + px * 16 * 4,
+        const bool o16 = out16(*nx);
+        HIP_TRY(prof_launch(c, s, "x2_front_kernel<stem+block1>", (double)B * h * w * 3 + px * 16 * (o16 ? 2 : 4),
                             px * (2 * 27 * 32 + 18 * 32 + 2 * 32 * 16), [&] {
           return launch_x2_front(input, ptr<void>(c, op.x0), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
                                  ptr<float>(c, nx->b1), ptr<void>(c, nx->w2), ptr<float>(c, nx->b2), y, B, h, w, OH,
-                                 OW, s);
+                                 OW, s, o16);
         }));
         cur = y;
+        cur16 = o16;
         h = OH;
         w = OW;
         ch = (int)nx->cout;
@@ -332,7 +340,10 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const double flops = 2.0 * M * op.cin * op.hidden * (expand ? 1 : 0) + 18.0 * M2 * op.hidden +
                              2.0 * M2 * op.hidden * op.cout;
         const double hp = (op.hidden + 31) & ~31u;
-        const double bytes = (double)M * op.cin * 4 + (double)M2 * op.cout * 4 * (res ? 2 : 1) +
+        const bool o16 = out16(op);
+        const int io = (cur16 ? 1 : 0) | (o16 ? 2 : 0);
+        const double ib = cur16 ? 2 : 4, ob = o16 ? 2 : 4;
+        const double bytes = (double)M * op.cin * ib + (double)M2 * op.cout * (ob + (res ? ib : 0)) +
                              (expand ? hp * ((op.cin + 31) & ~31u) * 4 : 0) + hp * 48 +
                              ((op.cout + 15) & ~15u) * (hp * 4 + 4);
         char key[96];
@@ -342,9 +353,10 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
           return launch_x2_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
                                ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
                                ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s,
-                               (float*)pick({x, y}));
+                               (float*)pick({x, y}), io);
         }));
         cur = y;
+        cur16 = o16;
         h = OH;
         w = OW;
         ch = (int)op.cout;
@@ -488,6 +500,7 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
     if (mode == 1 && op_index == stop) break;
     ++op_index;
   }
+  c->probe_f16 = cur16;
   if (out_buf) *out_buf = cur;
   if (oc) *oc = ch;
   if (oh) *oh = h;
@@ -756,7 +769,8 @@ static void op_extents(const OpDesc& op, uint32_t dtype, uint64_t ext[9]) {
   const uint64_t rq = 20;                                 // int64 M + int64 B + int32 S per channel
   for (int i = 0; i < 9; ++i) ext[i] = 0;
   const uint64_t ci = op.cin, co = op.cout, h = op.hidden;
-  if (dtype == DT_X2) {   // fp16x2: 1x1 weights as [2][rows][Kp] fp16 planes (hi, lo); depthwise / biases padded to 32
+  if (dtype == DT_X2 || dtype == DT_MX) {   // fp16x2 / fp16mx: 1x1 weights as [2][rows][Kp] fp16 planes (hi, lo);
+                                            // depthwise / biases padded to 32
     switch (op.kind) {
       case OP_STEM: ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * 3 * co * 32 * 2; break;
       case OP_IRB:
@@ -804,7 +818,8 @@ static int parse_blob(const uint8_t* head_bytes, size_t meta_bytes, size_t bytes
   memcpy(&h, head_bytes, sizeof(h));
   if (memcmp(h.magic, kBlobMagic, 8) != 0) return fail(SPEF_ERR_BLOB, "bad blob magic");
   if (h.version != kBlobVersion) return fail(SPEF_ERR_BLOB, "unsupported blob version");
-  if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8 && h.dtype != DT_F32 && h.dtype != DT_X2)
+  if (h.dtype != DT_F16 && h.dtype != DT_BF16 && h.dtype != DT_I8 && h.dtype != DT_F32 && h.dtype != DT_X2 &&
+      h.dtype != DT_MX)
     return fail(SPEF_ERR_BLOB, "unsupported blob dtype");
   if (h.n_ops == 0 || h.n_ops > 4096) return fail(SPEF_ERR_BLOB, "bad op count");
   // every term bounded on its own before any sum (a crafted ops_off near 2^64 must not wrap ops_end)
@@ -1382,7 +1397,8 @@ int spef_probe(spef_ctx* c, const void* input, int layout, int B, int H, int W, 
   } else {
     rc = run_backbone(c, input, layout, B, H, W, s, 1, stop_op, &act, &ch, &h, &w);
     if (rc) return rc;
-    HIP_TRY(launch_to_f32((int)c->hdr.dtype, act, out, (int64_t)B * h * w * ch, s));
+    const int adt = c->hdr.dtype == DT_MX ? (c->probe_f16 ? (int)DT_F16 : (int)DT_F32) : (int)c->hdr.dtype;
+    HIP_TRY(launch_to_f32(adt, act, out, (int64_t)B * h * w * ch, s));
   }
   if (oc) *oc = ch;
   if (oh) *oh = h;

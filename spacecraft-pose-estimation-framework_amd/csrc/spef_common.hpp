@@ -13,6 +13,7 @@ typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef __bf16 bf16x4 __attribute__((ext_vector_type(4)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 
 // Element-type traits: the MFMA used for a 16x16 output tile with K = 32 per instruction.
 // gfx950 lane map (cdna_hip_programming.md §3): A[i = l&15][k = 8(l>>4)+e], B[k = 8(l>>4)+e][j = l&15],

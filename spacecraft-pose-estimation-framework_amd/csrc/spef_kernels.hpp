@@ -11,7 +11,11 @@ namespace spef {
 // Sets the calling thread's spef_last_error() message and returns `code` (spef_api.cpp).
 int report_error(int code, const std::string& msg);
 
-enum Dtype : int { DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3, DT_F32 = 4, DT_X2 = 5 /* fp32 I/O, split-fp16 MFMA (k_x2.hip) */ };
+enum Dtype : int {
+  DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3, DT_F32 = 4,
+  DT_X2 = 5,   // fp32 I/O, split-fp16 MFMA (k_x2.hip)
+  DT_MX = 6    // fp16mx: the fp16x2 kernels and weights, block outputs with <= 32 channels (blocks 1-6) stored fp16
+};
 enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RELU_F32 = 3 /* ReLU, fp32 output */ };
 enum InLayout : int { IN_U8_NHWC = 0, IN_F32_NCHW = 1 };
 
@@ -86,12 +90,15 @@ const char* gemm_f32_key(int N);
 // wd fp32 [9][r32(hid)], bd fp32 [r32(hid)], wp [2][r16(cout)][r32(hid)] fp16, bp fp32 [r16(cout)]; zero padded.
 bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
 // scratch (nullable): B * OH * OW * cout * 2 floats for the hidden-split form of the late blocks on small maps.
+// io: bit 0 = fp16 input x, bit 1 = fp16 output y (the fp16mx schedule; slab-kernel geometries, blocks 1-7, only).
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
-                         int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch = nullptr);
-// uint8 NHWC frames -> stem + block 1 -> fp32 [B][OH][OW][16] (x2_front_kernel); wsx: blob OP_STEM x0 of dtype 5.
+                         int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch = nullptr, int io = 0);
+// uint8 NHWC frames -> stem + block 1 -> [B][OH][OW][16] (x2_front_kernel), fp32 or (out16) fp16; wsx: blob OP_STEM
+// x0 of dtype 5 / 6.
 hipError_t launch_x2_front(const void* x, const void* wsx, const float* bs, const float* wd, const float* bd,
-                           const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s);
+                           const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW, hipStream_t s,
+                           bool out16 = false);
 // 1x1 conv + BN + ReLU on fp32 activations X [M][K] with wt [2][Np][Kp] fp16 (hi, lo) -> fp32 Y [M][N]; Np % 64 == 0.
 hipError_t launch_x2_pw_relu(const void* x, const void* wt, const float* bias, float* y, int64_t M, int K, int N,
                              hipStream_t s);

@@ -16,6 +16,10 @@ planes [2][rows][Kp], hi = fp16(w) and lo = fp16(w - hi) of the float64 folded w
 rows padded to 32; depthwise weights fp32 [9][H32] and the hidden-width biases padded to H32 = hidden rounded up to
 32 (zeros), so the kernel never masks a channel; the stem's /255-folded MFMA operand x0 as [2][3 ky][32][32] hi / lo
 planes with k = 4 kx + ci (the front kernel's fragment order).
+
+``fp16mx`` (dtype 6, the headline schedule): the fp16x2 layout and kernels; the schedule stores the block outputs
+with <= 32 channels (blocks 1-6, the high-resolution maps) in fp16 and every other activation in fp32
+(tools/precision_budget.py: 4.0e-4 max |d logit| at head std 0.3 against 1.3e-2 for the fp16 schedule).
 """
 from __future__ import annotations
 
@@ -28,8 +32,10 @@ from .arch import Arch, BN_EPS, ConvSpec, LAST_CHANNELS, arch_from_state_dict, m
 
 MAGIC = b'SPEFMI35'
 VERSION = 2   # 2: fp16 stem MFMA operand in the front_vp_kernel row-triple k order (csrc/spef_blob.hpp)
-DTYPES = {'fp16': 1, 'bf16': 2, 'fp32': 4, 'fp16x2': 5}   # fp32: the reference's own arithmetic (k_f32.hip);
-# fp16x2: fp32 activations with hi + lo fp16 MFMA operands (k_x2.hip)
+DTYPES = {'fp16': 1, 'bf16': 2, 'fp32': 4, 'fp16x2': 5, 'fp16mx': 6}   # fp32: the reference's own arithmetic
+# (k_f32.hip); fp16x2: fp32 activations with hi + lo fp16 MFMA operands (k_x2.hip); fp16mx: the same weights,
+# fp16 block outputs on blocks 1-6
+X2_DTYPES = ('fp16x2', 'fp16mx')   # the split-fp16 weight layout
 DT_I8 = 3
 OP_STEM, OP_IRB, OP_LAST, OP_FC, OP_FCKP = 1, 2, 3, 4, 5
 OP_QSTEM, OP_QIRB, OP_QLAST, OP_QFC = 11, 12, 13, 14
@@ -165,7 +171,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
                 hi[:, k] = w255[ky * 9 + j]
     else:
         hi[:, :27] = w255.T
-    if dtype == 'fp16x2':   # x2_front_kernel's operand: [plane][ky][32 ch][32 k], k = 4 kx + ci (k >= 12 zero)
+    if dtype in X2_DTYPES:   # x2_front_kernel's operand: [plane][ky][32 ch][32 k], k = 4 kx + ci (k >= 12 zero)
         a = np.zeros((3, arch.stem.cout, 32), np.float64)
         for ky in range(3):
             for kx in range(3):
@@ -181,7 +187,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
 
     for blk in arch.blocks:
         convs = list(blk.convs)
-        if dtype == 'fp16x2':
+        if dtype in X2_DTYPES:
             hp = (blk.hidden + 31) // 32 * 32
             e = (ABSENT, ABSENT)
             if blk.expand != 1:
@@ -199,7 +205,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
         ops.append((OP_IRB, blk.cin, blk.cout, blk.hidden, blk.stride, blk.expand, 1 if blk.residual else 0,
                     e[0], e[1], d[0], d[1], p[0], p[1]))
 
-    if dtype == 'fp16x2':
+    if dtype in X2_DTYPES:
         lw, lb = _pw_x2(*fold_bn(sd, arch.last), data, (arch.last.cout + 15) // 16 * 16)
     else:
         lw, lb = _pw_tensor(*fold_bn(sd, arch.last), dtype, data)

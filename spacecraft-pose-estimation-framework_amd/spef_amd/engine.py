@@ -42,6 +42,9 @@ class Engine:
         self.ctx = h
         self._reserved = (0, 0, 0)
         self._decode_tables = None
+        # bumped by every call that moves device buffers or changes what a recorded forward / decode would do
+        # (workspace reallocation, weights, decode tables, options, camera): StreamPipeline's recorded HIP graphs key on it
+        self.epoch = 0
         self.head = self.n_out0 = self.n_out1 = self.n_ops = None
         self.dtype = None
         if blob is not None:
@@ -68,9 +71,10 @@ class Engine:
         L.check(self.lib.spef_model_info(self.ctx, C.byref(head), C.byref(n0), C.byref(n1), C.byref(dt),
                                          C.byref(nops)))
         self.head, self.n_out0, self.n_out1 = head.value, n0.value, n1.value
-        self.dtype = {1: 'fp16', 2: 'bf16', 3: 'int8', 4: 'fp32', 5: 'fp16x2'}[dt.value]
+        self.dtype = {1: 'fp16', 2: 'bf16', 3: 'int8', 4: 'fp32', 5: 'fp16x2', 6: 'fp16mx'}[dt.value]
         self.n_ops = nops.value
         self._reserved = (0, 0, 0)
+        self.epoch += 1
 
     def reserve(self, B: int, H: int, W: int) -> None:
         rb, rh, rw = self._reserved
@@ -78,6 +82,7 @@ class Engine:
             return
         L.check(self.lib.spef_reserve(self.ctx, B, H, W))
         self._reserved = (B, H, W)
+        self.epoch += 1
 
     def set_decode_tables(self, ori_bins: Optional[np.ndarray], pos_grid: Optional[np.ndarray]) -> None:
         ob = None if ori_bins is None else np.ascontiguousarray(ori_bins, np.float64)
@@ -86,6 +91,7 @@ class Engine:
             self.ctx, None if ob is None else ob.ctypes.data_as(C.c_void_p), 0 if ob is None else ob.shape[0],
             None if pg is None else pg.ctypes.data_as(C.c_void_p), 0 if pg is None else pg.shape[0]))
         self._decode_tables = (ob, pg)
+        self.epoch += 1
 
     # ------------------------------------------------------------------ compute
     @staticmethod
@@ -162,6 +168,7 @@ class Engine:
 
     def set_option(self, option: int, value: int) -> None:
         L.check(self.lib.spef_set_option(self.ctx, option, int(value)))
+        self.epoch += 1
 
     def set_keypoints(self, kp3d: np.ndarray, K: np.ndarray, nu: float, nv: float, dist=None) -> None:
         """Keypoint-mode camera: 3-D model points, K, image size; ``dist`` = the camera's distCoeffs (k1, k2, p1,
@@ -173,6 +180,7 @@ class Engine:
         dd = np.zeros(0) if dist is None else np.ascontiguousarray(np.asarray(dist, np.float64).reshape(-1))
         L.check(self.lib.spef_set_keypoint_distortion(self.ctx, dd.ctypes.data_as(C.c_void_p) if dd.size else None,
                                                       int(dd.size)))
+        self.epoch += 1
         self._kp = (kp, kk, dd)
 
     def decode_keypoints(self, raw: torch.Tensor, apply_sigmoid: bool = True):

@@ -11,7 +11,10 @@ runs ``SPETorch.predict`` batch after batch; each submitted batch is still the c
 
 ``use_graphs()`` (optional) records each (stream, input batch) pair's forward + decode once as a HIP graph and
 replays it on later submits of the same input tensor: one graph launch per batch instead of ~20 kernel launches.
-Its decode outputs then live in the graph's memory and are overwritten when that pair is submitted again.
+Its decode outputs then live in the graph's memory and are overwritten when that pair is submitted again. A recorded
+graph holds fixed device addresses (the engine's workspace, the stream's output buffers, the decode tables), so its
+key carries the engine's ``epoch`` (bumped by every workspace reallocation and state change) and the output buffers'
+addresses, and a stream's graphs are dropped as soon as either moves.
 """
 from __future__ import annotations
 
@@ -71,6 +74,7 @@ class StreamPipeline:
             buf = (torch.empty((B, eng.n_out0), dtype=torch.float32, device=self.device),
                    torch.empty((B, eng.n_out1), dtype=torch.float32, device=self.device) if eng.n_out1 else None)
             self._bufs[i] = buf
+            self._drop_graphs(i)                                 # recorded against the previous buffers
         s.wait_stream(torch.cuda.current_stream(self.device))   # frames were produced on the caller's stream
         if self.graphs:
             return self._submit_graph(i, eng, s, buf, frames, ori_mode, pos_mode, want_soft)
@@ -80,11 +84,23 @@ class StreamPipeline:
             dec = eng.decode(ori_mode, pos_mode, raw0, raw1, want_soft=want_soft)
             ev = torch.cuda.Event()
             ev.record(s)
+        dec['raw0'], dec['raw1'] = raw0, raw1
         dec['event'] = ev
         return dec
 
+    def _drop_graphs(self, i: int) -> None:
+        for k in [k for k in self._graphs if k[0] == i]:
+            del self._graphs[k]
+
     def _submit_graph(self, i, eng, s, buf, frames, ori_mode, pos_mode, want_soft) -> dict:
-        key = (i, frames.data_ptr(), tuple(frames.shape), frames.dtype, ori_mode, pos_mode, want_soft)
+        _, B, H, W = eng._layout(frames)
+        eng.reserve(B, H, W)                                     # any reallocation happens before the key is taken
+        bufkey = tuple(0 if t is None else t.data_ptr() for t in buf)
+        key = (i, frames.data_ptr(), tuple(frames.shape), frames.dtype, ori_mode, pos_mode, want_soft, eng.epoch,
+               bufkey)
+        stale = [k for k in self._graphs if k[0] == i and (k[7] != eng.epoch or k[8] != bufkey)]
+        for k in stale:                                          # their workspace / buffers may be freed memory now
+            del self._graphs[k]
         ent = self._graphs.get(key)
         if ent is None:
             with torch.cuda.stream(s):   # one eager pass first: lazily set kernel attributes stay out of the capture
@@ -103,6 +119,7 @@ class StreamPipeline:
             ev = torch.cuda.Event()
             ev.record(s)
         dec = dict(dec0)
+        dec['raw0'], dec['raw1'] = buf
         dec['event'] = ev
         return dec
 
