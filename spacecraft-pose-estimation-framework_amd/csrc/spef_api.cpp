@@ -79,6 +79,7 @@ struct spef_ctx {
   int q8_rolesplit = 0;      // SPEF_OPT_Q8_ROLESPLIT: int8 blocks 8-17 role-split (k_q8irw.hip)
   int test_fail_bcast = 0;   // SPEF_OPT_TEST_FAIL_BCAST (spef_tuning.hpp): failure injection in spef_bcast_weights
   bool probe_f16 = false;    // run_backbone: the activation it stopped at is fp16 (fp16mx blocks 1-6)
+  int mx_kernels = 1;        // SPEF_OPT_MX_KERNELS (spef_tuning.hpp): fp16mx blocks 2-7 on k_mx.hip
   // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
   std::vector<double> q8_sw, q8_bias;
   std::vector<int32_t> q8_wsum;
@@ -283,8 +284,14 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         void* y = c->buf[0];
         const double px = (double)B * OH * OW;
         const bool o16 = out16(*nx);
-        HIP_TRY(prof_launch(c, s, "x2_front_kernel<stem+block1>", (double)B * h * w * 3 + px * 16 * (o16 ? 2 : 4),
-                            px * (2 * 27 * 32 + 18 * 32 + 2 * 32 * 16), [&] {
+        const bool mxf = mx && o16 && c->mx_kernels && op.x1 != kAbsent;
+        HIP_TRY(prof_launch(c, s, mxf ? "mx_front_kernel<stem+block1>" : "x2_front_kernel<stem+block1>",
+                            (double)B * h * w * 3 + px * 16 * (o16 ? 2 : 4), px * (2 * 27 * 32 + 18 * 32 + 2 * 32 * 16),
+                            [&] {
+          if (mxf)
+            return launch_mx_front(input, ptr<void>(c, op.x1), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
+                                   ptr<float>(c, nx->b1), ptr<void>(c, nx->w2), ptr<float>(c, nx->b2), y, B, h, w, OH,
+                                   OW, s);
           return launch_x2_front(input, ptr<void>(c, op.x0), ptr<float>(c, op.b0), ptr<float>(c, nx->w1),
                                  ptr<float>(c, nx->b1), ptr<void>(c, nx->w2), ptr<float>(c, nx->b2), y, B, h, w, OH,
                                  OW, s, o16);
@@ -347,8 +354,15 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
                              (expand ? hp * ((op.cin + 31) & ~31u) * 4 : 0) + hp * 48 +
                              ((op.cout + 15) & ~15u) * (hp * 4 + 4);
         char key[96];
-        snprintf(key, sizeof(key), "x2_irb_kernel<%u,%u,%u,s%u>", op.cin, op.hidden, op.cout, op.stride);
+        const bool mxk = mx && cur16 && c->mx_kernels &&
+                         mx_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, o16);
+        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", mxk ? "mx_irb_kernel" : "x2_irb_kernel", op.cin, op.hidden,
+                 op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
+          if (mxk)
+            return launch_mx_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, o16, x,
+                                 ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
+                                 ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
           // a third activation buffer (each holds the largest map) is the hidden-split form's partial-sum scratch
           return launch_x2_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, x,
                                ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
@@ -772,7 +786,10 @@ static void op_extents(const OpDesc& op, uint32_t dtype, uint64_t ext[9]) {
   if (dtype == DT_X2 || dtype == DT_MX) {   // fp16x2 / fp16mx: 1x1 weights as [2][rows][Kp] fp16 planes (hi, lo);
                                             // depthwise / biases padded to 32
     switch (op.kind) {
-      case OP_STEM: ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * 3 * co * 32 * 2; break;
+      case OP_STEM:
+        ext[0] = 27 * co * 4; ext[1] = co * 4; ext[6] = 2 * 3 * co * 32 * 2;
+        if (dtype == DT_MX) ext[7] = 2 * co * 32 * 2;   // front_mx_kernel's operand (row-triple k order)
+        break;
       case OP_IRB:
         if (op.expand != 1) { ext[0] = 2 * r32(h) * r32(ci) * 2; ext[1] = r32(h) * 4; }
         ext[2] = 9 * r32(h) * 4; ext[3] = r32(h) * 4;
@@ -1708,6 +1725,10 @@ int spef_set_option(spef_ctx* c, int option, int value) {
   if (option == SPEF_OPT_Q8_ROLESPLIT) {
     if (value < 0 || value > 1) return fail(SPEF_ERR_ARG, "SPEF_OPT_Q8_ROLESPLIT: 0 or 1");
     c->q8_rolesplit = value;
+    return SPEF_OK;
+  }
+  if (option == SPEF_OPT_MX_KERNELS) {   // spef_tuning.hpp
+    c->mx_kernels = value ? 1 : 0;
     return SPEF_OK;
   }
   if (option == SPEF_OPT_WAVESPEC) {

@@ -7,11 +7,14 @@
 //   SPEF_OPT_TEST_FAIL_BCAST: failure injection for spef_bcast_weights tests: 1 = this rank fails its local check
 //                         before the data broadcast, 2 = fails staging after it, 3 = the header wait never completes
 //                         (exercises the timeout -> ncclCommAbort path without a hung peer). 0 = off.
+//   SPEF_OPT_MX_KERNELS : fp16mx blocks 2-7 on the dedicated kernels of k_mx.hip (1, default) or on the fp16x2 slab
+//                         kernels with fp16 block I/O (0).
 #pragma once
 
 enum spef_tuning_option {
   SPEF_OPT_FUSE_MIN_HW = 2,
   SPEF_OPT_PW_GEMM = 3,
   SPEF_OPT_IRB_VARIANT = 4,
-  SPEF_OPT_TEST_FAIL_BCAST = 5
+  SPEF_OPT_TEST_FAIL_BCAST = 5,
+  SPEF_OPT_MX_KERNELS = 8
 };

@@ -36,11 +36,11 @@ CXXFLAGS = ['-O3', '-fPIC', '-std=c++17', f'--offload-arch={ARCH}', '-Wall', '-W
 # compiler emit a single v_max_f32 per ReLU instead of canonicalize + max (~18 % fewer VALU ops in the fused
 # block loop). Decode / EPnP keep IEEE NaN semantics (they detect NaNs, classification_utils.py:134).
 NO_NAN_SOURCES = {'k_irb.hip', 'k_irw.hip', 'k_irp.hip', 'k_front.hip', 'k_conv.hip', 'k_gemm.hip', 'k_pool.hip',
-                  'k_x2.hip'}
+                  'k_x2.hip', 'k_mx.hip'}
 # The SLP vectorizer packs the depthwise FMAs into v_pk_fma_f32 with explicit fp16->fp32 converts (in the fused
 # block kernels as soon as their outputs are converted pairwise); scalar v_fma_mix_f32 (fp16 operands read in place)
 # is fewer instructions, and every fp32 VALU op costs the same 4 cycles (profiles/r01_valu_rate.txt).
-NO_SLP_SOURCES = {'k_irb.hip', 'k_irw.hip', 'k_irp.hip', 'k_front.hip'}
+NO_SLP_SOURCES = {'k_irb.hip', 'k_irw.hip', 'k_irp.hip', 'k_front.hip', 'k_mx.hip'}
 
 
 def lib_path() -> str:

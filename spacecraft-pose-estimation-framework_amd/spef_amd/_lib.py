@@ -16,6 +16,7 @@ ABI_VERSION = 3
 COMM_ID_BYTES = 128
 OPT_FUSE_BLOCKS, OPT_WAVESPEC, OPT_Q8_ROLESPLIT = 1, 6, 7     # public schedule options (include/spef.h)
 OPT_FUSE_MIN_HW, OPT_PW_GEMM, OPT_IRB_VARIANT, OPT_TEST_FAIL_BCAST = 2, 3, 4, 5   # internal (csrc/spef_tuning.hpp)
+OPT_MX_KERNELS = 8   # internal: fp16mx blocks 2-7 on k_mx.hip (1) or the fp16x2 slab kernels (0)
 
 # name -> (restype, argtypes); keep in sync with include/spef.h (tests/test_abi.py checks the header)
 _vp, _i, _sz = C.c_void_p, C.c_int, C.c_size_t

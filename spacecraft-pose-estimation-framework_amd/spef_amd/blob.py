@@ -17,9 +17,10 @@ rows padded to 32; depthwise weights fp32 [9][H32] and the hidden-width biases p
 32 (zeros), so the kernel never masks a channel; the stem's /255-folded MFMA operand x0 as [2][3 ky][32][32] hi / lo
 planes with k = 4 kx + ci (the front kernel's fragment order).
 
-``fp16mx`` (dtype 6, the headline schedule): the fp16x2 layout and kernels; the schedule stores the block outputs
-with <= 32 channels (blocks 1-6, the high-resolution maps) in fp16 and every other activation in fp32
-(tools/precision_budget.py: 4.0e-4 max |d logit| at head std 0.3 against 1.3e-2 for the fp16 schedule).
+``fp16mx`` (dtype 6, the headline schedule): the fp16x2 layout, plus the stem operand in the fp16 front kernel's
+row-triple k order as a second tensor (x1, hi / lo [2][32][32]); the schedule stores the stem map, the block
+outputs of blocks 1-6 and the hidden tensors of blocks 2-7 in fp16 and every other activation in fp32, with every
+weight exact (tools/precision_budget.py: ~5e-4 max |d logit| at head std 0.3 against 1.3e-2 for the fp16 schedule).
 """
 from __future__ import annotations
 
@@ -162,7 +163,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
     # j = 2 c + h = kx*3 + ci of input row ky (j = 9 and d = 15 are zero-weight pads)
     w255 = ws / np.float32(255.0)
     hi = np.zeros((arch.stem.cout, 32), np.float32)
-    if dtype == 'fp16':
+    if dtype in ('fp16', 'fp16mx'):
         for k in range(30):
             d, h = divmod(k, 2)
             c, ky = divmod(d, 3)
@@ -171,6 +172,7 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
                 hi[:, k] = w255[ky * 9 + j]
     else:
         hi[:, :27] = w255.T
+    x1 = None
     if dtype in X2_DTYPES:   # x2_front_kernel's operand: [plane][ky][32 ch][32 k], k = 4 kx + ci (k >= 12 zero)
         a = np.zeros((3, arch.stem.cout, 32), np.float64)
         for ky in range(3):
@@ -178,12 +180,15 @@ def pack(sd: Dict, arch: Optional[Arch] = None, dtype: str = 'fp16', kp_feat_hw=
                 for ci in range(3):
                     a[ky, :, 4 * kx + ci] = w255[ky * 9 + kx * 3 + ci]
         x0 = np.concatenate(split_f16(a)).tobytes()
+        if dtype == 'fp16mx':   # + the fp16 front kernel's row-triple k order, hi / lo [2][32][32] (front_mx_kernel)
+            x1 = data.add(np.concatenate(split_f16(hi)).tobytes())
     else:
         hi_r = _round_act(hi, dtype)
         x0 = _to_act(np.concatenate([hi_r, _round_act(hi - hi_r, dtype)]), dtype)
-    ops.append((OP_STEM, 3, arch.stem.cout, 0, 2, 1, 0,
-                data.add(ws.tobytes()), data.add(np.asarray(b, np.float32).tobytes()), ABSENT, ABSENT, ABSENT, ABSENT,
-                data.add(x0)))
+    stem = (OP_STEM, 3, arch.stem.cout, 0, 2, 1, 0,
+            data.add(ws.tobytes()), data.add(np.asarray(b, np.float32).tobytes()), ABSENT, ABSENT, ABSENT, ABSENT,
+            data.add(x0))
+    ops.append(stem if x1 is None else stem + (x1,))
 
     for blk in arch.blocks:
         convs = list(blk.convs)

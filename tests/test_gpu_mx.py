@@ -1,7 +1,7 @@
 """GPU: the fp16mx schedule (blob dtype 6) -- the headline: the fp16x2 kernels and weights (hi + lo fp16 MFMA
-operands, fp32 accumulation, fp32 depthwise) with the block outputs of blocks 1-6 stored fp16 and every other
-activation fp32 (tools/precision_budget.py: 4.0e-4 max |d logit| at head std 0.3 in float64, against 1.3e-2 for the
-fp16 schedule).
+operands, fp32 accumulation, fp32 depthwise) with the block outputs of blocks 1-6 and the hidden tensors of blocks
+2-7 stored fp16 and every other activation fp32 (tools/precision_budget.py: 4.9e-4 max |d logit| at head std 0.3 in
+float64, 16 frames, against 1.3e-2 for the fp16 schedule).
 
 Tolerances are the north star's, absolute, with no scaling by the head's weight scale: raw head outputs 1e-3,
 orientation < 0.1 deg, position < 1 mm -- at the reference init (std 0.01) and at a sharp head (std 0.3, the
@@ -25,6 +25,7 @@ POS_TOL_M = 1e-3
 ORI_TOL_DEG = 0.1
 MX_GOLDEN_TOL = 2e-4  # reference init (std 0.01): ~30x below the sharp-head figure (measured, printed below)
 F16_BLOCKS = range(1, 7)   # blocks whose output the schedule stores in fp16 (cout <= 32)
+F16_HIDDEN = range(2, 8)   # blocks whose expanded hidden tensor the schedule stores in fp16 (csrc/k_mx.hip)
 
 
 def _frames(b, h, w, seed):
@@ -41,7 +42,8 @@ def _sharp_sd():
 
 def _oracle_block(x, sd, idx):
     """features.features[idx] of the oracle (oracle/model_ref.py: the reference's float32 arithmetic, op for op) on
-    the activation x; idx 0 = the stem."""
+    the activation x, with the schedule's fp16 hidden storage of blocks 2-7 restated (the expand output rounded to
+    fp16 before the depthwise); idx 0 = the stem."""
     fp = 'features.features'
     if idx == 0:
         return M._conv_bn_act(x, sd, f'{fp}.0', 2, 1, True)
@@ -53,6 +55,8 @@ def _oracle_block(x, sd, idx):
                 y, j = x, 0
                 if t != 1:
                     y = M._conv_bn_act(y, sd, f'{fp}.{idx}.conv.{j}', 1, 1, True)
+                    if idx in F16_HIDDEN:
+                        y = y.half().float()
                     j += 1
                 y = M._conv_bn_act(y, sd, f'{fp}.{idx}.conv.{j}', stride, int(round(cin * t)), True)
                 y = M._conv_bn_act(y, sd, f'{fp}.{idx}.conv.{j + 1}', 1, 1, False)
@@ -82,7 +86,9 @@ def test_blob_layout(sd):
     dt = C.c_int()
     L.check(L.load().spef_validate_blob(C.create_string_buffer(b, len(b)), len(b), C.byref(dt), None, None, None))
     assert dt.value == 6
-    assert b[128:] == Bl.pack(sd, dtype='fp16x2')[128:]   # same tensors and op table as fp16x2; the header differs
+    ops = Bl.describe(b)['ops']
+    assert ops[0][0] == Bl.OP_STEM and ops[0][15] != Bl.ABSENT   # + the front kernel's row-triple stem operand (x1)
+    assert [o[:7] for o in ops] == [o[:7] for o in Bl.describe(Bl.pack(sd, dtype='fp16x2'))['ops']]
 
 
 @pytest.mark.parametrize('name', ['fwd_64x64_b2.npz', 'fwd_240x384_b1.npz', 'fwd_512x512_b1.npz'])
@@ -98,10 +104,11 @@ def test_forward_vs_reference_golden(mx, golden, name):
 @pytest.mark.parametrize('b,h,w', [(2, 96, 128), (1, 100, 136)])
 def test_block_outputs_vs_oracle(mx, sd, b, h, w):
     """Every block kernel (ragged maps: partial tiles) against the oracle's block applied to the GPU's own input for
-    that block (the previous probe), so each kernel is checked on its own: blocks 1-6 store fp16, so the oracle's
+    that block (the previous probe), so each kernel is checked on its own, with the schedule's fp16 storage points
+    restated in the oracle (hidden tensors of blocks 2-7, outputs of blocks 1-6): blocks 1-6 store fp16, so the oracle's
     output is rounded to fp16 too and the two may differ by one fp16 rounding step where the exact value sits next to a
-    rounding boundary (bound 1.2e-3 of the map's max: one ulp is at most 2^-10 of it); blocks 7-17 keep fp32 (the
-    fp16x2 bound, 5e-5 of the map's max). Block 1 runs fused with the stem (front kernel) and is compared from the
+    rounding boundary (bound 1.2e-3 of the map's max: one ulp is at most 2^-10 of it); block 7 (fp16 hidden, fp32 out)
+    2e-4; blocks 8-17 keep fp32 throughout (the fp16x2 bound, 5e-5 of the map's max). Block 1 runs fused with the stem (front kernel) and is compared from the
     frames."""
     fr = _frames(b, h, w, 5 + h)
     x = M.u8_nhwc_to_nchw_f32(fr)
@@ -125,7 +132,9 @@ def test_block_outputs_vs_oracle(mx, sd, b, h, w):
             prev = got
     print('block output error / map max:', {k: f'{v:.1e}' for k, v in errs.items()})
     for op, err in errs.items():
-        assert err < (1.2e-3 if op in F16_BLOCKS else 5e-5), (op, err)
+        # fp16 output: one fp16 step; block 7 (fp16 hidden, fp32 output): the hidden tensor's rare one-step rounding
+        # differences (values within ~1e-7 of a rounding boundary) carried through depthwise and project; fp32: fp16x2
+        assert err < (1.2e-3 if op in F16_BLOCKS else 2e-4 if op in F16_HIDDEN else 5e-5), (op, err)
 
 
 def test_sharp_head_logits_absolute():

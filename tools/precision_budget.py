@@ -152,14 +152,28 @@ SCHEDULES = {
     'mx O1-6 H2-7': mixed([((1, 6), 'O'), ((2, 7), 'H')]),
     'mx O1-6 H2-7 S': mixed([((1, 6), 'O'), ((2, 7), 'H'), ((0, 0), 'S')]),
     'mx O1-7 H2-7 S': mixed([((1, 7), 'O'), ((2, 7), 'H'), ((0, 0), 'S')]),
+    'mx O1-6 H247': mixed([((1, 6), 'O'), ((2, 2), 'H'), ((4, 4), 'H'), ((7, 7), 'H')]),
+    'mx O1-6 H247 S': mixed([((1, 6), 'O'), ((2, 2), 'H'), ((4, 4), 'H'), ((7, 7), 'H'), ((0, 0), 'S')]),
+    'mx O1-3 H2-7 S': mixed([((1, 3), 'O'), ((2, 7), 'H'), ((0, 0), 'S')]),
+    'mx O1-4 H2-7 S': mixed([((1, 4), 'O'), ((2, 7), 'H'), ((0, 0), 'S')]),
+    'mx O1-2 H2-7 S': mixed([((1, 2), 'O'), ((2, 7), 'H'), ((0, 0), 'S')]),
+    'mx O1-3 H2-4 S': mixed([((1, 3), 'O'), ((2, 4), 'H'), ((0, 0), 'S')]),
 }
+
+
+def test_frames(b, h, w, seed):
+    """tests/test_gpu_mx.py's blocky random frames (FRAMES=test)."""
+    rng = np.random.Generator(np.random.PCG64(seed))
+    base = rng.integers(0, 40, (b, h, w, 1), dtype=np.uint8)
+    blob = rng.integers(0, 215, (b, h // 4, w // 4, 1), dtype=np.uint8).repeat(4, 1).repeat(4, 2)
+    return np.repeat(np.clip(base.astype(np.int32) + blob, 0, 255).astype(np.uint8), 3, axis=3)
 
 
 def setup(n, s, hs=0.3):
     torch.set_num_threads(8)
     arch = mobilenet_v2('ursonet', 1728, 3)
     sd = synthetic_state_dict(arch, seed=1001, head_std=hs, pos_std=0.01, pos_bias=(0.3, -0.2, 12.0))
-    fr = synth_frames(n, s, s, 10_000)
+    fr = test_frames(n, s, s, 77) if os.environ.get('FRAMES') == 'test' else synth_frames(n, s, s, 10_000)
     x = torch.from_numpy(fr).permute(0, 3, 1, 2).to(torch.float64) / 255.0
     return Net(sd, arch), x
 
