@@ -463,6 +463,9 @@ struct X2wGeom {
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
+#ifndef SPEF_X2_ABL_STAGE
+#define SPEF_X2_ABL_STAGE 0
+#endif
 // P > 1 (hidden split): the P workgroups of a tile each run NCH / P consecutive hidden chunks and store their
 // project partial sums (no bias, no residual) to Y + part * pstride; x2_split_reduce_kernel adds the P parts in order,
 // the bias and the residual. Small maps get P times the workgroups while every workgroup streams only 1 / P of the
@@ -647,6 +650,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     // LDS at the start of iteration c (the same buffers and barriers as a load-and-store in iteration c).
     uint4 v[G::NPIECE];
     auto load_stage = [&](int c) {
+#if SPEF_X2_ABL_STAGE < 2   // timing ablation only (wrong results): 2 = no stage loads
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
         const void* src;
@@ -654,8 +658,10 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
         v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
       }
+#endif
     };
     auto store_stage = [&](int c) {
+#if SPEF_X2_ABL_STAGE < 1   // timing ablation only (wrong results): 1 = no stage stores
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
         const void* src;
@@ -663,6 +669,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
         if (src) *reinterpret_cast<uint4*>(dst) = v[i];
       }
+#endif
     };
     load_stage(0);
     __syncthreads();                 // prologue stages visible

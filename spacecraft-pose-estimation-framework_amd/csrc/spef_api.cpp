@@ -246,10 +246,10 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
   const int dt = (int)c->hdr.dtype;
   const bool f32 = dt == DT_F32;   // fp32 schedule: one kernel per conv (k_f32.hip), no fused kernels
   const bool x2 = dt == DT_X2 || dt == DT_MX;   // fp16x2 kernels: fused split-fp16 blocks (k_x2.hip)
-  // fp16mx: the same kernels and weights; block outputs with <= 32 channels (blocks 1-6: the high-resolution maps,
-  // DESIGN.md section 5) are stored fp16, every other activation fp32
+  // fp16mx: the same weights; the block outputs with <= 24 channels (blocks 1-3: the 256^2 / 128^2 maps, DESIGN.md
+  // section 5) are stored fp16, every other block output fp32
   const bool mx = dt == DT_MX;
-  auto out16 = [&](const OpDesc& o) { return mx && o.cout <= 32; };
+  auto out16 = [&](const OpDesc& o) { return mx && o.cout <= 24; };
   bool cur16 = false;                  // the current activation is fp16 (fp16mx early blocks)
   const double es = (f32 || x2) ? 4.0 : 2.0;   // activation bytes per element (profiler byte counts)
   void* cur = nullptr;
@@ -354,13 +354,14 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
                              (expand ? hp * ((op.cin + 31) & ~31u) * 4 : 0) + hp * 48 +
                              ((op.cout + 15) & ~15u) * (hp * 4 + 4);
         char key[96];
-        const bool mxk = mx && cur16 && c->mx_kernels &&
-                         mx_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, o16);
+        const bool mxk = mx && c->mx_kernels &&
+                         mx_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, cur16,
+                                          o16);
         snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", mxk ? "mx_irb_kernel" : "x2_irb_kernel", op.cin, op.hidden,
                  op.cout, op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
           if (mxk)
-            return launch_mx_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, o16, x,
+            return launch_mx_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, cur16, o16, x,
                                  ptr<void>(c, op.w0), ptr<float>(c, op.b0), ptr<float>(c, op.w1), ptr<float>(c, op.b1),
                                  ptr<void>(c, op.w2), ptr<float>(c, op.b2), y, B, h, w, OH, OW, s);
           // a third activation buffer (each holds the largest map) is the hidden-split form's partial-sum scratch

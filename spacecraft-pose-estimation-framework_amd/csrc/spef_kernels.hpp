@@ -94,10 +94,11 @@ bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool 
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
                          int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch = nullptr, int io = 0);
-// fp16mx blocks 2-7 (k_mx.hip): fp16 input, hi + lo fp16 weights (blob dtype 5 / 6 layout), fp16 hidden slab, fp32
-// depthwise, hi + lo project operand; fp16 (out16) or fp32 output.
-bool mx_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res, bool out16);
-hipError_t launch_mx_irb(int cin, int hid, int cout, int stride, bool res, bool out16, const void* x, const void* we,
+// fp16mx blocks 2-7 (k_mx.hip): fp16 (in16) or fp32 input, hi + lo fp16 weights (blob dtype 5 / 6 layout), fp16
+// hidden slab, fp32 depthwise, hi + lo project operand; fp16 (out16) or fp32 output.
+bool mx_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res, bool in16, bool out16);
+hipError_t launch_mx_irb(int cin, int hid, int cout, int stride, bool res, bool in16, bool out16, const void* x,
+                         const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
                          int B, int H, int W, int OH, int OW, hipStream_t s);
 // fp16mx front (k_mx.hip front_mx_kernel): uint8 NHWC -> stem + block 1 -> fp16 [B][OH][OW][16]; wsp = OP_STEM x1.

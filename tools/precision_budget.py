@@ -158,6 +158,10 @@ SCHEDULES = {
     'mx O1-4 H2-7 S': mixed([((1, 4), 'O'), ((2, 7), 'H'), ((0, 0), 'S')]),
     'mx O1-2 H2-7 S': mixed([((1, 2), 'O'), ((2, 7), 'H'), ((0, 0), 'S')]),
     'mx O1-3 H2-4 S': mixed([((1, 3), 'O'), ((2, 4), 'H'), ((0, 0), 'S')]),
+    'mx O1-3 H2-3 S': mixed([((1, 3), 'O'), ((2, 3), 'H'), ((0, 0), 'S')]),
+    'mx O1-3 H2-7': mixed([((1, 3), 'O'), ((2, 7), 'H')]),
+    'mx O1-2 H2-4 S': mixed([((1, 2), 'O'), ((2, 4), 'H'), ((0, 0), 'S')]),
+    'mx O1-3 H247 S': mixed([((1, 3), 'O'), ((2, 2), 'H'), ((4, 4), 'H'), ((7, 7), 'H'), ((0, 0), 'S')]),
 }
 
 
