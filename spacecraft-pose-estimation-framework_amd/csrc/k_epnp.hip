@@ -2,7 +2,7 @@
 // (src/spe/keypoints_utils.py:112-150) = cv2.solvePnP(SOLVEPNP_EPNP) -> Rodrigues -> dcm2quat (spe/utils.py:56-118),
 // including solvePnP's undistortPoints for cameras with lens distortion (SPEED+, data/datasets/speed_plus.py:18-40).
 //
-// One 64-lane wave per problem, fp64; the algorithm is OpenCV 4.5.5 epnp.cpp's (the reference's pinned OpenCV):
+// One 3-wave workgroup per problem, fp64; the algorithm is OpenCV 4.5.5 epnp.cpp's (the reference's pinned OpenCV):
 // PCA control points, barycentric alphas, M (2n x 12), the 4 eigenvectors of M^T M with the smallest
 // eigenvalues, L_6x10 / rho, beta approximations 1/2/3 (least squares), 5 Gauss-Newton steps (Householder
 // QR), R|t by Procrustes with OpenCV's sign fixes, lowest mean reprojection error wins. Symmetric
@@ -17,6 +17,52 @@
 namespace spef {
 
 #define EPNP_MAXN 16
+
+// Jacobi rotation (c, s) annihilating a_pq: theta = (a_qq - a_pp) / (2 a_pq), t = sign(theta) / (|theta| +
+// sqrt(theta^2 + 1)), c = 1 / sqrt(t^2 + 1), s = t c. The reciprocals and square roots are the hardware fp64
+// estimates (v_rcp_f64 / v_rsq_f64) refined by Newton steps instead of the IEEE-correct library sequences (scaling,
+// fixup): a rotation only has to be orthogonal to fp64 precision, not correctly rounded, and these four operations are
+// the serial latency of every Jacobi round (the rounds are ~55 % of the kernel, tools/epnp_time.py ablations).
+__device__ __forceinline__ double rcp_nr(double x) {
+  double r = __builtin_amdgcn_rcp(x);
+  r = fma(r, fma(-x, r, 1.0), r);
+  return fma(r, fma(-x, r, 1.0), r);
+}
+__device__ __forceinline__ double rsq_nr(double x) {   // x > 0
+  double r = __builtin_amdgcn_rsq(x);
+  const double h = 0.5 * x;
+  r = r * fma(-h * r, r, 1.5);
+  return r * fma(-h * r, r, 1.5);
+}
+#ifndef SPEF_EPNP_ROT32
+#define SPEF_EPNP_ROT32 0
+#endif
+#ifndef SPEF_EPNP_ROTLOCAL
+#define SPEF_EPNP_ROTLOCAL 0
+#endif
+__device__ __forceinline__ void jacobi_rot(double app, double aqq, double apq, double& c, double& s) {
+#if SPEF_EPNP_ROT32   // the angle in fp32 (fast rcp / sqrt), the rotation itself orthogonal to fp64 for that angle
+  {
+    const float th = (float)(aqq - app) * __builtin_amdgcn_rcpf((float)(2.0 * apq));
+    const float tf = (th >= 0 ? 1.0f : -1.0f) * __builtin_amdgcn_rcpf(fabsf(th) + __builtin_sqrtf(th * th + 1.0f));
+    const double t = (double)tf;
+    c = rsq_nr(t * t + 1.0);
+    s = t * c;
+    return;
+  }
+#endif
+  const double theta = (aqq - app) * rcp_nr(2.0 * apq);
+  double t;
+  if (fabs(theta) > 1e100) {                             // sqrt(theta^2 + 1) = |theta| to fp64: t = 1 / (2 theta)
+    t = 0.5 * rcp_nr(theta);
+  } else {
+    const double t2 = theta * theta + 1.0;
+    const double sq = t2 * rsq_nr(t2);                   // sqrt(theta^2 + 1)
+    t = (theta >= 0 ? 1.0 : -1.0) * rcp_nr(fabs(theta) + sq);
+  }
+  c = rsq_nr(t * t + 1.0);
+  s = t * c;
+}
 
 // cyclic Jacobi on a symmetric N x N: a is destroyed (diagonal = eigenvalues), v = eigenvectors (columns)
 template <int N>
@@ -34,9 +80,8 @@ __device__ void jacobi_sym(double (&a)[N][N], double (&v)[N][N]) {
       for (int q = p + 1; q < N; ++q) {
         const double apq = a[p][q];
         if (fabs(apq) < 1e-300) continue;
-        const double theta = (a[q][q] - a[p][p]) / (2.0 * apq);
-        const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-        const double c = 1.0 / sqrt(t * t + 1.0), s = t * c;
+        double c, s;
+        jacobi_rot(a[p][p], a[q][q], apq, c, s);
         for (int k = 0; k < N; ++k) {
           const double akp = a[k][p], akq = a[k][q];
           a[k][p] = c * akp - s * akq;
@@ -147,14 +192,16 @@ __device__ __forceinline__ void undistort_point(const EpnpDist& d, double fu, do
   v_out = (double)(float)y * fv + vc;
 }
 
-// ---- one wave per problem ----
-// Lane i < n holds point i (its 3-D point, undistorted pixel, barycentric alphas); the 12 x 12 symmetric eigenproblem
-// of M^T M runs as a parallel (tournament-ordered) cyclic Jacobi in LDS: each of the 11 rounds of a sweep applies 6
-// disjoint rotations at once, every lane updating 2-3 of the 144 entries of A and of V (A' = J^T A J, V' = V J with J
-// the product of the round's rotations), double-buffered. The small fixed-size steps (L_6x10, betas, Gauss-Newton,
-// 3x3 Procrustes) run uniformly on every lane; the per-point sums (pcs centroid, the Procrustes cross-covariance,
-// the reprojection error) are wave reductions. Latency per problem is what this buys: the former one-thread-per-
-// problem kernel took ~2 ms for any batch (its 12x12 Jacobi indexed private arrays dynamically: scratch memory).
+// ---- one 3-wave workgroup per problem ----
+// Every wave's lane i < n holds point i (its 3-D point, undistorted pixel, barycentric alphas). The 12 x 12 symmetric
+// eigenproblem of M^T M runs as a parallel (tournament-ordered) cyclic Jacobi in LDS: each of the 11 rounds of a sweep
+// applies 6 disjoint rotations at once (wave 0's lanes 0..11 compute them), thread e < 144 updating entry e of A and of
+// V (A' = J^T A J, V' = V J with J the product of the round's rotations), double-buffered. The three beta
+// approximations of epnp.cpp compute_pose are independent: wave w runs approximation w + 1 (L_6x10 betas, 5
+// Gauss-Newton steps, R|t by Procrustes, mean reprojection error) on its own lanes, and the lowest error wins (ties:
+// the lower approximation, as epnp.cpp). The small fixed-size steps run uniformly on every lane of a wave; the per-point
+// sums are wave reductions. Latency per problem is what all this buys (a B = 64 batch is 64 concurrent problems):
+// one wave per problem took 134 us per launch, the former one-thread-per-problem kernel ~2 ms.
 
 // partner of index i in round r of the 12-player round robin: pairs (r, 11) and (r + k, r - k) mod 11, k = 1..5
 __device__ __forceinline__ int rr_partner(int r, int i) {
@@ -163,21 +210,24 @@ __device__ __forceinline__ int rr_partner(int r, int i) {
   return (2 * r - i + 22) % 11;
 }
 
-__global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw, int B, int n,
-                                                  const float* __restrict__ kp3d, const double* __restrict__ model,
-                                                  double fu, double fv, double uc,
-                                                  double vc, float nu, float nv, EpnpDist dist, int apply_sigmoid,
-                                                  float* __restrict__ kp_out, float* __restrict__ quat,
-                                                  float* __restrict__ pos, int* __restrict__ status) {
+__global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw, int B, int n,
+                                                   const float* __restrict__ kp3d, const double* __restrict__ model,
+                                                   double fu, double fv, double uc,
+                                                   double vc, float nu, float nv, EpnpDist dist, int apply_sigmoid,
+                                                   float* __restrict__ kp_out, float* __restrict__ quat,
+                                                   float* __restrict__ pos, int* __restrict__ status) {
   __shared__ double As[2][144], Vs[2][144];
   __shared__ double Cc[12], Cs[12];
   __shared__ double Pal[EPNP_MAXN][4], Pdu[EPNP_MAXN], Pdv[EPNP_MAXN];
+  __shared__ double Red[3][2];
+  __shared__ double Ls[6][10], Rho[6];
+  __shared__ double Res[3][13];   // per approximation: error, R (9), t (3)
   const int b = blockIdx.x;
-  const int lane = threadIdx.x;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (b >= B) return;   // uniform per workgroup
   const int nk = 2 * (n + 1);
 
-  // ---- points: lane i <= n reads raw point i (origin first); lane j < n then owns keypoint j
+  // ---- points: lane i <= n reads raw point i (origin first); lane j < n then owns keypoint j (every wave)
   double uu = 0.0, vv = 0.0;
   if (lane <= n) {
     float x = raw[(size_t)b * nk + 2 * lane], y = raw[(size_t)b * nk + 2 * lane + 1];
@@ -185,7 +235,7 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
       x = 1.0f / (1.0f + expf(-x));
       y = 1.0f / (1.0f + expf(-y));
     }
-    if (kp_out) {
+    if (kp_out && wave == 0) {
       kp_out[(size_t)b * nk + 2 * lane] = x;
       kp_out[(size_t)b * nk + 2 * lane + 1] = y;
     }
@@ -200,10 +250,12 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
     for (int k = 0; k < 3; ++k) pw[k] = (double)kp3d[3 * lane + k];
 #pragma unroll
     for (int k = 0; k < 4; ++k) al[k] = model[12 + 4 * lane + k];
+    if (wave == 0) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) Pal[lane][k] = al[k];
-    Pdu[lane] = uc - us0;
-    Pdv[lane] = vc - us1;
+      for (int k = 0; k < 4; ++k) Pal[lane][k] = al[k];
+      Pdu[lane] = uc - us0;
+      Pdv[lane] = vc - us1;
+    }
   }
   double cws[4][3];   // control points (model-only, spef_set_keypoints)
 #pragma unroll
@@ -212,72 +264,85 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
     for (int j = 0; j < 3; ++j) cws[i][j] = model[3 * i + j];
   __syncthreads();
 
-  // ---- M^T M (M never stored): entry e = (p, q) accumulated point by point as r1[p] r1[q] + r2[p] r2[q]
-#pragma unroll
-  for (int s = 0; s < 3; ++s) {
-    const int e = lane + 64 * s;
-    if (e < 144) {
-      const int p = e / 12, q = e - 12 * (e / 12);
-      const int cp = p / 3, dp = p - 3 * cp, cq = q / 3, dq = q - 3 * cq;
-      double acc = 0.0;
-      for (int i = 0; i < n; ++i) {
-        const double ap = Pal[i][cp], aq = Pal[i][cq];
-        const double r1p = dp == 0 ? ap * fu : dp == 2 ? ap * Pdu[i] : 0.0;
-        const double r1q = dq == 0 ? aq * fu : dq == 2 ? aq * Pdu[i] : 0.0;
-        const double r2p = dp == 1 ? ap * fv : dp == 2 ? ap * Pdv[i] : 0.0;
-        const double r2q = dq == 1 ? aq * fv : dq == 2 ? aq * Pdv[i] : 0.0;
-        acc += r1p * r1q + r2p * r2q;
-      }
-      As[0][e] = acc;
-      Vs[0][e] = p == q ? 1.0 : 0.0;
+  // ---- M^T M (M never stored): entry e = (p, q) = thread e, accumulated point by point as r1[p] r1[q] + r2[p] r2[q]
+  const int e = tid;
+  const bool ent = e < 144;
+  const int ei = e / 12, ej = e - 12 * (e / 12);
+  if (ent) {
+    const int cp = ei / 3, dp = ei - 3 * cp, cq = ej / 3, dq = ej - 3 * cq;
+    double acc = 0.0;
+    for (int i = 0; i < n; ++i) {
+      const double ap = Pal[i][cp], aq = Pal[i][cq];
+      const double r1p = dp == 0 ? ap * fu : dp == 2 ? ap * Pdu[i] : 0.0;
+      const double r1q = dq == 0 ? aq * fu : dq == 2 ? aq * Pdu[i] : 0.0;
+      const double r2p = dp == 1 ? ap * fv : dp == 2 ? ap * Pdv[i] : 0.0;
+      const double r2q = dq == 1 ? aq * fv : dq == 2 ? aq * Pdv[i] : 0.0;
+      acc += r1p * r1q + r2p * r2q;
     }
+    As[0][e] = acc;
+    Vs[0][e] = ei == ej ? 1.0 : 0.0;
   }
   __syncthreads();
 
   // ---- parallel cyclic Jacobi (tournament order): sweeps of 11 rounds x 6 disjoint rotations
+#ifndef SPEF_EPNP_ABL   // timing ablations only (wrong results): 1 = no Jacobi sweeps, 2 = approximation 1 only
+#define SPEF_EPNP_ABL 0
+#endif
   int cur = 0;
-  for (int sweep = 0; sweep < 40; ++sweep) {
+  for (int sweep = 0; sweep < (SPEF_EPNP_ABL == 1 ? 0 : 40); ++sweep) {
     double off = 0.0, diag = 0.0;
-#pragma unroll
-    for (int s = 0; s < 3; ++s) {
-      const int e = lane + 64 * s;
-      if (e < 144) {
-        const double a = As[cur][e];
-        if (e / 12 == e - 12 * (e / 12)) diag += a * a;
-        else if (e / 12 < e - 12 * (e / 12)) off += a * a;
-      }
+    if (ent) {
+      const double a = As[cur][e];
+      if (ei == ej) diag = a * a;
+      else if (ei < ej) off = a * a;
     }
     off = warp_sum_d(off);
     diag = warp_sum_d(diag);
-    if (off <= 1e-32 * diag || off == 0.0) break;
+    if (lane == 0) {
+      Red[wave][0] = off;
+      Red[wave][1] = diag;
+    }
+    __syncthreads();
+    off = Red[0][0] + Red[1][0] + Red[2][0];
+    diag = Red[0][1] + Red[1][1] + Red[2][1];
+#ifndef SPEF_EPNP_JTOL
+#define SPEF_EPNP_JTOL 1e-32
+#endif
+    if (off <= SPEF_EPNP_JTOL * diag || off == 0.0) break;   // uniform: every thread read the same sums
     for (int r = 0; r < 11; ++r) {
-      if (lane < 12) {   // lane i: the rotation of its pair, its own signed coefficient
-        const int j = rr_partner(r, lane);
-        const int p = lane < j ? lane : j, q = lane < j ? j : lane;
+#if SPEF_EPNP_ROTLOCAL   // every thread computes the two rotations it applies (one barrier per round instead of two)
+      const int i2 = rr_partner(r, ei), j2 = rr_partner(r, ej);
+      auto coef = [&](int i, int j, double& c, double& sg) {   // index i's signed coefficient of pair (i, j)
+        const int p = i < j ? i : j, q = i < j ? j : i;
+        const double apq = As[cur][12 * p + q];
+        double sn = 0.0;
+        c = 1.0;
+        if (fabs(apq) >= 1e-300) jacobi_rot(As[cur][13 * p], As[cur][13 * q], apq, c, sn);
+        sg = i == p ? -sn : sn;
+      };
+      if (ent) {
+        double ci, si, cj, sj;
+        coef(ei, i2, ci, si);
+        coef(ej, j2, cj, sj);
+#else
+      if (tid < 12) {   // thread i: the rotation of its pair, its own signed coefficient
+        const int j = rr_partner(r, tid);
+        const int p = tid < j ? tid : j, q = tid < j ? j : tid;
         const double apq = As[cur][12 * p + q];
         double c = 1.0, sn = 0.0;
-        if (fabs(apq) >= 1e-300) {
-          const double theta = (As[cur][13 * q] - As[cur][13 * p]) / (2.0 * apq);
-          const double t = (theta >= 0 ? 1.0 : -1.0) / (fabs(theta) + sqrt(theta * theta + 1.0));
-          c = 1.0 / sqrt(t * t + 1.0);
-          sn = t * c;
-        }
-        Cc[lane] = c;
-        Cs[lane] = lane == p ? -sn : sn;
+        if (fabs(apq) >= 1e-300) jacobi_rot(As[cur][13 * p], As[cur][13 * q], apq, c, sn);
+        Cc[tid] = c;
+        Cs[tid] = tid == p ? -sn : sn;
       }
       __syncthreads();
-#pragma unroll
-      for (int s = 0; s < 3; ++s) {
-        const int e = lane + 64 * s;
-        if (e < 144) {
-          const int i = e / 12, j = e - 12 * (e / 12);
-          const int i2 = rr_partner(r, i), j2 = rr_partner(r, j);
-          const double ci = Cc[i], si = Cs[i], cj = Cc[j], sj = Cs[j];
-          const double* a = As[cur];
-          As[cur ^ 1][e] = ci * (cj * a[12 * i + j] + sj * a[12 * i + j2]) + si * (cj * a[12 * i2 + j] + sj * a[12 * i2 + j2]);
-          const double* v = Vs[cur];
-          Vs[cur ^ 1][e] = cj * v[12 * i + j] + sj * v[12 * i + j2];
-        }
+      if (ent) {
+        const int i2 = rr_partner(r, ei), j2 = rr_partner(r, ej);
+        const double ci = Cc[ei], si = Cs[ei], cj = Cc[ej], sj = Cs[ej];
+#endif
+        const double* a = As[cur];
+        As[cur ^ 1][e] = ci * (cj * a[12 * ei + ej] + sj * a[12 * ei + j2]) + si * (cj * a[12 * i2 + ej] + sj * a[12 * i2 + j2]);
+        const double* v = Vs[cur];
+        Vs[cur ^ 1][e] = cj * v[12 * ei + ej] + sj * v[12 * ei + j2];
       }
       cur ^= 1;
       __syncthreads();
@@ -303,12 +368,11 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
     idx[i] = bi;
     used |= 1u << bi;
   }
-  // ut4[i][k] = V[k][idx[i]] stays in LDS (read as broadcasts); L_6x10 rows and rho by lanes 0..5 into LDS
-  __shared__ double Ls[6][10], Rho[6];
+  // ut4[i][k] = V[k][idx[i]] stays in LDS (read as broadcasts); L_6x10 rows and rho by threads 0..5 into LDS
   const double* Vf = Vs[cur];
   auto ut4 = [&](int i, int k) { return Vf[12 * k + idx[i]]; };
-  if (lane < 6) {
-    const int r = lane;
+  if (tid < 6) {
+    const int r = tid;
     const int pa = r < 3 ? 0 : r < 5 ? 1 : 2, pb = r < 3 ? r + 1 : r < 5 ? r - 1 : 3;
     double dv[4][3];
 #pragma unroll
@@ -344,9 +408,9 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
 #pragma unroll
   for (int k = 0; k < 3; ++k) pw0[k] = warp_sum_d(pw[k]) / n;
 
-  double bestR[3][3] = {}, bestT[3] = {}, bestE = INFINITY;
-#pragma unroll 1
-  for (int ap = 1; ap <= 3; ++ap) {
+  // ---- approximation ap = wave + 1 (epnp.cpp compute_pose: find_betas_approx_1/2/3 + gauss_newton + compute_R_and_t)
+  const int ap = wave + 1;
+  if (SPEF_EPNP_ABL != 2 || ap == 1) {
     double be[4] = {0, 0, 0, 0};
     double rr[6];
 #pragma unroll
@@ -457,18 +521,33 @@ __global__ __launch_bounds__(64) void epnp_kernel(const float* __restrict__ raw,
       const double ue = uc + fu * xc * iz, ve = vc + fv * yc * iz;
       err = sqrt((us0 - ue) * (us0 - ue) + (us1 - ve) * (us1 - ve));
     }
-    const double e = warp_sum_d(err) / n;
-    if (e < bestE) {   // strict: ties keep the lower approximation index (epnp.cpp compute_pose)
-      bestE = e;
+    const double em = warp_sum_d(err) / n;
+    if (lane == 0) {
+      Res[wave][0] = em;
 #pragma unroll
       for (int i = 0; i < 3; ++i) {
-        bestT[i] = t[i];
 #pragma unroll
-        for (int j = 0; j < 3; ++j) bestR[i][j] = R[i][j];
+        for (int j = 0; j < 3; ++j) Res[wave][1 + 3 * i + j] = R[i][j];
+        Res[wave][10 + i] = t[i];
       }
     }
+  } else if (lane == 0) {
+    Res[wave][0] = INFINITY;
   }
-  if (lane != 0) return;
+  __syncthreads();
+  if (tid != 0) return;
+  int bw = 0;   // lowest mean reprojection error; strict, so ties keep the lower approximation (epnp.cpp compute_pose)
+  double bestE = Res[0][0];
+  for (int w = 1; w < 3; ++w)
+    if (Res[w][0] < bestE) {
+      bestE = Res[w][0];
+      bw = w;
+    }
+  double bestR[3][3], bestT[3];
+  for (int i = 0; i < 3; ++i) {
+    for (int j = 0; j < 3; ++j) bestR[i][j] = Res[bw][1 + 3 * i + j];
+    bestT[i] = Res[bw][10 + i];
+  }
   // dcm2quat (spe/utils.py:56-118, Spurrier)
   const double m11 = bestR[0][0], m12 = bestR[0][1], m13 = bestR[0][2];
   const double m21 = bestR[1][0], m22 = bestR[1][1], m23 = bestR[1][2];
@@ -502,7 +581,7 @@ hipError_t launch_epnp(const float* raw, int B, int n, const float* kp3d, const 
                        float nu, float nv, const EpnpDist& dist, int apply_sigmoid, float* kp_out, float* quat,
                        float* pos, int* status, hipStream_t s) {
   if (n < 4 || n > EPNP_MAXN) return hipErrorInvalidValue;
-  epnp_kernel<<<B, 64, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, dist, apply_sigmoid, kp_out,
+  epnp_kernel<<<B, 192, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, dist, apply_sigmoid, kp_out,
                                 quat, pos, status);
   return hipGetLastError();
 }

@@ -26,7 +26,7 @@ def test_config_merge_and_validation(tmp_path):
     p.write_text(EXP_YAML)
     cfg = load_config(str(p))
     assert cfg.DATA.IMG_SIZE == (240, 384) and cfg.DATA.BATCH_SIZE == 32 and cfg.MODEL.PRETRAINED_PATH is None
-    assert cfg.TRAIN.MILESTONES == (35, 45) and cfg.MI355X.DTYPE == 'fp16'
+    assert cfg.TRAIN.MILESTONES == (35, 45) and cfg.MI355X.DTYPE == 'fp16mx'
     save_config(cfg, str(tmp_path / 'again.yaml'))
     assert load_config(str(tmp_path / 'again.yaml')) == cfg
     (tmp_path / 'bad.yaml').write_text('MODEL: {HEAD: {NOPE: 1}}')
@@ -70,7 +70,7 @@ def test_evaluation_loop_matches_get_score():
     assert set(error['valid']) == {'ori', 'pos', 'ori_std', 'pos_std', 'ori_mad', 'pos_mad'}
 
 
-@pytest.mark.parametrize('dtype', ['fp16', 'int8', 'fp16x2'])
+@pytest.mark.parametrize('dtype', ['fp16mx', 'fp16', 'int8', 'fp16x2'])
 def test_build_tool_synthetic(tmp_path, dtype):
     from spef_amd import blob as Bl
     from spef_amd.tools.build_mi355x import main
@@ -78,7 +78,7 @@ def test_build_tool_synthetic(tmp_path, dtype):
     assert main(['--synthetic', '--dtype', dtype, '--out', out]) == 0
     info = json.load(open(os.path.join(out, 'build.json')))
     d = Bl.describe(open(os.path.join(out, 'model.spef'), 'rb').read())
-    assert d['dtype'] == {'fp16': 1, 'int8': 3, 'fp16x2': 5}[dtype] and info['n_ori'] == 1728
+    assert d['dtype'] == {'fp16': 1, 'int8': 3, 'fp16x2': 5, 'fp16mx': 6}[dtype] and info['n_ori'] == 1728
     assert os.path.exists(os.path.join(out, 'config.yaml'))
 
 
@@ -100,15 +100,16 @@ def test_build_tool_evaluates_precision_variants(tmp_path):
     eval_host/eval_<variant>.json each, and variants.json comparing head outputs and poses with the fp32 variant."""
     from spef_amd.tools.build_mi355x import main
     out = str(tmp_path / 'b')
-    assert main(['--synthetic', '--out', out, '--eval-variants', 'fp32,fp16x2,fp16,bf16,int8', '--eval-batches',
+    assert main(['--synthetic', '--out', out, '--eval-variants', 'fp32,fp16mx,fp16x2,fp16,bf16,int8', '--eval-batches',
                  '1']) == 0
     v = json.load(open(os.path.join(out, 'eval_host', 'variants.json')))
-    for name in ('fp32', 'fp16x2', 'fp16', 'bf16', 'int8'):
+    for name in ('fp32', 'fp16mx', 'fp16x2', 'fp16', 'bf16', 'int8'):
         assert os.path.exists(os.path.join(out, 'eval_host', f'eval_{name}.json'))
         assert name in v['variants']
     assert v['variants']['fp16']['vs_fp32_variant']['max_abs'] < 1e-3          # north-star logit bound
     assert v['variants']['fp16x2']['vs_fp32_variant']['max_abs'] < 1e-4        # fp32-accurate split schedule
-    assert 'fp16x2' in v['within_north_star'] and 'fp32' in v['within_north_star']
+    assert v['variants']['fp16mx']['vs_fp32_variant']['max_abs'] < 1e-3        # the default (headline) schedule
+    assert {'fp32', 'fp16mx', 'fp16x2'} <= set(v['within_north_star'])
     assert v['variants']['bf16']['vs_fp32_variant']['max_abs'] < 6e-3          # test_gpu_c2_precision bound
     assert v['variants']['fp16']['vs_fp32_variant']['ori_max_deg'] < 0.1
     assert v['variants']['int8']['vs_fp32_variant']['max_abs'] < 0.05          # INT8_BOUND (bench.py)
