@@ -34,8 +34,24 @@ __device__ __forceinline__ double rsq_nr(double x) {   // x > 0
   r = r * fma(-h * r, r, 1.5);
   return r * fma(-h * r, r, 1.5);
 }
+// Division and square root in the small serial solves (QR least squares, Gauss-Newton, Procrustes): the same
+// hardware-estimate + Newton forms (a x (1/b) is within an ulp or two of a / b, against ~15 dependent instructions of
+// the IEEE division sequence on one lane's critical path).
+#ifndef SPEF_EPNP_FASTDIV
+#define SPEF_EPNP_FASTDIV 1
+#endif
+#if SPEF_EPNP_FASTDIV
+__device__ __forceinline__ double ddiv(double a, double b) { return a * rcp_nr(b); }
+__device__ __forceinline__ double dsqrt(double x) { return x > 0.0 ? x * rsq_nr(x) : 0.0; }   // x >= 0
+#else
+__device__ __forceinline__ double ddiv(double a, double b) { return a / b; }
+__device__ __forceinline__ double dsqrt(double x) { return sqrt(x); }
+#endif
 #ifndef SPEF_EPNP_ROT32
 #define SPEF_EPNP_ROT32 0
+#endif
+#ifndef SPEF_EPNP_FUSEROT
+#define SPEF_EPNP_FUSEROT 1
 #endif
 #ifndef SPEF_EPNP_ROTLOCAL
 #define SPEF_EPNP_ROTLOCAL 0
@@ -104,7 +120,7 @@ __device__ void jacobi_sym(double (&a)[N][N], double (&v)[N][N]) {
 // least squares min ||A x - b|| for a full-column-rank 6 x NC A by Householder QR (epnp.cpp qr_solve)
 template <int NC>
 __device__ void qr_lstsq(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
-  double a1[NC], a2[NC];
+  double a1[NC], a2[NC], ia1[NC], ia2[NC];
   for (int k = 0; k < NC; ++k) {
     double eta = 0.0;
     for (int i = k; i < 6; ++i) eta = fmax(eta, fabs(A[i][k]));
@@ -112,35 +128,37 @@ __device__ void qr_lstsq(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
       for (int j = 0; j < NC; ++j) x[j] = 0.0;
       return;
     }
-    const double inv = 1.0 / eta;
+    const double inv = ddiv(1.0, eta);
     double sum2 = 0.0;
     for (int i = k; i < 6; ++i) {
       A[i][k] *= inv;
       sum2 += A[i][k] * A[i][k];
     }
-    double sigma = sqrt(sum2);
+    double sigma = dsqrt(sum2);
     if (A[k][k] < 0) sigma = -sigma;
     A[k][k] += sigma;
     a1[k] = sigma * A[k][k];
     a2[k] = -eta * sigma;
+    ia1[k] = ddiv(1.0, a1[k]);
+    ia2[k] = ddiv(1.0, a2[k]);
     for (int j = k + 1; j < NC; ++j) {
       double sum = 0.0;
       for (int i = k; i < 6; ++i) sum += A[i][k] * A[i][j];
-      const double tau = sum / a1[k];
+      const double tau = sum * ia1[k];
       for (int i = k; i < 6; ++i) A[i][j] -= tau * A[i][k];
     }
   }
   for (int j = 0; j < NC; ++j) {
     double tau = 0.0;
     for (int i = j; i < 6; ++i) tau += A[i][j] * b[i];
-    tau /= a1[j];
+    tau *= ia1[j];
     for (int i = j; i < 6; ++i) b[i] -= tau * A[i][j];
   }
-  x[NC - 1] = b[NC - 1] / a2[NC - 1];
+  x[NC - 1] = b[NC - 1] * ia2[NC - 1];
   for (int i = NC - 2; i >= 0; --i) {
     double sum = 0.0;
     for (int j = i + 1; j < NC; ++j) sum += A[i][j] * x[j];
-    x[i] = (b[i] - sum) / a2[i];
+    x[i] = (b[i] - sum) * ia2[i];
   }
 }
 
@@ -218,6 +236,7 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
                                                    float* __restrict__ pos, int* __restrict__ status) {
   __shared__ double As[2][144], Vs[2][144];
   __shared__ double Cc[12], Cs[12];
+  __shared__ double Cr[2][2][12];   // SPEF_EPNP_FUSEROT: [buffer][c | signed s][index]
   __shared__ double Pal[EPNP_MAXN][4], Pdu[EPNP_MAXN], Pdv[EPNP_MAXN];
   __shared__ double Red[3][2];
   __shared__ double Ls[6][10], Rho[6];
@@ -289,6 +308,22 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
 #define SPEF_EPNP_ABL 0
 #endif
   int cur = 0;
+#if SPEF_EPNP_FUSEROT
+  // One barrier per round: the six threads owning the next round's pivots a_pq (p < q) also form that round's a_pp and
+  // a_qq from this round's inputs and compute the next rotation right after their own update (coefficients
+  // double-buffered in Cr[cb]); the first round's rotations come from the initial matrix.
+  int cb = 0;
+  if (tid < 12) {
+    const int j = rr_partner(0, tid);
+    const int p = tid < j ? tid : j, q = tid < j ? j : tid;
+    const double apq = As[0][12 * p + q];
+    double c = 1.0, sn = 0.0;
+    if (fabs(apq) >= 1e-300) jacobi_rot(As[0][13 * p], As[0][13 * q], apq, c, sn);
+    Cr[0][0][tid] = c;
+    Cr[0][1][tid] = tid == p ? -sn : sn;
+  }
+  __syncthreads();
+#endif
   for (int sweep = 0; sweep < (SPEF_EPNP_ABL == 1 ? 0 : 40); ++sweep) {
     double off = 0.0, diag = 0.0;
     if (ent) {
@@ -309,6 +344,33 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
 #define SPEF_EPNP_JTOL 1e-32
 #endif
     if (off <= SPEF_EPNP_JTOL * diag || off == 0.0) break;   // uniform: every thread read the same sums
+#if SPEF_EPNP_FUSEROT
+    for (int r = 0; r < 11; ++r) {
+      if (ent) {
+        const int i2 = rr_partner(r, ei), j2 = rr_partner(r, ej);
+        const double ci = Cr[cb][0][ei], si = Cr[cb][1][ei], cj = Cr[cb][0][ej], sj = Cr[cb][1][ej];
+        const double* a = As[cur];
+        const double anew = ci * (cj * a[12 * ei + ej] + sj * a[12 * ei + j2]) + si * (cj * a[12 * i2 + ej] + sj * a[12 * i2 + j2]);
+        As[cur ^ 1][e] = anew;
+        const double* v = Vs[cur];
+        Vs[cur ^ 1][e] = cj * v[12 * ei + ej] + sj * v[12 * ei + j2];
+        const int rn = r == 10 ? 0 : r + 1;
+        if (ei < ej && rr_partner(rn, ei) == ej) {   // pivot (ei, ej) of the next round: a_pp', a_qq' as above
+          const double pp = ci * (ci * a[13 * ei] + si * a[12 * ei + i2]) + si * (ci * a[12 * i2 + ei] + si * a[13 * i2]);
+          const double qq = cj * (cj * a[13 * ej] + sj * a[12 * ej + j2]) + sj * (cj * a[12 * j2 + ej] + sj * a[13 * j2]);
+          double c = 1.0, sn = 0.0;
+          if (fabs(anew) >= 1e-300) jacobi_rot(pp, qq, anew, c, sn);
+          Cr[cb ^ 1][0][ei] = c;
+          Cr[cb ^ 1][1][ei] = -sn;
+          Cr[cb ^ 1][0][ej] = c;
+          Cr[cb ^ 1][1][ej] = sn;
+        }
+      }
+      cur ^= 1;
+      cb ^= 1;
+      __syncthreads();
+    }
+#else
     for (int r = 0; r < 11; ++r) {
 #if SPEF_EPNP_ROTLOCAL   // every thread computes the two rotations it applies (one barrier per round instead of two)
       const int i2 = rr_partner(r, ei), j2 = rr_partner(r, ej);
@@ -347,6 +409,7 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
       cur ^= 1;
       __syncthreads();
     }
+#endif
   }
   // the 4 eigenvectors of smallest eigenvalue, ascending (ties keep the lower index); static loops only (a
   // dynamically indexed private array would live in scratch)
@@ -405,8 +468,9 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
   }
   // pw centroid (uniform): a wave reduction over the point lanes
   double pw0[3];
+  const double inv_n = ddiv(1.0, (double)n);
 #pragma unroll
-  for (int k = 0; k < 3; ++k) pw0[k] = warp_sum_d(pw[k]) / n;
+  for (int k = 0; k < 3; ++k) pw0[k] = warp_sum_d(pw[k]) * inv_n;
 
   // ---- approximation ap = wave + 1 (epnp.cpp compute_pose: find_betas_approx_1/2/3 + gauss_newton + compute_R_and_t)
   const int ap = wave + 1;
@@ -423,10 +487,11 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
       }
       qr_lstsq<4>(A, rr, x);
       const double s = x[0] < 0 ? -1.0 : 1.0;
-      be[0] = sqrt(fabs(x[0]));
-      be[1] = s * x[1] / be[0];
-      be[2] = s * x[2] / be[0];
-      be[3] = s * x[3] / be[0];
+      be[0] = dsqrt(fabs(x[0]));
+      const double ib = ddiv(s, be[0]);
+      be[1] = x[1] * ib;
+      be[2] = x[2] * ib;
+      be[3] = x[3] * ib;
     } else if (ap == 2) {
       double A[6][3], x[3];
 #pragma unroll
@@ -435,11 +500,11 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
       }
       qr_lstsq<3>(A, rr, x);
       if (x[0] < 0) {
-        be[0] = sqrt(-x[0]);
-        be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0;
+        be[0] = dsqrt(-x[0]);
+        be[1] = x[2] < 0 ? dsqrt(-x[2]) : 0.0;
       } else {
-        be[0] = sqrt(x[0]);
-        be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0;
+        be[0] = dsqrt(x[0]);
+        be[1] = x[2] > 0 ? dsqrt(x[2]) : 0.0;
       }
       if (x[1] < 0) be[0] = -be[0];
     } else {
@@ -450,14 +515,14 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
         for (int k = 0; k < 5; ++k) A[i][k] = L[i][k];
       qr_lstsq<5>(A, rr, x);
       if (x[0] < 0) {
-        be[0] = sqrt(-x[0]);
-        be[1] = x[2] < 0 ? sqrt(-x[2]) : 0.0;
+        be[0] = dsqrt(-x[0]);
+        be[1] = x[2] < 0 ? dsqrt(-x[2]) : 0.0;
       } else {
-        be[0] = sqrt(x[0]);
-        be[1] = x[2] > 0 ? sqrt(x[2]) : 0.0;
+        be[0] = dsqrt(x[0]);
+        be[1] = x[2] > 0 ? dsqrt(x[2]) : 0.0;
       }
       if (x[1] < 0) be[0] = -be[0];
-      be[2] = x[3] / be[0];
+      be[2] = ddiv(x[3], be[0]);
     }
     epnp_gn(L, rho, be);
     // R|t (epnp.cpp compute_R_and_t): ccs uniform, pcs of point = lane, sums by wave reduction
@@ -476,7 +541,7 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
       for (int j = 0; j < 3; ++j) pc[j] = -pc[j];
     double pc0[3];
 #pragma unroll
-    for (int j = 0; j < 3; ++j) pc0[j] = warp_sum_d(pc[j]) / n;
+    for (int j = 0; j < 3; ++j) pc0[j] = warp_sum_d(pc[j]) * inv_n;
     double abt[3][3];
 #pragma unroll
     for (int j = 0; j < 3; ++j)
@@ -498,9 +563,9 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
         col[r] = abt[r][0] * Vm[0][c] + abt[r][1] * Vm[1][c] + abt[r][2] * Vm[2][c];
         nrm += col[r] * col[r];
       }
-      nrm = sqrt(nrm);
+      const double inrm = nrm > 0 ? rsq_nr(nrm) : 0.0;
 #pragma unroll
-      for (int r = 0; r < 3; ++r) U[r][c] = nrm > 0 ? col[r] / nrm : 0.0;
+      for (int r = 0; r < 3; ++r) U[r][c] = col[r] * inrm;
     }
 #pragma unroll
     for (int i = 0; i < 3; ++i)
@@ -517,11 +582,11 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
     if (pt) {
       const double xc = R[0][0] * pw[0] + R[0][1] * pw[1] + R[0][2] * pw[2] + t[0];
       const double yc = R[1][0] * pw[0] + R[1][1] * pw[1] + R[1][2] * pw[2] + t[1];
-      const double iz = 1.0 / (R[2][0] * pw[0] + R[2][1] * pw[1] + R[2][2] * pw[2] + t[2]);
+      const double iz = ddiv(1.0, R[2][0] * pw[0] + R[2][1] * pw[1] + R[2][2] * pw[2] + t[2]);
       const double ue = uc + fu * xc * iz, ve = vc + fv * yc * iz;
-      err = sqrt((us0 - ue) * (us0 - ue) + (us1 - ve) * (us1 - ve));
+      err = dsqrt((us0 - ue) * (us0 - ue) + (us1 - ve) * (us1 - ve));
     }
-    const double em = warp_sum_d(err) / n;
+    const double em = warp_sum_d(err) * inv_n;
     if (lane == 0) {
       Res[wave][0] = em;
 #pragma unroll

@@ -28,6 +28,13 @@
 #include "spef_common.hpp"
 #include "spef_kernels.hpp"
 
+#ifndef SPEF_MX_DEINTERLEAVE
+#define SPEF_MX_DEINTERLEAVE 1
+#endif
+#ifndef SPEF_MX_PACK16
+#define SPEF_MX_PACK16 1
+#endif
+
 namespace spef {
 
 namespace {
@@ -96,6 +103,10 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
                    int tiles_y, uint32_t nwg) {
   using G = MxGeom<CIN, HID, COUT, S, TH>;
   constexpr int TW = G::TW;
+  // CIN = 16 (block 2): W_hi x + W_lo x as ONE K = 32 MFMA -- A = [W_hi | W_lo] along k, B = [x ; x] (lanes kg = 2, 3
+  // repeat the channels of kg = 0, 1): half the expand MFMAs of the two-product form, the same sums.
+  constexpr bool PK = IN16 && CIN == 16 && SPEF_MX_PACK16;
+  constexpr int KX = PK ? 16 : 32;   // channel span of the B fragment's k groups
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -111,6 +122,18 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
 
   // ---- expand operands: this wave's input-tile pixel tiles pt = wave + 4 j (lane: pixel r16, channels 8kg..8kg+7);
   // an fp32 input (blocks 5-7) is split hi / lo once (three MFMAs per product), an fp16 input is exact (two)
+  // slab slot of input-tile pixel p: row-major, except that at stride 2 a row holds its even columns, then its odd ones
+  // (the depthwise's 16 lanes then read 16 consecutive slots -- 80-B steps, conflict-free -- instead of every other)
+  constexpr bool DEI = S == 2 && SPEF_MX_DEINTERLEAVE;
+  constexpr int HALF = (G::IW + 1) / 2;
+  auto slab_slot = [&](int p) {
+    if constexpr (DEI) {
+      const int py = p / G::IW, px = p - py * G::IW;
+      return py * G::IW + ((px & 1) ? HALF + (px >> 1) : (px >> 1));
+    } else {
+      return p;
+    }
+  };
   f16x8 bx[G::EPT], bxl[IN16 ? 1 : G::EPT];
   int soff[G::EPT];   // slab byte offset of the lane's pixel (channels 4kg.. of h = 0), or its dummy row
 #pragma unroll
@@ -124,10 +147,11 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       ix = ix0 + px;
       ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
     }
-    const size_t e0 = xb + ((size_t)iy * W + ix) * CIN + 8 * kg;
+    const int kc = 8 * kg % KX;   // the lane's first input channel
+    const size_t e0 = xb + ((size_t)iy * W + ix) * CIN + kc;
     if constexpr (IN16) {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
-      if (ok && 8 * kg < CIN) v = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(X) + e0);
+      if (ok && kc < CIN) v = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(X) + e0);
       bx[j] = __builtin_bit_cast(f16x8, v);
     } else {
       float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
@@ -145,17 +169,19 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       bx[j] = __builtin_bit_cast(f16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
       bxl[j] = __builtin_bit_cast(f16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
     }
-    soff[j] = ok ? p * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
-    if (!ok && p < G::PINP) {   // the depthwise's zero padding: stored once, never overwritten
-      *reinterpret_cast<uint2*>(smem + p * G::SPB + 8 * kg) = make_uint2(0u, 0u);
-      *reinterpret_cast<uint2*>(smem + p * G::SPB + 32 + 8 * kg) = make_uint2(0u, 0u);
+    const int ps = slab_slot(p);
+    soff[j] = ok ? ps * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
+    if (!ok && p < G::PIN) {   // the depthwise's zero padding: stored once, never overwritten
+      *reinterpret_cast<uint2*>(smem + ps * G::SPB + 8 * kg) = make_uint2(0u, 0u);
+      *reinterpret_cast<uint2*>(smem + ps * G::SPB + 32 + 8 * kg) = make_uint2(0u, 0u);
     }
   }
 
   // ---- depthwise lane geometry: (row group ry, column cx) from the ds_read_b128 lane groups
   int ry, cx;
   b128_group(lane, ry, cx);
-  const int dbase = (S * ry * G::PPL * G::IW + S * cx) * G::SPB + 16 * wave;   // slab byte offset, input row 0, kx 0
+  const int dbase = (S * ry * G::PPL * G::IW + (DEI ? cx : S * cx)) * G::SPB + 16 * wave;   // input row 0, kx 0
+  constexpr int KXO[3] = {0, (DEI ? HALF : 1) * G::SPB, (DEI ? 1 : 2) * G::SPB};   // slab byte step of tap kx
   char* Dh = smem + G::OFF_DX;
   char* Dl = Dh + G::DX_B;
   const int skw = (ry & 1) * 16;
@@ -174,9 +200,14 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
   auto load_e = [&](int k) {
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
-      const size_t off = (size_t)(32 * k + 16 * h + r16) * 32 + 8 * kg;
-      eah[h] = *reinterpret_cast<const f16x8*>(We + off);
-      eal[h] = *reinterpret_cast<const f16x8*>(WeLo + off);
+      if constexpr (PK) {   // k groups 0, 1: W_hi channels 0-15; 2, 3: W_lo channels 0-15
+        const size_t off = (size_t)(32 * k + 16 * h + r16) * 32 + 8 * (kg & 1);
+        eah[h] = *reinterpret_cast<const f16x8*>((kg < 2 ? We : WeLo) + off);
+      } else {
+        const size_t off = (size_t)(32 * k + 16 * h + r16) * 32 + 8 * kg;
+        eah[h] = *reinterpret_cast<const f16x8*>(We + off);
+        eal[h] = *reinterpret_cast<const f16x8*>(WeLo + off);
+      }
     }
   };
   auto load_p = [&](int k) {
@@ -212,7 +243,9 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           f32x4 e = f32x4{eb[h].x, eb[h].y, eb[h].z, eb[h].w};
-          if constexpr (IN16) {
+          if constexpr (PK) {
+            e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e, 0, 0, 0);
+          } else if constexpr (IN16) {
             e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e, 0, 0, 0);
             e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eal[h], bx[j], e, 0, 0, 0);
           } else {
@@ -235,7 +268,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     for (int r = 0; r < G::NR; ++r) {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) {
-        const uint4 xv = *reinterpret_cast<const uint4*>(smem + dbase + (r * G::IW + kx) * G::SPB);
+        const uint4 xv = *reinterpret_cast<const uint4*>(smem + dbase + r * G::IW * G::SPB + KXO[kx]);
         const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
         for (int t = 0; t < G::PPL; ++t) {

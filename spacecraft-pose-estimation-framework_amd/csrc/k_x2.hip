@@ -430,6 +430,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
 // Stage buffers (double-buffered, written one iteration before use): expand weights + expand bias of chunk k in
 // iteration k - 2, depthwise weights + bias and project weights of chunk k in iteration k - 1. Same arithmetic and
 // rounding as x2_irb_kernel (bit-identical results).
+#ifndef SPEF_X2_GLDS   // stage the role-split kernels' chunk weights by LDS-DMA (global_load_lds) instead of registers
+#define SPEF_X2_GLDS 1
+#endif
 template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST, int P = 1>
 struct X2wGeom {
   static constexpr int NE = 4, ND = 4, NW = NE + ND;
@@ -450,8 +453,21 @@ struct X2wGeom {
   static constexpr int SE_B = 2 * 32 * WES * 2 + 32 * 4;   // hi / lo weight planes + expand bias
   static constexpr int SD_B = (9 * 32 + 32) * 4;            // depthwise weights [9][32] + depthwise bias
   static constexpr int SP_B = PST ? 2 * NPC * WPS * 2 : 0;
+#if SPEF_X2_GLDS
+  // LDS-DMA staging: every stage region a whole number of 1-KiB wave-instruction pieces (a piece writes 64 x 16 B
+  // lane-linearly); per buffer the depthwise and project stages are one contiguous region
+  static constexpr int SE_BQ = (SE_B + 1023) / 1024 * 1024, SD_BQ = (SD_B + 1023) / 1024 * 1024;
+  static constexpr int SP_BQ = (SP_B + 1023) / 1024 * 1024, DP_BQ = SD_BQ + SP_BQ;
+  static constexpr int SE_STR = SE_BQ, SD_STR = DP_BQ, SP_STR = DP_BQ;
+  static constexpr int OFF_SE = 2 * SLAB_B, OFF_SD = OFF_SE + 2 * SE_BQ, OFF_SP = OFF_SD + SD_BQ;
+  static constexpr int OFF_TR = OFF_SD + 2 * DP_BQ;
+  static constexpr int NIE = SE_BQ / 1024, NID = DP_BQ / 1024;                  // pieces per chunk stage
+  static constexpr int IEW = (NIE + NE - 1) / NE, IDW = (NID + ND - 1) / ND;    // pieces per wave
+#else
+  static constexpr int SE_STR = SE_B, SD_STR = SD_B, SP_STR = SP_B;
   static constexpr int OFF_SE = 2 * SLAB_B, OFF_SD = OFF_SE + 2 * SE_B, OFF_SP = OFF_SD + 2 * SD_B;
   static constexpr int OFF_TR = OFF_SP + 2 * SP_B;          // dummy rows: expand stores of invalid input pixels
+#endif
   static constexpr int LDS_BYTES = OFF_TR + 16 * 24 * 4;
   // 16-B stage pieces per chunk
   static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = 9 * 8 + 8, NPP = PST ? 2 * NPC * 4 : 0;
@@ -492,9 +508,9 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   const int oy0 = ty * TH, ox0 = tx * TW;
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
   auto slab = [&](int i) { return reinterpret_cast<float*>(smem + i * G::SLAB_B); };
-  auto se = [&](int i) { return smem + G::OFF_SE + i * G::SE_B; };
-  auto sd = [&](int i) { return reinterpret_cast<float*>(smem + G::OFF_SD + i * G::SD_B); };
-  auto sp = [&](int i) { return reinterpret_cast<_Float16*>(smem + G::OFF_SP + i * G::SP_B); };
+  auto se = [&](int i) { return smem + G::OFF_SE + i * G::SE_STR; };
+  auto sd = [&](int i) { return reinterpret_cast<float*>(smem + G::OFF_SD + i * G::SD_STR); };
+  auto sp = [&](int i) { return reinterpret_cast<_Float16*>(smem + G::OFF_SP + i * G::SP_STR); };
 
   // 16-B stage piece u of chunk k: kind 0 = expand (weights + bias, chunk ke), 1 = depthwise (chunk kd),
   // 2 = project (chunk kd). Source / destination pointers; null source = nothing to stage (chunk out of range).
@@ -537,6 +553,74 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     }
   };
 
+#if SPEF_X2_GLDS
+  // ---- LDS-DMA stage pieces. Expand waves: pieces e + NE j of the expand stage (weights hi / lo + bias); depthwise
+  // waves: pieces d + ND j of the depthwise + project stage. Lane l of piece i fills LDS slot 64 i + l of the region
+  // from a source whose address at chunk k is src0 + k * kstr (pad slots read a valid address of the same tensor).
+  const bool ewave = wave < G::NE;
+  const int wr = ewave ? wave : wave - G::NE;
+  constexpr int NJ = G::IEW > G::IDW ? G::IEW : G::IDW;
+  const char* gsrc[NJ];
+  int kstr[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int off = ((ewave ? wr + G::NE * j : wr + G::ND * j) * 64 + lane) * 16;   // byte offset in the region
+    const char* src;
+    int ks;
+    if (ewave) {
+      constexpr int EW_B = 2 * 32 * G::WES * 2, ROW_B = G::WES * 2;
+      if (off < EW_B) {
+        const int pl = off / (32 * ROW_B), rem = off - pl * (32 * ROW_B), rr = rem / ROW_B;
+        const int col = (rem - rr * ROW_B) / 16;
+        src = reinterpret_cast<const char*>(We + (size_t)pl * G::HIDP * G::CINP + (size_t)(32 * cb + rr) * G::CINP +
+                                            (col < G::CINP / 8 ? 8 * col : 0));
+        ks = 32 * G::CINP * 2;
+      } else {
+        const int g = (off - EW_B) / 16;
+        src = reinterpret_cast<const char*>(be + 32 * cb + (g < 8 ? 4 * g : 0));
+        ks = 128;
+      }
+    } else {
+      if (off < G::SD_BQ) {
+        if (off < 1152) {
+          src = reinterpret_cast<const char*>(Wd + (size_t)(off / 128) * G::HIDP + 32 * cb + 4 * ((off % 128) / 16));
+        } else {
+          const int g = (off - 1152) / 16;
+          src = reinterpret_cast<const char*>(bd + 32 * cb + (g < 8 ? 4 * g : 0));
+        }
+        ks = 128;
+      } else {
+        const int o2 = off - G::SD_BQ;
+        constexpr int ROW_B = G::WPS * 2;
+        const int pl = o2 / (G::NPC * ROW_B), rem = o2 - pl * (G::NPC * ROW_B), rr = rem / ROW_B;
+        const int q = (rem - rr * ROW_B) / 16;
+        const bool ok = PST && o2 < G::SP_B;
+        src = reinterpret_cast<const char*>(Wp + (ok ? (size_t)pl * G::NPC * G::HIDP + (size_t)rr * G::HIDP : 0) + 32 * cb +
+                                            (ok && q < 4 ? 8 * q : 0));
+        ks = 64;
+      }
+    }
+    gsrc[j] = src;
+    kstr[j] = ks;
+  }
+  // issue this wave's pieces of chunk k's stage (expand waves: the expand stage; depthwise waves: depthwise + project)
+  auto dma = [&](int k) {
+    char* base = ewave ? smem + G::OFF_SE + (k & 1) * G::SE_STR : smem + G::OFF_SD + (k & 1) * G::SD_STR;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int i = ewave ? wr + G::NE * j : wr + G::ND * j;
+      if ((ewave && j < G::IEW && i < G::NIE) || (!ewave && j < G::IDW && i < G::NID))
+        __builtin_amdgcn_global_load_lds((const void*)(gsrc[j] + (size_t)k * kstr[j]),
+                                         (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
+    }
+  };
+  if (ewave) {
+    dma(0);
+    dma(1);
+  } else {
+    dma(0);
+  }
+#else
   // ---- prologue (all waves): expand stages of chunks 0 and 1, depthwise / project stage of chunk 0
   {
     constexpr int NP0 = 2 * G::NPE + G::NPD + G::NPP;
@@ -556,6 +640,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     for (int i = 0; i < NIT; ++i)
       if (dst[i]) *reinterpret_cast<uint4*>(dst[i]) = v[i];
   }
+#endif
 
   if (wave < G::NE) {
     // ================= expand waves
@@ -648,6 +733,17 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     // Stage data is loaded one iteration before it is stored: the pieces of expand chunk c + 2 and depthwise /
     // project chunk c + 1 are fetched in iteration c - 1 (a whole chunk period of L2 latency hidden) and written to
     // LDS at the start of iteration c (the same buffers and barriers as a load-and-store in iteration c).
+#if SPEF_X2_GLDS
+    __syncthreads();                 // prologue stages landed (vmcnt(0) + barrier)
+    expand(0);
+    __syncthreads();                 // slab 0 visible
+#pragma unroll 1
+    for (int c = 0; c < G::NCL; ++c) {
+      if (c + 2 < G::NCL) dma(c + 2);   // expand stage of chunk c + 2 into the buffer chunk c's expand released
+      if (c + 1 < G::NCL) expand(c + 1);
+      __syncthreads();                  // (waits for this wave's pieces: visible to every wave after the barrier)
+    }
+#else
     uint4 v[G::NPIECE];
     auto load_stage = [&](int c) {
 #if SPEF_X2_ABL_STAGE < 2   // timing ablation only (wrong results): 2 = no stage loads
@@ -684,6 +780,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       }
       __syncthreads();
     }
+#endif
   } else {
     // ================= depthwise / project waves
     const int d = wave - G::NE;
@@ -720,6 +817,9 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     __syncthreads();
 #pragma unroll 1
     for (int c = 0; c < G::NCL; ++c) {
+#if SPEF_X2_GLDS
+      if (c + 1 < G::NCL) dma(c + 1);   // depthwise + project stage of chunk c + 1 (buffer released by chunk c - 1)
+#endif
       const float* Sl = slab(c & 1);
       const float* D = sd(c & 1);
       f32x2 a[G::QPW][4];
