@@ -28,6 +28,9 @@
 #include "spef_common.hpp"
 #include "spef_kernels.hpp"
 
+#ifndef SPEF_MX_FRONT_F32W   // front kernel: block-1 depthwise with fp32 weights (one v_fma_mix per tap)
+#define SPEF_MX_FRONT_F32W 1
+#endif
 #ifndef SPEF_MX_DEINTERLEAVE
 #define SPEF_MX_DEINTERLEAVE 1
 #endif
@@ -443,7 +446,11 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t In[IH * IRS];
   __shared__ __attribute__((aligned(16))) uint32_t Lr[SH * RSL + 4];
   __shared__ __attribute__((aligned(16))) char Ps[4 * RSB];
+#if SPEF_MX_FRONT_F32W
+  __shared__ __attribute__((aligned(16))) float Sw[9 * 32];          // dw weights fp32 [kx][ky][32] (exact)
+#else
   __shared__ __attribute__((aligned(16))) uint32_t Sv[2][3 * 64];   // dw weight pairs [hi|lo][kx][(w0,w1)|(w1,w2)][32]
+#endif
   __shared__ __attribute__((aligned(16))) float Sb[32];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -488,11 +495,15 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
     // dw weight pairs: the last wave's threads 0..47 (kx = t / 16, pair (ky, ky+1), ky = (t / 8) % 2, 4 channels)
     const int vt = NW * 64 - 1 - tid;
     float4 wa = make_float4(0.f, 0.f, 0.f, 0.f), wb = wa;
+#if SPEF_MX_FRONT_F32W
+    if (vt < 72) wa = *reinterpret_cast<const float4*>(Wd + 4 * vt);   // [ky*3+kx][32]: tap vt / 8, channels 4 (vt % 8)
+#else
     if (vt < 48) {
       const int kx = vt >> 4, ky = (vt >> 3) & 1, ch = 4 * (vt & 7);
       wa = *reinterpret_cast<const float4*>(Wd + (ky * 3 + kx) * 32 + ch);
       wb = *reinterpret_cast<const float4*>(Wd + ((ky + 1) * 3 + kx) * 32 + ch);
     }
+#endif
     if (fast) {
       static_assert(TW == 16, "fast-path byte phase assumes 16-wide tiles");
 #pragma unroll
@@ -534,6 +545,12 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
         }
       }
     }
+#if SPEF_MX_FRONT_F32W
+    if (vt < 72) {   // -> [kx][ky][32]
+      const int tap = vt >> 3, ky = tap / 3, kx = tap - 3 * ky;
+      *reinterpret_cast<float4*>(&Sw[(kx * 3 + ky) * 32 + 4 * (vt & 7)]) = wa;
+    }
+#else
     if (vt < 48) {   // hi / lo split of the fp32 weights, packed as (ky, ky + 1) fp16 pairs
       const int kx = vt >> 4, ky = (vt >> 3) & 1;
       const float xa[4] = {wa.x, wa.y, wa.z, wa.w}, xb[4] = {wb.x, wb.y, wb.z, wb.w};
@@ -547,6 +564,7 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
       *reinterpret_cast<uint4*>(&Sv[0][kx * 64 + ky * 32 + 4 * (vt & 7)]) = make_uint4(ph[0], ph[1], ph[2], ph[3]);
       *reinterpret_cast<uint4*>(&Sv[1][kx * 64 + ky * 32 + 4 * (vt & 7)]) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
     }
+#endif
     if (tid < 32) Sb[tid] = bd[tid];
     if (tid < 4) Lr[SH * RSL + tid] = 0;   // pad dwords read (zero weight) by the last position of the last row
   }
@@ -651,6 +669,33 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
       const uint4 x = *reinterpret_cast<const uint4*>(p), y = *(reinterpret_cast<const uint4*>(p) + 1);
       v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
     };
+#if SPEF_MX_FRONT_F32W
+    // rows oy (a0) and oy + 1 (a1) of column ox: stem rows oy .. oy + 3 are the pairs pc (oy, oy + 1), pn (oy + 2,
+    // oy + 3); fp32 weights, one v_fma_mix per tap and channel
+#pragma unroll
+    for (int kx = 0; kx < 3; ++kx) {
+      uint32_t pc[8], pn[8];
+      rd8(pbase + kx * 32, pc);
+      rd8(pbase + (SW + kx) * 32, pn);
+      float w[3][8];
+#pragma unroll
+      for (int ky = 0; ky < 3; ++ky) {
+        const float4 u0 = *reinterpret_cast<const float4*>(&Sw[(kx * 3 + ky) * 32 + 8 * kg]);
+        const float4 u1 = *reinterpret_cast<const float4*>(&Sw[(kx * 3 + ky) * 32 + 8 * kg + 4]);
+        w[ky][0] = u0.x; w[ky][1] = u0.y; w[ky][2] = u0.z; w[ky][3] = u0.w;
+        w[ky][4] = u1.x; w[ky][5] = u1.y; w[ky][6] = u1.z; w[ky][7] = u1.w;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        a0[e] = fmaf(h_lo(pc[e]), w[0][e], a0[e]);
+        a1[e] = fmaf(h_hi(pc[e]), w[0][e], a1[e]);
+        a0[e] = fmaf(h_hi(pc[e]), w[1][e], a0[e]);
+        a1[e] = fmaf(h_lo(pn[e]), w[1][e], a1[e]);
+        a0[e] = fmaf(h_lo(pn[e]), w[2][e], a0[e]);
+        a1[e] = fmaf(h_hi(pn[e]), w[2][e], a1[e]);
+      }
+    }
+#else
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx) {
       uint32_t pc[8], pn[8];
@@ -670,6 +715,7 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
         }
       }
     }
+#endif
     f32x4 acc[2] = {f32x4{pb.x, pb.y, pb.z, pb.w}, f32x4{pb.x, pb.y, pb.z, pb.w}};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
