@@ -28,6 +28,9 @@
 #include "spef_common.hpp"
 #include "spef_kernels.hpp"
 
+#ifndef SPEF_MX_HALF_LAST   // HID % 32 == 16: skip the empty half of the last hidden chunk
+#define SPEF_MX_HALF_LAST 1
+#endif
 #ifndef SPEF_MX_FRONT_F32W   // front kernel: block-1 depthwise with fp32 weights (one v_fma_mix per tap)
 #define SPEF_MX_FRONT_F32W 1
 #endif
@@ -109,6 +112,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
   // CIN = 16 (block 2): W_hi x + W_lo x as ONE K = 32 MFMA -- A = [W_hi | W_lo] along k, B = [x ; x] (lanes kg = 2, 3
   // repeat the channels of kg = 0, 1): half the expand MFMAs of the two-product form, the same sums.
   constexpr bool PK = IN16 && CIN == 16 && SPEF_MX_PACK16;
+  constexpr bool HALF_LAST = HID % 32 == 16 && SPEF_MX_HALF_LAST;
   constexpr int KX = PK ? 16 : 32;   // channel span of the B fragment's k groups
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -226,6 +230,11 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
 
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
+    // HID = 144 (blocks 3, 4): the last chunk holds 16 real channels. Its upper half is skipped -- no expand MFMAs or
+    // stores for hidden rows 16-31, no depthwise on waves 2-3 -- so those slab / exchange rows keep the previous
+    // chunk's finite values, which meet the zero-padded project weights of rows >= HID (0 x finite = 0).
+    const bool half = HALF_LAST && c == G::NCH - 1;
+    const bool dw_on = !(half && wave >= 2);
     // wave-uniform depthwise weights + bias of this wave's 8 channels (scalar loads; fp32, exact)
     const float* wdc = Wd + 32 * c + 8 * wave;
     float wd[9][8], db[8];
@@ -245,6 +254,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       for (int j = 0; j < G::EPT; ++j) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
+          if (h == 1 && half) continue;
           f32x4 e = f32x4{eb[h].x, eb[h].y, eb[h].z, eb[h].w};
           if constexpr (PK) {
             e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e, 0, 0, 0);
@@ -262,6 +272,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     __syncthreads();   // slab of chunk c complete (and chunk c - 1's exchange buffer consumed)
 
     // ---- depthwise: PPL output rows of column cx, channels 8 wave .. +7, fp32 accumulation, exact weights
+    if (dw_on) {
     float a[G::PPL][8];
 #pragma unroll
     for (int t = 0; t < G::PPL; ++t)
@@ -300,6 +311,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       *reinterpret_cast<uint4*>(Dh + o) = make_uint4(hh[0], hh[1], hh[2], hh[3]);
       *reinterpret_cast<uint4*>(Dl + o) = make_uint4(ll[0], ll[1], ll[2], ll[3]);
     }
+    }   // dw_on
     __syncthreads();   // exchange buffer of chunk c complete (and the slab consumed)
 
     // ---- project: output rows q = wave QPW + i, three MFMAs per product
