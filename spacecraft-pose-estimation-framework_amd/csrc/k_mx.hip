@@ -28,6 +28,9 @@
 #include "spef_common.hpp"
 #include "spef_kernels.hpp"
 
+#ifndef SPEF_MX_ALIAS
+#define SPEF_MX_ALIAS 0
+#endif
 #ifndef SPEF_MX_HALF_LAST   // HID % 32 == 16: skip the empty half of the last hidden chunk
 #define SPEF_MX_HALF_LAST 1
 #endif
@@ -92,9 +95,12 @@ struct MxGeom {
   static constexpr int SLAB_B = PINP * SPB;
   static constexpr int DX_B = POUT * DXB + 16;            // one exchange plane (+ the odd-row-group skew)
   static constexpr int TRASH_B = 16 * SPB;                // dummy rows for invalid pixels' expand stores
-  static constexpr int OFF_DX = SLAB_B, OFF_TR = OFF_DX + 2 * DX_B;
+  // SPEF_MX_ALIAS: the exchange planes overlay the slab (two more barriers per chunk, ~35 % less LDS: 3 workgroups per CU
+  // instead of 2 at stride 2)
+  static constexpr int OFF_DX = SPEF_MX_ALIAS ? 0 : SLAB_B;
+  static constexpr int OFF_TR = SPEF_MX_ALIAS ? (SLAB_B > 2 * DX_B ? SLAB_B : 2 * DX_B) : OFF_DX + 2 * DX_B;
   static constexpr int LDS_BYTES = OFF_TR + TRASH_B;
-  static constexpr int WAVES_PER_EU = (163840 / LDS_BYTES) > 8 ? 8 : (163840 / LDS_BYTES);
+  static constexpr int WAVES_PER_EU = (163840 / LDS_BYTES) > 4 ? 4 : (163840 / LDS_BYTES);   // (> 4: spills)
   static_assert(CIN <= 32 && CIN % 8 == 0, "blocks 2-7: one K = 32 step");
   static_assert(POUT % 64 == 0 && (POUT / 16) % NW == 0, "tile");
   static_assert(COUT % 4 == 0, "cout");
@@ -142,6 +148,8 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     }
   };
   f16x8 bx[G::EPT], bxl[IN16 ? 1 : G::EPT];
+  uint32_t zmask = 0;   // SPEF_MX_ALIAS: the lane's padding pixels (per expand tile)
+  const bool edge = iy0 < 0 || ix0 < 0 || iy0 + G::IH > H || ix0 + G::IW > W;   // workgroup-uniform
   int soff[G::EPT];   // slab byte offset of the lane's pixel (channels 4kg.. of h = 0), or its dummy row
 #pragma unroll
   for (int j = 0; j < G::EPT; ++j) {
@@ -177,6 +185,11 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       bxl[j] = __builtin_bit_cast(f16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
     }
     const int ps = slab_slot(p);
+    if constexpr (SPEF_MX_ALIAS) {   // padding pixels store zeros every chunk (the exchange overwrites them)
+      soff[j] = p < G::PIN ? ps * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
+      if (!ok && p < G::PIN) zmask |= 1u << j;
+      continue;
+    }
     soff[j] = ok ? ps * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
     if (!ok && p < G::PIN) {   // the depthwise's zero padding: stored once, never overwritten
       *reinterpret_cast<uint2*>(smem + ps * G::SPB + 8 * kg) = make_uint2(0u, 0u);
@@ -264,7 +277,9 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
           } else {
             e = mfma3(eah[h], eal[h], bx[j], bxl[IN16 ? 0 : j], e);
           }
-          *reinterpret_cast<uint2*>(smem + soff[j] + 32 * h) = make_uint2(relu_pk2(e[0], e[1]), relu_pk2(e[2], e[3]));
+          uint2 st = make_uint2(relu_pk2(e[0], e[1]), relu_pk2(e[2], e[3]));
+          if (SPEF_MX_ALIAS && edge && ((zmask >> j) & 1u)) st = make_uint2(0u, 0u);
+          *reinterpret_cast<uint2*>(smem + soff[j] + 32 * h) = st;
         }
       }
       if (c + 1 < G::NCH) load_e(c + 1);
@@ -272,8 +287,8 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     __syncthreads();   // slab of chunk c complete (and chunk c - 1's exchange buffer consumed)
 
     // ---- depthwise: PPL output rows of column cx, channels 8 wave .. +7, fp32 accumulation, exact weights
-    if (dw_on) {
     float a[G::PPL][8];
+    if (dw_on) {
 #pragma unroll
     for (int t = 0; t < G::PPL; ++t)
 #pragma unroll
@@ -296,7 +311,10 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
         }
       }
     }
+    }   // dw_on
+    if constexpr (SPEF_MX_ALIAS) __syncthreads();   // every wave's slab reads done before the exchange overlays it
     // ReLU, hi / lo split -> exchange buffer (pixel (row ry PPL + t, column cx), channels 8 wave ..)
+    if (dw_on) {
 #pragma unroll
     for (int t = 0; t < G::PPL; ++t) {
       uint32_t hh[4], ll[4];
@@ -325,6 +343,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       for (int t = 0; t < G::NCT; ++t) acc[i][t] = mfma3(pah[t], pal[t], bh, bl, acc[i][t]);
     }
     if (c + 1 < G::NCH) load_p(c + 1);
+    if constexpr (SPEF_MX_ALIAS) __syncthreads();   // exchange reads done before the next expand overlays them
   }
 
   // ---- epilogue: + residual (fp16 block input, added after the BN bias, pytorch_layers.py:93-96)

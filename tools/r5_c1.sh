@@ -8,4 +8,4 @@ python tools/lib_cmp.py --cmp gpurun_out/cmp_g0.npz gpurun_out/cmp_g1.npz
 timeout -k 10 600 python -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_gpu_keypoints.py tests/test_gpu_mx.py tests/test_gpu_x2.py \
   > gpurun_out/c1_tests.log 2>&1 || { tail -40 gpurun_out/c1_tests.log; exit 1; }
 tail -3 gpurun_out/c1_tests.log
-bash tools/r5_var.sh "pk0 pk1d0 g0 g1 fw1 hl1" 2
+bash tools/r5_var.sh "pk0 pk1d0 g0 g1 fw1 hl1 al1" 2
