@@ -48,10 +48,10 @@ __device__ __forceinline__ double ddiv(double a, double b) { return a / b; }
 __device__ __forceinline__ double dsqrt(double x) { return sqrt(x); }
 #endif
 #ifndef SPEF_EPNP_ROT32
-#define SPEF_EPNP_ROT32 0
+#define SPEF_EPNP_ROT32 1
 #endif
 #ifndef SPEF_EPNP_FUSEROT
-#define SPEF_EPNP_FUSEROT 1
+#define SPEF_EPNP_FUSEROT 0
 #endif
 #ifndef SPEF_EPNP_ROTLOCAL
 #define SPEF_EPNP_ROTLOCAL 0
@@ -341,7 +341,7 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
     off = Red[0][0] + Red[1][0] + Red[2][0];
     diag = Red[0][1] + Red[1][1] + Red[2][1];
 #ifndef SPEF_EPNP_JTOL
-#define SPEF_EPNP_JTOL 1e-32
+#define SPEF_EPNP_JTOL 1e-26
 #endif
     if (off <= SPEF_EPNP_JTOL * diag || off == 0.0) break;   // uniform: every thread read the same sums
 #if SPEF_EPNP_FUSEROT

@@ -29,16 +29,16 @@
 #include "spef_kernels.hpp"
 
 #ifndef SPEF_MX_ALIAS
-#define SPEF_MX_ALIAS 0
+#define SPEF_MX_ALIAS 1
 #endif
 #ifndef SPEF_MX_HALF_LAST   // HID % 32 == 16: skip the empty half of the last hidden chunk
-#define SPEF_MX_HALF_LAST 1
+#define SPEF_MX_HALF_LAST 0
 #endif
 #ifndef SPEF_MX_FRONT_F32W   // front kernel: block-1 depthwise with fp32 weights (one v_fma_mix per tap)
 #define SPEF_MX_FRONT_F32W 1
 #endif
 #ifndef SPEF_MX_DEINTERLEAVE
-#define SPEF_MX_DEINTERLEAVE 1
+#define SPEF_MX_DEINTERLEAVE 0
 #endif
 #ifndef SPEF_MX_PACK16
 #define SPEF_MX_PACK16 1

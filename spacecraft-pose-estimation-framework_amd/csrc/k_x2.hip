@@ -453,21 +453,19 @@ struct X2wGeom {
   static constexpr int SE_B = 2 * 32 * WES * 2 + 32 * 4;   // hi / lo weight planes + expand bias
   static constexpr int SD_B = (9 * 32 + 32) * 4;            // depthwise weights [9][32] + depthwise bias
   static constexpr int SP_B = PST ? 2 * NPC * WPS * 2 : 0;
-#if SPEF_X2_GLDS
-  // LDS-DMA staging: every stage region a whole number of 1-KiB wave-instruction pieces (a piece writes 64 x 16 B
-  // lane-linearly); per buffer the depthwise and project stages are one contiguous region
+  // LDS-DMA staging (GL): every stage region a whole number of 1-KiB wave-instruction pieces (a piece writes 64 x 16 B
+  // lane-linearly); per buffer the depthwise and project stages are one contiguous region. Interleaved A/B at B = 64:
+  // blocks 14-17 -1.6 to -5 us per step, blocks 8-13 +12 / +36 us (their padded stages cost LDS), so cout >= 160 only.
+  static constexpr bool GL = SPEF_X2_GLDS && COUT >= 160;
   static constexpr int SE_BQ = (SE_B + 1023) / 1024 * 1024, SD_BQ = (SD_B + 1023) / 1024 * 1024;
   static constexpr int SP_BQ = (SP_B + 1023) / 1024 * 1024, DP_BQ = SD_BQ + SP_BQ;
-  static constexpr int SE_STR = SE_BQ, SD_STR = DP_BQ, SP_STR = DP_BQ;
-  static constexpr int OFF_SE = 2 * SLAB_B, OFF_SD = OFF_SE + 2 * SE_BQ, OFF_SP = OFF_SD + SD_BQ;
-  static constexpr int OFF_TR = OFF_SD + 2 * DP_BQ;
   static constexpr int NIE = SE_BQ / 1024, NID = DP_BQ / 1024;                  // pieces per chunk stage
   static constexpr int IEW = (NIE + NE - 1) / NE, IDW = (NID + ND - 1) / ND;    // pieces per wave
-#else
-  static constexpr int SE_STR = SE_B, SD_STR = SD_B, SP_STR = SP_B;
-  static constexpr int OFF_SE = 2 * SLAB_B, OFF_SD = OFF_SE + 2 * SE_B, OFF_SP = OFF_SD + 2 * SD_B;
-  static constexpr int OFF_TR = OFF_SP + 2 * SP_B;          // dummy rows: expand stores of invalid input pixels
-#endif
+  static constexpr int SE_STR = GL ? SE_BQ : SE_B, SD_STR = GL ? DP_BQ : SD_B, SP_STR = GL ? DP_BQ : SP_B;
+  static constexpr int OFF_SE = 2 * SLAB_B;
+  static constexpr int OFF_SD = GL ? OFF_SE + 2 * SE_BQ : OFF_SE + 2 * SE_B;
+  static constexpr int OFF_SP = GL ? OFF_SD + SD_BQ : OFF_SD + 2 * SD_B;
+  static constexpr int OFF_TR = GL ? OFF_SD + 2 * DP_BQ : OFF_SP + 2 * SP_B;   // dummy rows: invalid pixels' stores
   static constexpr int LDS_BYTES = OFF_TR + 16 * 24 * 4;
   // 16-B stage pieces per chunk
   static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = 9 * 8 + 8, NPP = PST ? 2 * NPC * 4 : 0;
@@ -553,8 +551,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     }
   };
 
-#if SPEF_X2_GLDS
-  // ---- LDS-DMA stage pieces. Expand waves: pieces e + NE j of the expand stage (weights hi / lo + bias); depthwise
+  // ---- LDS-DMA stage pieces (G::GL). Expand waves: pieces e + NE j of the expand stage (weights hi / lo + bias); depthwise
   // waves: pieces d + ND j of the depthwise + project stage. Lane l of piece i fills LDS slot 64 i + l of the region
   // from a source whose address at chunk k is src0 + k * kstr (pad slots read a valid address of the same tensor).
   const bool ewave = wave < G::NE;
@@ -614,15 +611,15 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
                                          (__attribute__((address_space(3))) void*)(base + i * 1024), 16, 0, 0);
     }
   };
-  if (ewave) {
-    dma(0);
-    dma(1);
+  if constexpr (G::GL) {
+    if (ewave) {
+      dma(0);
+      dma(1);
+    } else {
+      dma(0);
+    }
   } else {
-    dma(0);
-  }
-#else
   // ---- prologue (all waves): expand stages of chunks 0 and 1, depthwise / project stage of chunk 0
-  {
     constexpr int NP0 = 2 * G::NPE + G::NPD + G::NPP;
     constexpr int NIT = (NP0 + G::NW * 64 - 1) / (G::NW * 64);
     uint4 v[NIT];
@@ -640,7 +637,6 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     for (int i = 0; i < NIT; ++i)
       if (dst[i]) *reinterpret_cast<uint4*>(dst[i]) = v[i];
   }
-#endif
 
   if (wave < G::NE) {
     // ================= expand waves
@@ -733,7 +729,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     // Stage data is loaded one iteration before it is stored: the pieces of expand chunk c + 2 and depthwise /
     // project chunk c + 1 are fetched in iteration c - 1 (a whole chunk period of L2 latency hidden) and written to
     // LDS at the start of iteration c (the same buffers and barriers as a load-and-store in iteration c).
-#if SPEF_X2_GLDS
+    if constexpr (G::GL) {
     __syncthreads();                 // prologue stages landed (vmcnt(0) + barrier)
     expand(0);
     __syncthreads();                 // slab 0 visible
@@ -743,7 +739,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       if (c + 1 < G::NCL) expand(c + 1);
       __syncthreads();                  // (waits for this wave's pieces: visible to every wave after the barrier)
     }
-#else
+    } else {
     uint4 v[G::NPIECE];
     auto load_stage = [&](int c) {
 #if SPEF_X2_ABL_STAGE < 2   // timing ablation only (wrong results): 2 = no stage loads
@@ -780,7 +776,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       }
       __syncthreads();
     }
-#endif
+    }
   } else {
     // ================= depthwise / project waves
     const int d = wave - G::NE;
@@ -817,9 +813,8 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     __syncthreads();
 #pragma unroll 1
     for (int c = 0; c < G::NCL; ++c) {
-#if SPEF_X2_GLDS
-      if (c + 1 < G::NCL) dma(c + 1);   // depthwise + project stage of chunk c + 1 (buffer released by chunk c - 1)
-#endif
+      if constexpr (G::GL)
+        if (c + 1 < G::NCL) dma(c + 1);   // depthwise + project stage of chunk c + 1 (buffer released by chunk c - 1)
       const float* Sl = slab(c & 1);
       const float* D = sd(c & 1);
       f32x2 a[G::QPW][4];
