@@ -56,8 +56,8 @@ ARITH = {'fp16': 'fp16 storage, fp16 MFMA operands, fp32 accumulate (packed-fp16
          'bf16': 'bf16 storage, bf16 MFMA operands, fp32 accumulate',
          'int8': 'int8 MFMA, exact int32 accumulate, fixed-point requant',
          'fp16x2': 'fp32 activations; hi + lo fp16 MFMA operands (3 MFMAs per product), fp32 accumulate, fp32 depthwise',
-         'fp16mx': 'hi + lo fp16 MFMA operands, fp32 accumulate, fp32 depthwise; fp32 activations except the fp16 block '
-                   'outputs of blocks 1-6'}
+         'fp16mx': 'hi + lo fp16 MFMA operands, fp32 accumulate, fp32 depthwise; fp32 activations except fp16 storage '
+                   'of the stem map, the block outputs of blocks 1-3 and the hidden tensors of blocks 2-4'}
 
 
 def pmc_traffic(kernel_key: str, path: str):
@@ -72,14 +72,17 @@ def pmc_traffic(kernel_key: str, path: str):
     if kernel_key in kernels:
         return kernels[kernel_key]['hbm_bytes_per_launch']
     import re
-    m = re.fullmatch(r'(x2_irb_kernel|ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
+    m = re.fullmatch(r'(x2_irb_kernel|mx_irb_kernel|ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
     if m:   # fused block key -> the one template instantiation profiled for that geometry (fp16x2: slab or role-split)
         geo = ','.join(m.groups()[1:]) + ','
-        kind = r'x2_ir[bw]_kernel<' if m.group(1).startswith('x2') else m.group(1) + r'<B?F16,'
+        kind = {'x2_irb_kernel': r'x2_ir[bw]_kernel<', 'mx_irb_kernel': r'mx_irb_kernel<'}.get(m.group(1),
+                                                                                             m.group(1) + r'<B?F16,')
         hits = [v for k, v in kernels.items() if re.match(kind + re.escape(geo), k)]
     else:   # e.g. front_kernel<stem+block1> -> front_kernel<...> or its fp16 form front_vp_kernel<...>
         base = kernel_key.split('<')[0]
         prefixes = (base + '<', base.replace('_kernel', '_vp_kernel') + '<')
+        if base == 'mx_front_kernel':   # the fp16mx front kernel's symbol
+            prefixes = ('front_mx_kernel<',)
         hits = [v for k, v in kernels.items() if k.startswith(prefixes)]
     return hits[0]['hbm_bytes_per_launch'] if len(hits) == 1 else None
 

@@ -185,11 +185,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       bxl[j] = __builtin_bit_cast(f16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
     }
     const int ps = slab_slot(p);
-    if constexpr (SPEF_MX_ALIAS) {   // padding pixels store zeros every chunk (the exchange overwrites them)
-      soff[j] = p < G::PIN ? ps * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
-      if (!ok && p < G::PIN) zmask |= 1u << j;
-      continue;
-    }
+    if (!ok && p < G::PIN) zmask |= 1u << j;   // (SPEF_MX_ALIAS: re-zeroed every chunk on edge tiles)
     soff[j] = ok ? ps * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
     if (!ok && p < G::PIN) {   // the depthwise's zero padding: stored once, never overwritten
       *reinterpret_cast<uint2*>(smem + ps * G::SPB + 8 * kg) = make_uint2(0u, 0u);
@@ -255,8 +251,11 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
       for (int e = 0; e < 8; ++e) wd[tap][e] = wdc[tap * G::HIDP + e];
-#pragma unroll
-    for (int e = 0; e < 8; ++e) db[e] = bd[32 * c + 8 * wave + e];
+    {   // the bias as two vector loads (uniform address: VGPRs, keeping the 72 weights' SGPRs free of spills)
+      const float4 b0 = *reinterpret_cast<const float4*>(bd + 32 * c + 8 * (tid >> 6));
+      const float4 b1 = *reinterpret_cast<const float4*>(bd + 32 * c + 8 * (tid >> 6) + 4);
+      db[0] = b0.x; db[1] = b0.y; db[2] = b0.z; db[3] = b0.w; db[4] = b1.x; db[5] = b1.y; db[6] = b1.z; db[7] = b1.w;
+    }
 
     // ---- expand chunk c -> fp16 slab
     {
@@ -277,10 +276,17 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
           } else {
             e = mfma3(eah[h], eal[h], bx[j], bxl[IN16 ? 0 : j], e);
           }
-          uint2 st = make_uint2(relu_pk2(e[0], e[1]), relu_pk2(e[2], e[3]));
-          if (SPEF_MX_ALIAS && edge && ((zmask >> j) & 1u)) st = make_uint2(0u, 0u);
-          *reinterpret_cast<uint2*>(smem + soff[j] + 32 * h) = st;
+          *reinterpret_cast<uint2*>(smem + soff[j] + 32 * h) = make_uint2(relu_pk2(e[0], e[1]), relu_pk2(e[2], e[3]));
         }
+      }
+      if (SPEF_MX_ALIAS && edge && c > 0) {   // the exchange overlaid the slab: restore the depthwise's zero padding
+#pragma unroll
+        for (int j = 0; j < G::EPT; ++j)
+          if ((zmask >> j) & 1u) {
+            const int zo = slab_slot((wave + G::NW * j) * 16 + r16) * G::SPB + 8 * kg;
+            *reinterpret_cast<uint2*>(smem + zo) = make_uint2(0u, 0u);
+            *reinterpret_cast<uint2*>(smem + zo + 32) = make_uint2(0u, 0u);
+          }
       }
       if (c + 1 < G::NCH) load_e(c + 1);
     }
