@@ -120,7 +120,7 @@ __device__ void jacobi_sym(double (&a)[N][N], double (&v)[N][N]) {
 // least squares min ||A x - b|| for a full-column-rank 6 x NC A by Householder QR (epnp.cpp qr_solve)
 template <int NC>
 __device__ void qr_lstsq(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
-  double a1[NC], a2[NC], ia1[NC], ia2[NC];
+  double ia1[NC], ia2[NC];   // reciprocals of epnp.cpp's A1 / A2 (the only form the solve uses)
   for (int k = 0; k < NC; ++k) {
     double eta = 0.0;
     for (int i = k; i < 6; ++i) eta = fmax(eta, fabs(A[i][k]));
@@ -137,10 +137,8 @@ __device__ void qr_lstsq(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
     double sigma = dsqrt(sum2);
     if (A[k][k] < 0) sigma = -sigma;
     A[k][k] += sigma;
-    a1[k] = sigma * A[k][k];
-    a2[k] = -eta * sigma;
-    ia1[k] = ddiv(1.0, a1[k]);
-    ia2[k] = ddiv(1.0, a2[k]);
+    ia1[k] = ddiv(1.0, sigma * A[k][k]);
+    ia2[k] = ddiv(1.0, -eta * sigma);
     for (int j = k + 1; j < NC; ++j) {
       double sum = 0.0;
       for (int i = k; i < 6; ++i) sum += A[i][k] * A[i][j];
@@ -162,7 +160,7 @@ __device__ void qr_lstsq(double (&A)[6][NC], double (&b)[6], double (&x)[NC]) {
   }
 }
 
-__device__ void epnp_gn(const double (&L)[6][10], const double (&rho)[6], double (&b)[4]) {
+__device__ __forceinline__ void epnp_gn(const double (&L)[6][10], const double (&rho)[6], double (&b)[4]) {
   for (int it = 0; it < 5; ++it) {
     double A[6][4], r[6], x[4];
     for (int i = 0; i < 6; ++i) {
@@ -228,7 +226,15 @@ __device__ __forceinline__ int rr_partner(int r, int i) {
   return (2 * r - i + 22) % 11;
 }
 
-__global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw, int B, int n,
+#ifndef SPEF_EPNP_WPE   // waves per SIMD the register allocation targets (0: the compiler's choice: 312 registers, one wave per SIMD; 2: 256 + a 200-B spill, two workgroups per CU -- P = 1800: 365 -> 232 us, B = 64 unchanged)
+#define SPEF_EPNP_WPE 2
+#endif
+#if SPEF_EPNP_WPE
+#define SPEF_EPNP_ATTR __attribute__((amdgpu_waves_per_eu(SPEF_EPNP_WPE)))
+#else
+#define SPEF_EPNP_ATTR
+#endif
+__global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* __restrict__ raw, int B, int n,
                                                    const float* __restrict__ kp3d, const double* __restrict__ model,
                                                    double fu, double fv, double uc,
                                                    double vc, float nu, float nv, EpnpDist dist, int apply_sigmoid,
@@ -276,11 +282,7 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
       Pdv[lane] = vc - us1;
     }
   }
-  double cws[4][3];   // control points (model-only, spef_set_keypoints)
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 3; ++j) cws[i][j] = model[3 * i + j];
+  // control points: model[0..11] (model-only, spef_set_keypoints), read where used
   __syncthreads();
 
   // ---- M^T M (M never stored): entry e = (p, q) = thread e, accumulated point by point as r1[p] r1[q] + r2[p] r2[q]
@@ -455,17 +457,19 @@ __global__ __launch_bounds__(192) void epnp_kernel(const float* __restrict__ raw
     Ls[r][9] = dot(3, 3);
     double d2 = 0.0;
 #pragma unroll
-    for (int k = 0; k < 3; ++k) d2 += (cws[pa][k] - cws[pb][k]) * (cws[pa][k] - cws[pb][k]);
+    for (int k = 0; k < 3; ++k) {
+      const double dk = model[3 * pa + k] - model[3 * pb + k];
+      d2 += dk * dk;
+    }
     Rho[r] = d2;
   }
   __syncthreads();
-  double L[6][10], rho[6];
+  // L_6x10 stays in LDS (read where used, broadcast): as 60 fp64 registers it held the kernel at 256+ VGPRs, one
+  // wave per SIMD (one problem per CU at a time)
+  const double (&L)[6][10] = Ls;
+  double rho[6];
 #pragma unroll
-  for (int r = 0; r < 6; ++r) {
-    rho[r] = Rho[r];
-#pragma unroll
-    for (int k = 0; k < 10; ++k) L[r][k] = Ls[r][k];
-  }
+  for (int r = 0; r < 6; ++r) rho[r] = Rho[r];
   // pw centroid (uniform): a wave reduction over the point lanes
   double pw0[3];
   const double inv_n = ddiv(1.0, (double)n);

@@ -18,7 +18,7 @@ g = np.load(os.path.join(ROOT, 'tests', 'golden', 'keypoints.npz'))
 arch = mobilenet_v2('keypoints')
 eng = Engine(Bl.pack(synthetic_state_dict(arch, seed=1001, head_std=0.002), arch, dtype='fp32'), 'cuda:0')
 eng.set_keypoints(g['kp3d'], g['K'], float(g['nu']), float(g['nv']))
-for P in (64, 512):
+for P in (64, 512, 1800):
     kp = torch.from_numpy(np.ascontiguousarray(g['kp2d'][:P], np.float32)).cuda()
     o = eng.decode_keypoints(kp, apply_sigmoid=False)
     torch.cuda.synchronize()
