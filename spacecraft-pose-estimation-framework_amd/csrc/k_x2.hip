@@ -455,8 +455,9 @@ struct X2wGeom {
   static constexpr int SP_B = PST ? 2 * NPC * WPS * 2 : 0;
   // LDS-DMA staging (GL): every stage region a whole number of 1-KiB wave-instruction pieces (a piece writes 64 x 16 B
   // lane-linearly); per buffer the depthwise and project stages are one contiguous region. Interleaved A/B at B = 64:
-  // blocks 14-17 -1.6 to -5 us per step, blocks 8-13 +12 / +36 us (their padded stages cost LDS), so cout >= 160 only.
-  static constexpr bool GL = SPEF_X2_GLDS && COUT >= 160;
+  // blocks 14 and 15-16 -2 / -5 us per step, block 17 +3, blocks 8-13 no gain (same box, interleaved), so the
+  // cout = 160 blocks only.
+  static constexpr bool GL = SPEF_X2_GLDS && COUT == 160;
   static constexpr int SE_BQ = (SE_B + 1023) / 1024 * 1024, SD_BQ = (SD_B + 1023) / 1024 * 1024;
   static constexpr int SP_BQ = (SP_B + 1023) / 1024 * 1024, DP_BQ = SD_BQ + SP_BQ;
   static constexpr int NIE = SE_BQ / 1024, NID = DP_BQ / 1024;                  // pieces per chunk stage
@@ -556,11 +557,11 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   // from a source whose address at chunk k is src0 + k * kstr (pad slots read a valid address of the same tensor).
   const bool ewave = wave < G::NE;
   const int wr = ewave ? wave : wave - G::NE;
-  constexpr int NJ = G::IEW > G::IDW ? G::IEW : G::IDW;
+  constexpr int NJ = G::GL ? (G::IEW > G::IDW ? G::IEW : G::IDW) : 1;
   const char* gsrc[NJ];
   int kstr[NJ];
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) {
+  for (int j = 0; j < (G::GL ? NJ : 0); ++j) {
     const int off = ((ewave ? wr + G::NE * j : wr + G::ND * j) * 64 + lane) * 16;   // byte offset in the region
     const char* src;
     int ks;
@@ -602,6 +603,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   }
   // issue this wave's pieces of chunk k's stage (expand waves: the expand stage; depthwise waves: depthwise + project)
   auto dma = [&](int k) {
+    if constexpr (!G::GL) return;
     char* base = ewave ? smem + G::OFF_SE + (k & 1) * G::SE_STR : smem + G::OFF_SD + (k & 1) * G::SD_STR;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
@@ -923,6 +925,22 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
 // (8x8, g 2) -> 125 (8x16, g 2) -> 89 us (8x16, g 1); blocks 15-16 93 -> 91 us (g 2 -> 1); block 17 142 us at g 4,
 // 125 at g 2, 322 at g 1 (80 accumulator registers per wave: spills). URSONet step 2.11 -> 1.85 ms, keypoint mode
 // 1.27 -> 1.05 ms (with the small-map table below).
+// Blocks 8-13. SPEF_X2_MID8 = 1: 8 x 8 tiles with the project weights from L2 (kind 2): 68-76 KB of LDS, two
+// workgroups per CU, against 8 x 16 tiles with LDS-staged project weights at 123-144 KB (one per CU).
+#ifndef SPEF_X2_MID8
+#define SPEF_X2_MID8 0
+#endif
+#if SPEF_X2_MID8
+#define SPEF_X2_MID(X)                                           \
+  X(64, 384, 64, 1, true, true, 8, 8, 8, 1, 2)      /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 8, 8, 1, 2)     /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 8, 8, 1, 2)      /* 12-13 */
+#else
+#define SPEF_X2_MID(X)                                           \
+  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, 1)     /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, 1)    /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, 1)     /* 12-13 */
+#endif
 #define SPEF_X2_TABLE(X)                                         \
   X(32, 32, 16, 1, false, false, 8, 16, 4, 1, 0)    /* 1 */      \
   X(16, 96, 24, 2, true, false, 8, 8, 4, 1, 0)      /* 2 */      \
@@ -930,9 +948,7 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(24, 144, 32, 2, true, false, 8, 8, 4, 1, 0)     /* 4 */      \
   X(32, 192, 32, 1, true, true, 8, 16, 4, 1, 0)     /* 5-6 */    \
   X(32, 192, 64, 2, true, false, 8, 8, 4, 1, 0)     /* 7 */      \
-  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, 1)     /* 8-10 */   \
-  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, 1)    /* 11 */     \
-  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, 1)     /* 12-13 */  \
+  SPEF_X2_MID(X)                                                 \
   X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
