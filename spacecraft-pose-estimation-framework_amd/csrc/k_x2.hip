@@ -952,12 +952,12 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
-// 16x16 tiles with 8 waves (2 workgroups per CU) where they tile the map exactly: blocks 3, 5-6 at 512^2 (interleaved
-// A/B: 165 -> 153 us and 119 -> 115 us per step); on maps they do not divide (60x96, 30x48 at 240x384) the partial
-// tiles cost more than the occupancy gains.
+// 16x16 tiles with 8 waves (2 workgroups per CU) where they tile the map exactly: block 3 at 512^2 (interleaved A/B,
+// round 4: 165 -> 153 us per step); on maps they do not divide (60x96, 30x48 at 240x384) the partial tiles cost more
+// than the occupancy gains. Blocks 5-6 left this table in round 5: behind the fp16mx front end 8 x 16 tiles measured
+// 139 -> 117 us per step (round 4, fp16x2: 119 -> 115 the other way).
 #define SPEF_X2_EXACT_TABLE(X)                                      \
-  X(24, 144, 24, 1, true, true, 16, 16, 8, 1, 0)     /* 3 */      \
-  X(32, 192, 32, 1, true, true, 16, 16, 8, 1, 0)     /* 5-6 */
+  X(24, 144, 24, 1, true, true, 16, 16, 8, 1, 0)     /* 3 */
 // Maps whose primary tiling leaves CUs idle (fewer workgroups than CUs; the role-split kernels run one workgroup
 // per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64) split the hidden dimension over P
 // workgroups per tile (last field; partial sums joined by x2_split_reduce_kernel in the caller's scratch).
@@ -1062,8 +1062,12 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
                                                                          OW, s, scratch);
   SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
 #undef SPEF_X2_SMALL
+#ifndef SPEF_X2_EXACT_ON   // A/B aid: 0 = the primary 8 x 16 tiles on exact maps too
+#define SPEF_X2_EXACT_ON 1
+#endif
 #define SPEF_X2_EXACT(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                        \
-  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && OH % (TH_) == 0 &&  \
+  if (SPEF_X2_EXACT_ON && cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS &&  \
+      OH % (TH_) == 0 &&                                                                                        \
       OW % (TW_) == 0)                                                                                        \
     SPEF_X2_IO_SWITCH(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)
   SPEF_X2_EXACT_TABLE(SPEF_X2_EXACT)
