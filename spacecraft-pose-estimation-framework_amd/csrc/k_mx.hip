@@ -411,7 +411,7 @@ static hipError_t mx_go(const void* x, const void* we, const float* be, const fl
 #define SPEF_MX_TH_S2 8
 #endif
 #ifndef SPEF_MX_TH_S1
-#define SPEF_MX_TH_S1 8
+#define SPEF_MX_TH_S1 16
 #endif
 // Blocks 5-7 keep an fp32 hidden tensor (the fp16x2 slab kernel, k_x2.hip): their fp16 hidden storage would add 31 % to
 // the schedule's logit error variance (tools/precision_budget.py: rms 1.21e-4 -> 1.46e-4 on the parity tests' frames)
