@@ -478,6 +478,9 @@ struct X2wGeom {
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
+#ifndef SPEF_X2_PRE   // register-staged blocks: stage-piece addresses evaluated once per workgroup
+#define SPEF_X2_PRE 0   // measured: no gain (blocks 12-13 181 -> 180, 8-10 162 -> 167 us per step)
+#endif
 #ifndef SPEF_X2_ABL_STAGE
 #define SPEF_X2_ABL_STAGE 0
 #endif
@@ -743,14 +746,48 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     }
     } else {
     uint4 v[G::NPIECE];
+    // PRE (the staged-project blocks 8-13): each piece's address pair evaluated once -- source pointer advanced by its
+    // per-chunk stride, destination toggled between the two stage buffers -- instead of piece()'s integer divisions
+    // per piece and chunk (~40 VALU each, twice per chunk: the expand role's VALU exceeded its MFMA time)
+    constexpr bool PRE = SPEF_X2_PRE && PST;
+    constexpr int NPR = PRE ? G::NPIECE : 1;
+    const char* psrc[NPR];
+    int pstr[NPR], pdst[NPR], pxor[NPR];
+    uint32_t pkind = 0;   // bit i: piece i is a depthwise / project piece (chunk c + 1), else expand (chunk c + 2)
+    uint32_t pval = 0;    // bit i: piece i exists
+    if constexpr (PRE) {
+#pragma unroll
+      for (int i = 0; i < NPR; ++i) {
+        const int u = tid + G::NE * 64 * i;
+        const void *s0, *s1;
+        void *d0, *d1;
+        piece(u, 0, 0, s0, d0);
+        piece(u, 1, 1, s1, d1);
+        if (s0) pval |= 1u << i;
+        if (u >= G::NPE) pkind |= 1u << i;
+        psrc[i] = reinterpret_cast<const char*>(s0);
+        pstr[i] = s0 ? (int)(reinterpret_cast<const char*>(s1) - reinterpret_cast<const char*>(s0)) : 0;
+        pdst[i] = s0 ? (int)(reinterpret_cast<char*>(d0) - smem) : 0;
+        pxor[i] = s0 ? (int)(reinterpret_cast<char*>(d0) - smem) ^ (int)(reinterpret_cast<char*>(d1) - smem) : 0;
+        // chunk of the first load_stage(0): expand c + 2 = 2, depthwise / project c + 1 = 1 (buffers 0 / 1)
+        const int k0 = (u >= G::NPE) ? 1 : 2;
+        psrc[i] += (size_t)k0 * pstr[i];
+        if (k0 & 1) pdst[i] ^= pxor[i];
+      }
+    }
     auto load_stage = [&](int c) {
 #if SPEF_X2_ABL_STAGE < 2   // timing ablation only (wrong results): 2 = no stage loads
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
-        const void* src;
-        void* dst;
-        piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
-        v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        if constexpr (PRE) {
+          const int k = ((pkind >> i) & 1u) ? c + 1 : c + 2;
+          v[i] = ((pval >> i) & 1u) && k < G::NCL ? *reinterpret_cast<const uint4*>(psrc[i]) : make_uint4(0, 0, 0, 0);
+        } else {
+          const void* src;
+          void* dst;
+          piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
+          v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
+        }
       }
 #endif
     };
@@ -758,10 +795,17 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
 #if SPEF_X2_ABL_STAGE < 1   // timing ablation only (wrong results): 1 = no stage stores
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
-        const void* src;
-        void* dst;
-        piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
-        if (src) *reinterpret_cast<uint4*>(dst) = v[i];
+        if constexpr (PRE) {
+          const int k = ((pkind >> i) & 1u) ? c + 1 : c + 2;
+          if (((pval >> i) & 1u) && k < G::NCL) *reinterpret_cast<uint4*>(smem + pdst[i]) = v[i];
+          psrc[i] += pstr[i];      // next chunk's source and buffer
+          pdst[i] ^= pxor[i];
+        } else {
+          const void* src;
+          void* dst;
+          piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
+          if (src) *reinterpret_cast<uint4*>(dst) = v[i];
+        }
       }
 #endif
     };
