@@ -250,6 +250,10 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (b >= B) return;   // uniform per workgroup
+#if defined(SPEF_EPNP_ABL) && SPEF_EPNP_ABL == 4   // timing ablation: launch only
+  if (tid == 0) status[b] = 0;
+  return;
+#endif
   const int nk = 2 * (n + 1);
 
   // ---- points: lane i <= n reads raw point i (origin first); lane j < n then owns keypoint j (every wave)
@@ -308,6 +312,10 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
   // ---- parallel cyclic Jacobi (tournament order): sweeps of 11 rounds x 6 disjoint rotations
 #ifndef SPEF_EPNP_ABL   // timing ablations only (wrong results): 1 = no Jacobi sweeps, 2 = approximation 1 only
 #define SPEF_EPNP_ABL 0
+#endif
+#if SPEF_EPNP_ABL == 3   // timing ablation: set-up (points, M^T M) only
+  if (tid == 0) status[b] = (int)(As[0][0] != 0.0);
+  return;
 #endif
   int cur = 0;
 #if SPEF_EPNP_FUSEROT
