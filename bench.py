@@ -514,6 +514,9 @@ def main():
                     help='CPU + gloo: the distributed control flow (weight distribution, timing, max over ranks, '
                          'JSON) without device work')
     args = ap.parse_args()
+    if args.graphs:   # every (stream, frame buffer) key recorded before timing starts (recording is not timed work)
+        import math
+        args.warmup = max(args.warmup, math.lcm(max(1, args.inflight), args.frame_buffers))
     if args.traffic is None:   # the newest committed FETCH/WRITE summary of this path
         args.traffic = newest_profile(TRAFFIC[args.dtype])
 
@@ -625,6 +628,9 @@ def main():
             'steps': args.steps,
             'warmup': args.warmup,
             'clock_settle_s': 0.0 if args.dry_run else args.settle,
+            **({'graphs': 'replayed HIP graphs: each replay reuses its key\'s graph-owned outputs, so the per-step '
+                          'decode-status check sees the last replay of every (stream, frame buffer) key'}
+               if args.graphs else {}),
             'ms_per_step': round(elapsed / args.steps * 1e3, 4),
             'higher_is_better': True,
             'scaling': 'weak',

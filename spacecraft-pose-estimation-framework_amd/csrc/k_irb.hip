@@ -968,11 +968,11 @@ static hipError_t irb_go(const void* x, const void* we, const float* be, const v
   const uint32_t nwg = (uint32_t)nwg64;
   const size_t lds = (size_t)G::LDS_BYTES;
   auto k = irb_kernel<DT, CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, DBUF, STW, ABL>;
-  static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
-  if (!attr_set && lds > 65536) {
+  static DevOnce attr_set;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
+  if (!attr_set.done() && lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set.set();
   }
   k<<<nwg, NW * 64, lds, s>>>((const T*)x, (const T*)we, be, (const DW*)wd, bd, (const T*)wp, bp, (T*)y, H, W, OH, OW, tiles_x,
                               tiles_y, nwg);
@@ -1013,10 +1013,14 @@ static hipError_t irb_dispatch(int variant, int cin, int hid, int cout, int stri
 #undef SPEF_IRB_ABL_CASE
     variant = 0;
   }
+  const bool lib_default = variant < 0;   // SPEF_OPT_IRB_VARIANT unset (an explicit 0 from a sweep stays 0)
   if (!irb_has(variant, cin, hid, cout, stride, expand, res)) variant = 0;
   // Blocks 5-6 take the 16x16 / 8-wave tiles (variant 1) where those tile the map exactly (64x64 at 512^2): pipelined
-  // bench 94.6k -> 95.2k img/s (interleaved, 5 pairs); on maps they do not divide, the 8x16 / 4-wave tiles.
-  if (variant == 0 && cin == 32 && hid == 192 && cout == 32 && stride == 1 && OH % 16 == 0 && OW % 16 == 0) variant = 1;
+  // bench 94.6k -> 95.2k img/s (interleaved, 5 pairs); on maps they do not divide, the 8x16 / 4-wave tiles. Only as
+  // the library default, and only where variant 1 exists for the full geometry (expand and residual included).
+  if (lib_default && irb_has(1, cin, hid, cout, stride, expand, res) && cin == 32 && hid == 192 && cout == 32 &&
+      stride == 1 && OH % 16 == 0 && OW % 16 == 0)
+    variant = 1;
 #define SPEF_IRB_CASE(V, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_)                            \
   if (variant == V && cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)   \
     return irb_go<DT, CI, HI, CO, ST, TH_, TW_, EX, RS, NW_, WC_, DB_, SW_>(x, we, be, wd, bd, wp, bp, y, B, H, W, \

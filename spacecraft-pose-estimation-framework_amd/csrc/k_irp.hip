@@ -443,11 +443,11 @@ static hipError_t irp_go(const void* x, const void* we, const float* be, const v
   const uint32_t nwg = (uint32_t)nwg64;
   const size_t lds = (size_t)G::LDS_BYTES;
   auto k = irp_kernel<DT, CIN, HID, COUT, S, TH, TW, RES, NM, NV>;
-  static bool attr_set = false;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
-  if (!attr_set && lds > 65536) {
+  static DevOnce attr_set;   // > 64 KiB dynamic LDS needs the attribute (once per instantiation)
+  if (!attr_set.done() && lds > 65536) {
     hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set.set();
   }
   k<<<nwg, G::NW * 64, lds, s>>>((const T*)x, (const T*)we, be, (const DW*)wd, bd, (const T*)wp, bp, (T*)y, H, W, OH,
                                  OW, tiles_x, tiles_y, nwg);

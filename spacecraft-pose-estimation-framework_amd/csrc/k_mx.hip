@@ -392,11 +392,11 @@ static hipError_t mx_go(const void* x, const void* we, const float* be, const fl
   const uint32_t nwg = (uint32_t)nwg64;
   auto k = mx_irb_kernel<CIN, HID, COUT, S, TH, RES, IN16, OUT16>;
   if (G::LDS_BYTES > 65536) {
-    static bool attr_set = false;   // per process: the attribute is a property of the code object
-    if (!attr_set) {
+    static DevOnce attr_set;   // per device
+    if (!attr_set.done()) {
       hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
       if (e != hipSuccess) return e;
-      attr_set = true;
+      attr_set.set();
     }
   }
   k<<<nwg, 256, G::LDS_BYTES, s>>>(x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp, y, H,

@@ -377,11 +377,11 @@ hipError_t q_irb_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
   const uint32_t nwg = (uint32_t)nwg64;
   auto k = q_irb_kernel<CIN, HID, COUT, S, TH, TW, RES, NW, EXPAND, SH32>;
   constexpr int lds = G::LDS_BYTES - ((EXPAND || RES) ? 0 : G::PINP * G::XSB);   // see XREG in the kernel
-  static bool attr_set = false;
-  if (!attr_set && lds > 65536) {
+  static DevOnce attr_set;
+  if (!attr_set.done() && lds > 65536) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, lds);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set.set();
   }
   k<<<nwg, NW * 64, lds, s>>>(x, we, wp, pinit, tabs, rm, rb, rs, (1 << qb.eb) - 1, (1 << qb.db) - 1,
                               -(1 << (qb.sb - 1)), (1 << (qb.sb - 1)) - 1, y, H, W, OH, OW, tiles_x, tiles_y, nwg);

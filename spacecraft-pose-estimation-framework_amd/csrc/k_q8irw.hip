@@ -373,11 +373,11 @@ hipError_t q_irw_go(const int8_t* x, const int8_t* we, const int8_t* wp, const i
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   auto k = q_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, NE, ND, SH32>;
-  static bool attr_set = false;
-  if (!attr_set && G::LDS_BYTES > 65536) {
+  static DevOnce attr_set;
+  if (!attr_set.done() && G::LDS_BYTES > 65536) {
     const hipError_t e = hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, G::LDS_BYTES);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set.set();
   }
   k<<<nwg, G::NW * 64, G::LDS_BYTES, s>>>(x, we, wp, pinit, tabs, rm, rb, rs, (1 << qb.eb) - 1, (1 << qb.db) - 1,
                                           -(1 << (qb.sb - 1)), (1 << (qb.sb - 1)) - 1, y, H, W, OH, OW, tiles_x,

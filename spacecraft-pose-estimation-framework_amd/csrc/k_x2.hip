@@ -1030,14 +1030,14 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B * P;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  static bool attr_set = false;
+  static DevOnce attr_set;
   if constexpr (KIND == 0) {
     using G = X2Geom<CIN, HID, COUT, S, TH, TW, EXPAND, NW, WCO>;
     auto k = x2_irb_kernel<CIN, HID, COUT, S, TH, TW, EXPAND, RES, NW, WCO, IO>;
-    if (!attr_set) {
+    if (!attr_set.done()) {
       hipError_t e = x2_set_lds(k, G::LDS_BYTES);
       if (e != hipSuccess) return e;
-      attr_set = true;
+      attr_set.set();
     }
     k<<<nwg, NW * 64, G::LDS_BYTES, s>>>(x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp, y, H, W, OH, OW,
                                         tiles_x, tiles_y, nwg);
@@ -1045,10 +1045,10 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
     static_assert(EXPAND && NW == 8, "role-split blocks expand, 4 + 4 waves");
     using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND == 1, P>;
     auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND == 1, P>;
-    if (!attr_set) {
+    if (!attr_set.done()) {
       hipError_t e = x2_set_lds(k, G::LDS_BYTES);
       if (e != hipSuccess) return e;
-      attr_set = true;
+      attr_set.set();
     }
     const size_t pstride = (size_t)B * OH * OW * COUT;   // floats per hidden part (16-B multiple: COUT % 4 == 0)
     if (P > 1 && !scratch) return hipErrorInvalidValue;
@@ -1078,14 +1078,11 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
   if (!x || !y || !wd || !bd || !wp || !bp || (expand && (!we || !be)) || io < 0 || io > 3) return hipErrorInvalidValue;
   int num_cu = 0;
   {
-    static int cus = 0;   // (first call per process; the library runs on one device type)
-    if (!cus) {
-      int dev = 0;
-      if (hipGetDevice(&dev) != hipSuccess ||
-          hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus = 256;
-    }
-    num_cu = cus;
+    static int cus[32] = {};   // per device (first call on each)
+    const int dev = DevOnce::dev();
+    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus[dev] = 256;
+    num_cu = cus[dev];
   }
 #define SPEF_X2_IO_SWITCH(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                    \
   switch (io) {                                                                                               \
@@ -1412,11 +1409,11 @@ static hipError_t x2_front_go(const void* x, const void* wsx, const float* bs, c
   const int64_t nwg64 = (int64_t)tiles_x * tiles_y * B;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
-  static bool attr_set = false;
-  if (!attr_set) {
+  static DevOnce attr_set;
+  if (!attr_set.done()) {
     hipError_t e = x2_set_lds(x2_front_kernel<TH, TW, NW, OUT16>, G::LDS_BYTES);
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set.set();
   }
   x2_front_kernel<TH, TW, NW, OUT16><<<nwg, NW * 64, G::LDS_BYTES, s>>>((const uint8_t*)x, (const _Float16*)wsx, bs,
                                                                       wd, bd, (const _Float16*)wp, bp, y, H, W, OH, OW,
@@ -1487,7 +1484,7 @@ __global__ __launch_bounds__(256) void x2_pw_kernel(const float* __restrict__ X,
       for (int m = 0; m < MT; ++m) acc[a][m] = mfma_x2(ah, al, bh[m], bl[m], acc[a][m]);
     }
   }
-  if constexpr (POOL) {   // MT = 4: the wave's 64 pixels m0 .. m0 + 63, all valid (M % 64 == 0)
+  if constexpr (POOL) {   // MT = 4: the wave's 64 pixels m0 .. m0 + 63, all valid when m0 < M (M % 64 == 0)
 #pragma unroll
     for (int a = 0; a < NT; ++a) {
       float sm[4];
@@ -1501,7 +1498,7 @@ __global__ __launch_bounds__(256) void x2_pw_kernel(const float* __restrict__ X,
         sm[r] = t;
       }
       const int i = n0 + 16 * a + 4 * kg;
-      if (r16 == 0 && i < N)
+      if (r16 == 0 && i < N && m0 < M)   // (a workgroup's last waves may lie past M: no partial for them)
         *reinterpret_cast<float4*>(Y + (size_t)(m0 / 64) * N + i) = make_float4(sm[0], sm[1], sm[2], sm[3]);
     }
     return;
@@ -1630,7 +1627,7 @@ __global__ __launch_bounds__(256) void x2_pws_kernel(const float* __restrict__ X
         sm[r] = t;
       }
       const int i = n0 + 16 * a + 4 * kg;
-      if (r16 == 0 && i < N)
+      if (r16 == 0 && i < N && m0 < M)   // (a workgroup's last waves may lie past M: no partial for them)
         *reinterpret_cast<float4*>(Y + (size_t)(m0 / 64) * N + i) = make_float4(sm[0], sm[1], sm[2], sm[3]);
     }
     return;
@@ -1660,11 +1657,11 @@ static hipError_t x2_pws_go(const void* x, const void* wt, const float* bias, fl
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   const int lds = 64 * Kp * 2 * (int)sizeof(_Float16);
-  static bool attr_set = false;
-  if (!attr_set) {
+  static DevOnce attr_set;
+  if (!attr_set.done()) {
     hipError_t e = x2_set_lds(x2_pws_kernel<POOL>, 64 * 320 * 2 * (int)sizeof(_Float16));   // the largest Kp
     if (e != hipSuccess) return e;
-    attr_set = true;
+    attr_set.set();
   }
   x2_pws_kernel<POOL><<<nwg, 256, lds, s>>>((const float*)x, (const _Float16*)wt, bias, y, M, K, N, Np, Kp, n_chunks,
                                             nwg);

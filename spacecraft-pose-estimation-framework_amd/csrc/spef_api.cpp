@@ -74,11 +74,11 @@ struct spef_ctx {
   int fuse = 1;              // SPEF_OPT_FUSE_BLOCKS: 0 never, 1 when input H*W >= fuse_min_hw
   int64_t fuse_min_hw = 0;   // SPEF_OPT_FUSE_MIN_HW
   int gemm = 1;              // SPEF_OPT_PW_GEMM: 1 LDS-tiled GEMM, 0 register-direct pw kernel
-  int irb_variant = 0;       // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps)
+  int irb_variant = -1;      // SPEF_OPT_IRB_VARIANT: fused-block tile variant (tuning sweeps; -1 = library default)
   int wavespec = 2;          // SPEF_OPT_WAVESPEC: 2 = pipelined (k_irp.hip), 1 = wave-specialised (k_irw.hip)
   int q8_rolesplit = 0;      // SPEF_OPT_Q8_ROLESPLIT: int8 blocks 8-17 role-split (k_q8irw.hip)
   int test_fail_bcast = 0;   // SPEF_OPT_TEST_FAIL_BCAST (spef_tuning.hpp): failure injection in spef_bcast_weights
-  bool probe_f16 = false;    // run_backbone: the activation it stopped at is fp16 (fp16mx blocks 1-6)
+  bool probe_f16 = false;    // run_backbone: the activation it stopped at is fp16 (fp16mx: blocks 1-3)
   int mx_kernels = 1;        // SPEF_OPT_MX_KERNELS (spef_tuning.hpp): fp16mx blocks 2-7 on k_mx.hip
   // int8 blob: host copies of the FC quantisation constants, and their per-map-size device forms
   std::vector<double> q8_sw, q8_bias;

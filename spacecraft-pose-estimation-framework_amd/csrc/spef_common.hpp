@@ -8,6 +8,19 @@
 
 namespace spef {
 
+// "Done once per device" flag (bit d: device d) for host-side launch set-up such as hipFuncSetAttribute: one process
+// may drive several GPUs, and the attribute applies to the current device's instance of the kernel. (A race only
+// repeats the idempotent set-up.)
+struct DevOnce {
+  uint32_t mask = 0;
+  static int dev() {
+    int d = 0;
+    return hipGetDevice(&d) == hipSuccess ? (d & 31) : 0;
+  }
+  bool done() const { return (mask >> dev()) & 1u; }
+  void set() { mask |= 1u << dev(); }
+};
+
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
