@@ -83,6 +83,8 @@ def pmc_traffic(kernel_key: str, path: str):
         prefixes = (base + '<', base.replace('_kernel', '_vp_kernel') + '<')
         if base == 'mx_front_kernel':   # the fp16mx front kernel's symbol
             prefixes = ('front_mx_kernel<',)
+        elif base == 'x2_pw_kernel' and kernel_key.endswith('<pool>'):   # the staged last conv + mean
+            prefixes = ('x2_pws_kernel<',)
         hits = [v for k, v in kernels.items() if k.startswith(prefixes)]
     return hits[0]['hbm_bytes_per_launch'] if len(hits) == 1 else None
 
