@@ -430,6 +430,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
 // Stage buffers (double-buffered, written one iteration before use): expand weights + expand bias of chunk k in
 // iteration k - 2, depthwise weights + bias and project weights of chunk k in iteration k - 1. Same arithmetic and
 // rounding as x2_irb_kernel (bit-identical results).
+#ifndef SPEF_X2_STAMP   // timing builds only (outputs overwritten): s_memtime stamps per chunk of one workgroup
+#define SPEF_X2_STAMP 0
+#endif
 #ifndef SPEF_X2_GLDS   // stage the role-split kernels' chunk weights by LDS-DMA (global_load_lds) instead of registers
 #define SPEF_X2_GLDS 1
 #endif
@@ -467,7 +470,8 @@ struct X2wGeom {
   static constexpr int OFF_SD = GL ? OFF_SE + 2 * SE_BQ : OFF_SE + 2 * SE_B;
   static constexpr int OFF_SP = GL ? OFF_SD + SD_BQ : OFF_SD + 2 * SD_B;
   static constexpr int OFF_TR = GL ? OFF_SD + 2 * DP_BQ : OFF_SP + 2 * SP_B;   // dummy rows: invalid pixels' stores
-  static constexpr int LDS_BYTES = OFF_TR + 16 * 24 * 4;
+  static constexpr int OFF_ST = OFF_TR + 16 * 24 * 4;     // SPEF_X2_STAMP: per-chunk clock stamps (timing builds)
+  static constexpr int LDS_BYTES = OFF_ST + (SPEF_X2_STAMP ? 8 * 4 * 64 : 0);
   // 16-B stage pieces per chunk
   static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = 9 * 8 + 8, NPP = PST ? 2 * NPC * 4 : 0;
   static constexpr int NPIECE = (NPE + NPD + NPP + NE * 64 - 1) / (NE * 64);
@@ -500,6 +504,13 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
   uint32_t L = xcd_remap(blockIdx.x, nwg);
+  const bool stamp_wg = SPEF_X2_STAMP && L == 0;   // the workgroup of tile 0 (its output holds the stamps)
+  auto stamp = [&](int c, int slot) {              // lane 0 of waves 0 / 4: shader clock into LDS slot (c, slot)
+    if constexpr (SPEF_X2_STAMP) {
+      if (stamp_wg && lane == 0 && c < 64)
+        reinterpret_cast<uint32_t*>(smem + G::OFF_ST)[c * 8 + slot] = (uint32_t)__builtin_amdgcn_s_memtime();
+    }
+  };
   const int part = (int)(L % (uint32_t)P);        // hidden part (the parts of a tile share an XCD)
   L /= (uint32_t)P;
   const int cb = part * G::NCL;                    // first hidden chunk of this part
@@ -740,8 +751,10 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     __syncthreads();                 // slab 0 visible
 #pragma unroll 1
     for (int c = 0; c < G::NCL; ++c) {
+      if (wave == 0) stamp(c, 0);
       if (c + 2 < G::NCL) dma(c + 2);   // expand stage of chunk c + 2 into the buffer chunk c's expand released
       if (c + 1 < G::NCL) expand(c + 1);
+      if (wave == 0) stamp(c, 1);
       __syncthreads();                  // (waits for this wave's pieces: visible to every wave after the barrier)
     }
     } else {
@@ -815,11 +828,14 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     __syncthreads();                 // slab 0 visible
 #pragma unroll 1
     for (int c = 0; c < G::NCL; ++c) {
+      if (wave == 0) stamp(c, 0);
       store_stage(c);                // expand chunk c + 2, depthwise / project chunk c + 1
+      if (wave == 0) stamp(c, 2);
       if (c + 1 < G::NCL) {
         load_stage(c + 1);
         expand(c + 1);
       }
+      if (wave == 0) stamp(c, 1);
       __syncthreads();
     }
     }
@@ -859,6 +875,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     __syncthreads();
 #pragma unroll 1
     for (int c = 0; c < G::NCL; ++c) {
+      if (wave == G::NE) stamp(c, 4);
       if constexpr (G::GL)
         if (c + 1 < G::NCL) dma(c + 1);   // depthwise + project stage of chunk c + 1 (buffer released by chunk c - 1)
       const float* Sl = slab(c & 1);
@@ -890,6 +907,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       f16x8 bh[G::QPW], bl[G::QPW];
 #pragma unroll
       for (int q = 0; q < G::QPW; ++q) relu_split8(a[q], bh[q], bl[q]);
+      if (wave == G::NE) stamp(c, 5);
       if constexpr (PST) {
         const _Float16* Ps = sp(c & 1);
 #pragma unroll
@@ -907,6 +925,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
           for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(pgh[t], pgl[t], bh[q], bl[q], acc[q][t]);
         if (c + 1 < G::NCL) load_pg(c + 1);   // next chunk's fragments: in flight across the barrier and its depthwise
       }
+      if (wave == G::NE) stamp(c, 6);
       __syncthreads();
     }
     // epilogue: + residual (fp32 block input) -> fp32 NHWC
@@ -932,6 +951,13 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         }
         *reinterpret_cast<float4*>(Y + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
       }
+    }
+  }
+  if constexpr (SPEF_X2_STAMP) {   // every wave: the last barrier, then the stamps over the start of tile 0's output
+    __syncthreads();
+    if (stamp_wg && tid < 8 * 64) {
+      const int n = 8 * (G::NCL < 64 ? G::NCL : 64);
+      if (tid < n) reinterpret_cast<uint32_t*>(Y)[tid] = reinterpret_cast<const uint32_t*>(smem + G::OFF_ST)[tid];
     }
   }
 }
