@@ -111,10 +111,12 @@ __device__ __forceinline__ void st_act4(void* p, size_t i, f32x4 v, bool f16) {
 // MI355X_MICROARCH.md (LDS): 24 floats make the 16 consecutive rows of a 16-wide stride-1 pixel tile conflict-free
 // (2-way on 8-wide tiles), 20 floats the stride-2 rows; the plane-1 base is offset to keep the expand's mixed-plane
 // stores conflict-free.
-template <int S, int PINP>
+// XC (channel-split depthwise, below): 20-float rows with the plane-1 base at granule 0 keep the expand's stores
+// conflict-free and its pixel-major reads at most 1.6-way (checked against the lane groups).
+template <int S, int PINP, bool XC = false>
 struct X2Slab {
-  static constexpr int SSP = S == 2 ? 20 : 24;                   // floats per pixel row of a plane
-  static constexpr int TGT = S == 2 ? 0 : 1;                     // plane-1 base, granules mod 16
+  static constexpr int SSP = (S == 2 || XC) ? 20 : 24;           // floats per pixel row of a plane
+  static constexpr int TGT = (S == 2 || XC) ? 0 : 1;             // plane-1 base, granules mod 16
   static constexpr int PLANE = PINP * SSP + ((TGT - PINP * SSP / 4) % 16 + 16) % 16 * 4;
   static constexpr int FLOATS = 2 * PLANE;
   static __device__ __forceinline__ int at(int p, int c4) {      // float offset of channels 4 c4 .. 4 c4 + 3 of pixel p
@@ -433,6 +435,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
 #ifndef SPEF_X2_STAMP   // timing builds only (outputs overwritten): s_memtime stamps per chunk of one workgroup
 #define SPEF_X2_STAMP 0
 #endif
+#ifndef SPEF_X2_XC   // channel-split depthwise + exchange + lagged project in the role-split kernels
+#define SPEF_X2_XC 0
+#endif
 #ifndef SPEF_X2_GLDS   // stage the role-split kernels' chunk weights by LDS-DMA (global_load_lds) instead of registers
 #define SPEF_X2_GLDS 1
 #endif
@@ -444,18 +449,24 @@ struct X2wGeom {
   static constexpr int CINP = (CIN + 31) / 32 * 32, KS = CINP / 32;
   static constexpr int WES = CINP + 16;                 // staged expand row (halves): 2 mod 4 granules
   static constexpr int WPS = 48;                        // staged project row (halves, 32 used)
-  using SL = X2Slab<S, PINP>;
+  // XC: the depthwise waves own a channel group each for every pixel of the tile (wave-uniform weights from scalar
+  // loads) and hand the hi / lo depthwise outputs to the project through an exchange buffer, one chunk behind
+  static constexpr bool XC = SPEF_X2_XC && PST && WCO == 1 && S == 1 && P == 1;
+  using SL = X2Slab<S, PINP, XC>;
   static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
   static constexpr int NCL = NCH / P;                   // chunks of this workgroup's hidden part
   static constexpr int NCT = (COUT + 15) / 16, NPC = NCT * 16;
   static constexpr int POUT16 = TH * TW / 16;
+  static constexpr int POUT = TH * TW, PPX = POUT / 64;   // XC: output pixels per depthwise lane
+  static constexpr int CTW = (NCT + 3) / 4;               // XC: output-channel tiles per depthwise wave
+  static constexpr int XPL = POUT * 96 + 32;              // XC: one exchange plane (96-B pixel rows, 16-B skew)
   static constexpr int WP = ND / WCO, QPW = POUT16 / WP, NCTW = NCT / WCO;
   static constexpr int EPT = (PIN16 + NE - 1) / NE;     // expand pixel tiles per expand wave
   // LDS: slabs | expand stage [2] | depthwise stage [2] | project stage [2]
   static constexpr int SLAB_B = SL::FLOATS * 4;
   static constexpr int SE_B = 2 * 32 * WES * 2 + 32 * 4;   // hi / lo weight planes + expand bias
-  static constexpr int SD_B = (9 * 32 + 32) * 4;            // depthwise weights [9][32] + depthwise bias
-  static constexpr int SP_B = PST ? 2 * NPC * WPS * 2 : 0;
+  static constexpr int SD_B = XC ? 0 : (9 * 32 + 32) * 4;   // depthwise weights [9][32] + depthwise bias
+  static constexpr int SP_B = (PST && !XC) ? 2 * NPC * WPS * 2 : 0;
   // LDS-DMA staging (GL): every stage region a whole number of 1-KiB wave-instruction pieces (a piece writes 64 x 16 B
   // lane-linearly); per buffer the depthwise and project stages are one contiguous region. Interleaved A/B at B = 64:
   // blocks 14 and 15-16 -2 / -5 us per step, block 17 +3, blocks 8-13 no gain (same box, interleaved), so the
@@ -470,10 +481,11 @@ struct X2wGeom {
   static constexpr int OFF_SD = GL ? OFF_SE + 2 * SE_BQ : OFF_SE + 2 * SE_B;
   static constexpr int OFF_SP = GL ? OFF_SD + SD_BQ : OFF_SD + 2 * SD_B;
   static constexpr int OFF_TR = GL ? OFF_SD + 2 * DP_BQ : OFF_SP + 2 * SP_B;   // dummy rows: invalid pixels' stores
-  static constexpr int OFF_ST = OFF_TR + 16 * 24 * 4;     // SPEF_X2_STAMP: per-chunk clock stamps (timing builds)
+  static constexpr int OFF_XC = OFF_TR + 16 * 24 * 4;     // XC: exchange [buffer][hi | lo] planes
+  static constexpr int OFF_ST = OFF_XC + (XC ? 4 * XPL : 0);   // SPEF_X2_STAMP: per-chunk clock stamps
   static constexpr int LDS_BYTES = OFF_ST + (SPEF_X2_STAMP ? 8 * 4 * 64 : 0);
   // 16-B stage pieces per chunk
-  static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = 9 * 8 + 8, NPP = PST ? 2 * NPC * 4 : 0;
+  static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = XC ? 0 : 9 * 8 + 8, NPP = (PST && !XC) ? 2 * NPC * 4 : 0;
   static constexpr int NPIECE = (NPE + NPD + NPP + NE * 64 - 1) / (NE * 64);
   static_assert(CIN % 8 == 0 && COUT % 4 == 0 && HID % 8 == 0, "channel counts");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
@@ -838,6 +850,125 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       if (wave == 0) stamp(c, 1);
       __syncthreads();
     }
+    }
+  } else if constexpr (G::XC) {
+    // ================= depthwise / project waves, channel-split (XC)
+    // Depthwise: wave d owns channels 8d..8d+7 of each chunk for every output pixel (lane l: pixels l + 64 t); its 72
+    // fp32 weights are wave-uniform (scalar loads, no LDS); the ReLU'd sums go to the exchange buffer of the chunk's
+    // parity as hi / lo fp16 (pixel o at byte o * 96 + 16 ((o >> 4) & 1) + 16 d: conflict-free for these pixel-major
+    // stores and for the fragment reads below). Project: wave d takes output-channel tiles d, d + 4, ... of every pixel
+    // tile, one chunk behind the depthwise (its B fragments from the exchange buffer written before the last barrier,
+    // its A fragments from L2 one chunk ahead), so no barrier is added. Same operations per output as the pixel-split
+    // form (fp32 depthwise in kx / ky order, hi / lo split, three MFMAs per product), in the same order.
+    const int d = __builtin_amdgcn_readfirstlane(wave - G::NE);
+    int pin[G::PPX];
+#pragma unroll
+    for (int t = 0; t < G::PPX; ++t) {
+      const int o = lane + 64 * t;
+      pin[t] = (o / TW) * G::IW + (o % TW);
+    }
+    f32x4 acc[G::CTW][G::POUT16];
+#pragma unroll
+    for (int j = 0; j < G::CTW; ++j) {
+      float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (d + 4 * j < G::NCT) bb = *reinterpret_cast<const float4*>(bp + (d + 4 * j) * 16 + 4 * kg);
+#pragma unroll
+      for (int q = 0; q < G::POUT16; ++q) acc[j][q] = f32x4{bb.x, bb.y, bb.z, bb.w};
+    }
+    const _Float16* WpLo = Wp + (size_t)G::NPC * G::HIDP;
+    f16x8 pgh[G::CTW], pgl[G::CTW];
+    auto load_pg = [&](int k) {
+#pragma unroll
+      for (int j = 0; j < G::CTW; ++j)
+        if (d + 4 * j < G::NCT) {
+          const size_t off = (size_t)((d + 4 * j) * 16 + r16) * G::HIDP + 32 * (cb + k) + 8 * kg;
+          pgh[j] = *reinterpret_cast<const f16x8*>(Wp + off);
+          pgl[j] = *reinterpret_cast<const f16x8*>(WpLo + off);
+        }
+    };
+    char* Xc = smem + G::OFF_XC;   // [chunk parity][hi | lo] planes
+    auto xoff = [](int o) { return o * 96 + ((o >> 4) & 1) * 16; };
+    auto project = [&](int k) {
+      const char* Xh = Xc + (k & 1) * 2 * G::XPL;
+      const char* Xl = Xh + G::XPL;
+#pragma unroll
+      for (int q = 0; q < G::POUT16; ++q) {
+        const int o = 16 * q + r16;
+        const f16x8 bh = *reinterpret_cast<const f16x8*>(Xh + xoff(o) + 16 * kg);
+        const f16x8 bl = *reinterpret_cast<const f16x8*>(Xl + xoff(o) + 16 * kg);
+#pragma unroll
+        for (int j = 0; j < G::CTW; ++j)
+          if (d + 4 * j < G::NCT) acc[j][q] = mfma_x2(pgh[j], pgl[j], bh, bl, acc[j][q]);
+      }
+    };
+    load_pg(0);
+    __syncthreads();
+    __syncthreads();
+#pragma unroll 1
+    for (int c = 0; c < G::NCL; ++c) {
+      if (wave == G::NE) stamp(c, 4);
+      if (c >= 1) {
+        project(c - 1);   // chunk c - 1: its exchange buffer is complete (last barrier)
+        load_pg(c);       // chunk c's fragments, used after the next barrier
+      }
+      const float* Sl = slab(c & 1);
+      const float* wdc = Wd + 32 * (cb + c) + 8 * d;   // wave-uniform
+      f32x2 a[G::PPX][4];
+      {
+        const float* bdc = bd + 32 * (cb + c) + 8 * d;
+        const f32x2 b4[4] = {f32x2{bdc[0], bdc[1]}, f32x2{bdc[2], bdc[3]}, f32x2{bdc[4], bdc[5]}, f32x2{bdc[6], bdc[7]}};
+#pragma unroll
+        for (int t = 0; t < G::PPX; ++t)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) a[t][e] = b4[e];
+      }
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx)
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const float* wt = wdc + (ky * 3 + kx) * G::HIDP;
+          const f32x2 w4[4] = {f32x2{wt[0], wt[1]}, f32x2{wt[2], wt[3]}, f32x2{wt[4], wt[5]}, f32x2{wt[6], wt[7]}};
+#pragma unroll
+          for (int t = 0; t < G::PPX; ++t) {
+            const int p = pin[t] + ky * G::IW + kx;
+            dw_tap8(a[t], *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * d)),
+                    *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * d + 1)), w4);
+          }
+        }
+      {
+        char* Xh = Xc + (c & 1) * 2 * G::XPL;
+        char* Xl = Xh + G::XPL;
+#pragma unroll
+        for (int t = 0; t < G::PPX; ++t) {
+          f16x8 bh, bl;
+          relu_split8(a[t], bh, bl);
+          const int o = lane + 64 * t;
+          *reinterpret_cast<f16x8*>(Xh + xoff(o) + 16 * d) = bh;
+          *reinterpret_cast<f16x8*>(Xl + xoff(o) + 16 * d) = bl;
+        }
+      }
+      if (wave == G::NE) stamp(c, 6);
+      __syncthreads();
+    }
+    project(G::NCL - 1);
+    // epilogue: + residual (fp32 block input) -> fp32 NHWC
+#pragma unroll
+    for (int q = 0; q < G::POUT16; ++q) {
+      const int o = 16 * q + r16;
+      const int gy = oy0 + o / TW, gx = ox0 + o % TW;
+      if (gy >= OH || gx >= OW) continue;
+      const size_t pix = ((size_t)b * OH + gy) * OW + gx;
+#pragma unroll
+      for (int j = 0; j < G::CTW; ++j) {
+        const int co = (d + 4 * j) * 16 + 4 * kg;
+        if (d + 4 * j >= G::NCT || co >= COUT) continue;
+        f32x4 v = acc[j][q];
+        if constexpr (RES) {
+          const float4 r = *reinterpret_cast<const float4*>(X + pix * CIN + co);
+          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        }
+        *reinterpret_cast<float4*>(Y + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
+      }
     }
   } else {
     // ================= depthwise / project waves
