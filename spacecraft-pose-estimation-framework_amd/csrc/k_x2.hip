@@ -854,7 +854,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   } else if constexpr (G::XC) {
     // ================= depthwise / project waves, channel-split (XC)
     // Depthwise: wave d owns channels 8d..8d+7 of each chunk for every output pixel (lane l: pixels l + 64 t); its 72
-    // fp32 weights are wave-uniform (scalar loads, no LDS); the ReLU'd sums go to the exchange buffer of the chunk's
+    // fp32 weights are wave-uniform (loaded from L2 per chunk, no LDS stage); the ReLU'd sums go to the exchange buffer of the chunk's
     // parity as hi / lo fp16 (pixel o at byte o * 96 + 16 ((o >> 4) & 1) + 16 d: conflict-free for these pixel-major
     // stores and for the fragment reads below). Project: wave d takes output-channel tiles d, d + 4, ... of every pixel
     // tile, one chunk behind the depthwise (its B fragments from the exchange buffer written before the last barrier,
@@ -907,27 +907,36 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
 #pragma unroll 1
     for (int c = 0; c < G::NCL; ++c) {
       if (wave == G::NE) stamp(c, 4);
+      // this chunk's 72 weights + 8 biases as vector loads (a uniform address through the lane-varying wave index:
+      // scalar loads share lgkmcnt with the LDS reads, and their lgkmcnt(0) waits serialised the depthwise), issued
+      // before the lagged project so its MFMAs cover their latency
+      const int dv = wave - G::NE;
+      const float* wdc = Wd + 32 * (cb + c) + 8 * dv;
+      float4 wv[9][2];
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        wv[tap][0] = *reinterpret_cast<const float4*>(wdc + tap * G::HIDP);
+        wv[tap][1] = *reinterpret_cast<const float4*>(wdc + tap * G::HIDP + 4);
+      }
+      const float4 bv0 = *reinterpret_cast<const float4*>(bd + 32 * (cb + c) + 8 * dv);
+      const float4 bv1 = *reinterpret_cast<const float4*>(bd + 32 * (cb + c) + 8 * dv + 4);
       if (c >= 1) {
         project(c - 1);   // chunk c - 1: its exchange buffer is complete (last barrier)
         load_pg(c);       // chunk c's fragments, used after the next barrier
       }
       const float* Sl = slab(c & 1);
-      const float* wdc = Wd + 32 * (cb + c) + 8 * d;   // wave-uniform
       f32x2 a[G::PPX][4];
-      {
-        const float* bdc = bd + 32 * (cb + c) + 8 * d;
-        const f32x2 b4[4] = {f32x2{bdc[0], bdc[1]}, f32x2{bdc[2], bdc[3]}, f32x2{bdc[4], bdc[5]}, f32x2{bdc[6], bdc[7]}};
 #pragma unroll
-        for (int t = 0; t < G::PPX; ++t)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) a[t][e] = b4[e];
+      for (int t = 0; t < G::PPX; ++t) {
+        a[t][0] = f32x2{bv0.x, bv0.y}; a[t][1] = f32x2{bv0.z, bv0.w};
+        a[t][2] = f32x2{bv1.x, bv1.y}; a[t][3] = f32x2{bv1.z, bv1.w};
       }
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
-          const float* wt = wdc + (ky * 3 + kx) * G::HIDP;
-          const f32x2 w4[4] = {f32x2{wt[0], wt[1]}, f32x2{wt[2], wt[3]}, f32x2{wt[4], wt[5]}, f32x2{wt[6], wt[7]}};
+          const float4 w0 = wv[ky * 3 + kx][0], w1 = wv[ky * 3 + kx][1];
+          const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
 #pragma unroll
           for (int t = 0; t < G::PPX; ++t) {
             const int p = pin[t] + ky * G::IW + kx;
