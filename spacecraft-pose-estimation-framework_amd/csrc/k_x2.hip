@@ -113,8 +113,12 @@ __device__ __forceinline__ void st_act4(void* p, size_t i, f32x4 v, bool f16) {
 // stores conflict-free.
 // XC (channel-split depthwise, below): 20-float rows with the plane-1 base at granule 0 keep the expand's stores
 // conflict-free and its pixel-major reads at most 1.6-way (checked against the lane groups).
-template <int S, int PINP, bool XC = false>
+#ifndef SPEF_X2_XC_SSP24   // A/B aid: XC on the pixel-split form's 24-float rows
+#define SPEF_X2_XC_SSP24 0
+#endif
+template <int S, int PINP, bool XC_ = false>
 struct X2Slab {
+  static constexpr bool XC = XC_ && !SPEF_X2_XC_SSP24;
   static constexpr int SSP = (S == 2 || XC) ? 20 : 24;           // floats per pixel row of a plane
   static constexpr int TGT = (S == 2 || XC) ? 0 : 1;             // plane-1 base, granules mod 16
   static constexpr int PLANE = PINP * SSP + ((TGT - PINP * SSP / 4) % 16 + 16) % 16 * 4;
