@@ -498,9 +498,6 @@ struct X2wGeom {
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
-#ifndef SPEF_X2_PRE   // register-staged blocks: stage-piece addresses evaluated once per workgroup
-#define SPEF_X2_PRE 0   // measured: no gain (blocks 12-13 181 -> 180, 8-10 162 -> 167 us per step)
-#endif
 #ifndef SPEF_X2_ABL_STAGE
 #define SPEF_X2_ABL_STAGE 0
 #endif
@@ -508,14 +505,21 @@ struct X2wGeom {
 // project partial sums (no bias, no residual) to Y + part * pstride; x2_split_reduce_kernel adds the P parts in order,
 // the bias and the residual. Small maps get P times the workgroups while every workgroup streams only 1 / P of the
 // block's weights.
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1>
+// PT (persistent tiles): a workgroup runs tiles L, L + nwg, ... < ntile as ONE chunk stream (global chunk g = tile
+// t * NCL + chunk c): the expand waves fetch the next tile's input two chunks ahead and expand its chunk 0 while the
+// depthwise waves finish the current tile (residual fetched two chunks ahead, epilogue stores issued, accumulators
+// reset), so a second tile per CU costs no prologue, epilogue or dispatch gap. Invalid input pixels are stored as
+// zeros by every expand (a pixel valid in one tile may be padding in the next). NCL even: the stage / slab parity of
+// global chunk g is that of its chunk c.
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1, bool PT = false>
 __global__ __launch_bounds__(512) void x2_irw_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
-    uint32_t nwg, size_t pstride) {
+    uint32_t nwg, size_t pstride, uint32_t ntile) {
   using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST, P>;
   using SL = typename G::SL;
+  static_assert(!PT || (P == 1 && G::NCL % 2 == 0 && !G::XC), "persistent tiles: one hidden part, even chunk count");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
@@ -527,16 +531,27 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         reinterpret_cast<uint32_t*>(smem + G::OFF_ST)[c * 8 + slot] = (uint32_t)__builtin_amdgcn_s_memtime();
     }
   };
+  const uint32_t L0 = L;                           // first work item (PT: then L0 + nwg, ...)
+  const int nt = PT ? (int)((ntile - L0 + nwg - 1) / nwg) : 1;   // tiles of this workgroup
+  const int GT = nt * G::NCL;                      // chunks of this workgroup
   const int part = (int)(L % (uint32_t)P);        // hidden part (the parts of a tile share an XCD)
   L /= (uint32_t)P;
   const int cb = part * G::NCL;                    // first hidden chunk of this part
-  const int tx = (int)(L % (uint32_t)tiles_x);
-  L /= (uint32_t)tiles_x;
-  const int ty = (int)(L % (uint32_t)tiles_y);
-  const int b = (int)(L / (uint32_t)tiles_y);
-  const int oy0 = ty * TH, ox0 = tx * TW;
+  auto tile_of = [&](uint32_t Lt, int& b_, int& oy0_, int& ox0_) {   // tile (without the part) -> image, origin
+    const int tx_ = (int)(Lt % (uint32_t)tiles_x);
+    Lt /= (uint32_t)tiles_x;
+    b_ = (int)(Lt / (uint32_t)tiles_y);
+    oy0_ = (int)(Lt % (uint32_t)tiles_y) * TH;
+    ox0_ = tx_ * TW;
+  };
+  int b, oy0, ox0;
+  tile_of(L, b, oy0, ox0);
   const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+  // local chunk of global chunk g (G::NCL: none, past this workgroup's last tile)
+  auto kmod = [&](int g) { return PT ? (g < GT ? g % G::NCL : G::NCL) : g; };
   auto slab = [&](int i) { return reinterpret_cast<float*>(smem + i * G::SLAB_B); };
+  if (wave == 0) stamp(0, 3);                      // kernel entry (expand wave 0)
+  if (wave == G::NE) stamp(1, 7);                  // kernel entry (depthwise wave 4)
   auto se = [&](int i) { return smem + G::OFF_SE + i * G::SE_STR; };
   auto sd = [&](int i) { return reinterpret_cast<float*>(smem + G::OFF_SD + i * G::SD_STR); };
   auto sp = [&](int i) { return reinterpret_cast<_Float16*>(smem + G::OFF_SP + i * G::SP_STR); };
@@ -674,52 +689,71 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     // ================= expand waves
     const int e = wave;
     // this wave's input-tile pixel tiles pt = e + NE j: B fragments (hi / lo) for every K step, loaded and split once
+    // per tile. The fp32 rows are loaded into the fragments' own registers (8 floats of (j, ks) in the bits of
+    // bxh[j][ks] | bxl[j][ks]) and split in place: no second register set
     f16x8 bxh[G::EPT][G::KS], bxl[G::EPT][G::KS];
-    uint32_t pvmask = 0;
-    int soff[G::EPT];   // slab store offset (floats) of this lane's pixel, or the dummy rows
-    {
-      const float* Xb = X + (size_t)b * H * W * CIN;
-      float4 raw[G::EPT][G::KS][2];
+    uint32_t pvmask = 0;   // bit j: pixel tile j's pixel of this lane is inside the map
+    int soff[G::EPT];      // slab store offset (floats) of this lane's pixel, or the dummy rows
+    auto pix = [&](int j, int iy0_, int ix0_, int& iy, int& ix) {   // input pixel of pixel tile j: inside the map?
+      const int p = (e + G::NE * j) * 16 + r16;
+      if (p >= G::PIN) return false;
+      const int py = p / G::IW, px = p - py * G::IW;
+      iy = iy0_ + py;
+      ix = ix0_ + px;
+      return iy >= 0 && iy < H && ix >= 0 && ix < W;
+    };
+    auto load_raw = [&](int b_, int iy0_, int ix0_) {   // fp32 input rows of the tile (zero outside the map)
+      const float* Xb = X + (size_t)b_ * H * W * CIN;
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j) {
+        int iy = 0, ix = 0;
+        const bool ok = pix(j, iy0_, ix0_, iy, ix);
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const int ch = 32 * ks + 8 * kg;
+          float4 r0 = make_float4(0.f, 0.f, 0.f, 0.f), r1 = r0;
+          if (ok && ch < CIN) {
+            const float* src = Xb + ((size_t)iy * W + ix) * CIN + ch;
+            r0 = *reinterpret_cast<const float4*>(src);
+            r1 = *reinterpret_cast<const float4*>(src + 4);
+          }
+          bxh[j][ks] = __builtin_bit_cast(f16x8, r0);
+          bxl[j][ks] = __builtin_bit_cast(f16x8, r1);
+        }
+      }
+    };
+    auto split_raw = [&]() {
+#pragma unroll
+      for (int j = 0; j < G::EPT; ++j)
+#pragma unroll
+        for (int ks = 0; ks < G::KS; ++ks) {
+          const float4 a = __builtin_bit_cast(float4, bxh[j][ks]), c = __builtin_bit_cast(float4, bxl[j][ks]);
+          const float v8[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
+          split8(v8, bxh[j][ks], bxl[j][ks]);
+        }
+    };
+    auto set_mask = [&](int iy0_, int ix0_) {   // PT: slab slots for every pixel of the tile (invalid ones get zeros)
+      pvmask = 0;
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
         const int p = (e + G::NE * j) * 16 + r16;
-        bool ok = false;
-        int iy = 0, ix = 0;
-        if (p < G::PIN) {
-          const int py = p / G::IW, px = p - py * G::IW;
-          iy = iy0 + py;
-          ix = ix0 + px;
-          ok = iy >= 0 && iy < H && ix >= 0 && ix < W;
-        }
+        int iy, ix;
+        const bool ok = pix(j, iy0_, ix0_, iy, ix);
         if (ok) pvmask |= 1u << j;
-        soff[j] = ok ? SL::at(p, kg) : G::OFF_TR / 4 + r16 * 24 + 4 * kg;
-        if (!ok && p < G::PINP) {   // zero padding of the depthwise: both slabs, once
+        soff[j] = (PT ? p < G::PINP : ok) ? SL::at(p, kg) : G::OFF_TR / 4 + r16 * 24 + 4 * kg;
+        if (!PT && !ok && p < G::PINP) {   // zero padding of the depthwise: both slabs, once
 #pragma unroll
           for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
             for (int h = 0; h < 2; ++h)
               *reinterpret_cast<float4*>(slab(sb) + SL::at(p, kg) + 8 * h) = make_float4(0.f, 0.f, 0.f, 0.f);
         }
-#pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-          const int ch = 32 * ks + 8 * kg;
-          raw[j][ks][0] = raw[j][ks][1] = make_float4(0.f, 0.f, 0.f, 0.f);
-          if (ok && ch < CIN) {
-            const float* src = Xb + ((size_t)iy * W + ix) * CIN + ch;
-            raw[j][ks][0] = *reinterpret_cast<const float4*>(src);
-            raw[j][ks][1] = *reinterpret_cast<const float4*>(src + 4);
-          }
-        }
       }
-#pragma unroll
-      for (int j = 0; j < G::EPT; ++j)
-#pragma unroll
-        for (int ks = 0; ks < G::KS; ++ks) {
-          const float4 a = raw[j][ks][0], c = raw[j][ks][1];
-          const float v8[8] = {a.x, a.y, a.z, a.w, c.x, c.y, c.z, c.w};
-          split8(v8, bxh[j][ks], bxl[j][ks]);
-        }
-    }
+    };
+    load_raw(b, iy0, ix0);
+    set_mask(iy0, ix0);
+    split_raw();
+    if (wave == 0) stamp(1, 3);   // input fragments loaded and split
     // expand of chunk k into slab k & 1 (stage k & 1)
     auto expand = [&](int k) {
       const char* S0 = se(k & 1);
@@ -746,16 +780,45 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
           for (int h = 0; h < 2; ++h) acc[j][h] = mfma_x2(ah[h], al[h], bxh[j][ks], bxl[j][ks], acc[j][h]);
         }
       }
-      // valid pixels -> slab k & 1; invalid ones -> the dummy rows (slab offsets are relative to slab 0, the dummy
-      // rows' to the LDS base, which is slab 0)
+      // valid pixels -> slab k & 1; invalid ones -> the dummy rows (PT: zeros into their slab slots; slab offsets
+      // are relative to slab 0, the dummy rows' to the LDS base, which is slab 0)
       float* Sl = reinterpret_cast<float*>(smem) + ((k & 1) ? G::SLAB_B / 4 : 0);
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
-        float* dst = ((pvmask >> j) & 1u) ? Sl + soff[j] : reinterpret_cast<float*>(smem) + soff[j];
+        const bool pv = (pvmask >> j) & 1u;
+        const int p = (e + G::NE * j) * 16 + r16;
+        float* dst = (PT ? p < G::PINP : pv) ? Sl + soff[j] : reinterpret_cast<float*>(smem) + soff[j];
 #pragma unroll
-        for (int h = 0; h < 2; ++h)
-          *reinterpret_cast<float4*>(dst + 8 * h) = make_float4(fmaxf(acc[j][h][0], 0.f), fmaxf(acc[j][h][1], 0.f),
-                                                                fmaxf(acc[j][h][2], 0.f), fmaxf(acc[j][h][3], 0.f));
+        for (int h = 0; h < 2; ++h) {
+          float4 v = make_float4(fmaxf(acc[j][h][0], 0.f), fmaxf(acc[j][h][1], 0.f), fmaxf(acc[j][h][2], 0.f),
+                                 fmaxf(acc[j][h][3], 0.f));
+          if (PT && !pv) v = make_float4(0.f, 0.f, 0.f, 0.f);
+          *reinterpret_cast<float4*>(dst + 8 * h) = v;
+        }
+      }
+    };
+    // PT, around the expand of global chunk gn: after a tile's last expand its successor's rows are loaded into the
+    // (now dead) fragment registers, after that iteration's stage loads so the stage stores' vmcnt waits do not cover
+    // them; chunk 0 of the next tile splits them. (An L2 prefetch chunks earlier by LDS-DMA into the dummy rows made
+    // the compiler wait vmcnt(0) at every barrier, which serialises the register-staged weight loads.)
+    auto next_tile = [&](int gn) {   // before expand(gn)
+      if constexpr (PT) {
+        if (gn % G::NCL == 0) {
+          int b_, oy_, ox_;
+          tile_of(L0 + (uint32_t)(gn / G::NCL) * nwg, b_, oy_, ox_);
+          set_mask(oy_ * S - 1, ox_ * S - 1);
+          split_raw();
+        }
+      }
+    };
+    auto fetch_tile = [&](int gn) {   // after expand(gn)
+      if constexpr (PT) {
+        const int cn = gn % G::NCL, tn = gn / G::NCL + 1;
+        if (tn < nt && cn == G::NCL - 1) {
+          int b_, oy_, ox_;
+          tile_of(L0 + (uint32_t)tn * nwg, b_, oy_, ox_);
+          load_raw(b_, oy_ * S - 1, ox_ * S - 1);
+        }
       }
     };
     // Stage data is loaded one iteration before it is stored: the pieces of expand chunk c + 2 and depthwise /
@@ -766,57 +829,27 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     expand(0);
     __syncthreads();                 // slab 0 visible
 #pragma unroll 1
-    for (int c = 0; c < G::NCL; ++c) {
+    for (int c = 0; c < GT; ++c) {
       if (wave == 0) stamp(c, 0);
-      if (c + 2 < G::NCL) dma(c + 2);   // expand stage of chunk c + 2 into the buffer chunk c's expand released
-      if (c + 1 < G::NCL) expand(c + 1);
+      if (c + 2 < GT) dma(kmod(c + 2));   // expand stage of chunk c + 2 into the buffer chunk c's expand released
+      if (c + 1 < GT) {
+        next_tile(c + 1);
+        expand(kmod(c + 1));
+        fetch_tile(c + 1);
+      }
       if (wave == 0) stamp(c, 1);
       __syncthreads();                  // (waits for this wave's pieces: visible to every wave after the barrier)
     }
     } else {
     uint4 v[G::NPIECE];
-    // PRE (the staged-project blocks 8-13): each piece's address pair evaluated once -- source pointer advanced by its
-    // per-chunk stride, destination toggled between the two stage buffers -- instead of piece()'s integer divisions
-    // per piece and chunk (~40 VALU each, twice per chunk: the expand role's VALU exceeded its MFMA time)
-    constexpr bool PRE = SPEF_X2_PRE && PST;
-    constexpr int NPR = PRE ? G::NPIECE : 1;
-    const char* psrc[NPR];
-    int pstr[NPR], pdst[NPR], pxor[NPR];
-    uint32_t pkind = 0;   // bit i: piece i is a depthwise / project piece (chunk c + 1), else expand (chunk c + 2)
-    uint32_t pval = 0;    // bit i: piece i exists
-    if constexpr (PRE) {
-#pragma unroll
-      for (int i = 0; i < NPR; ++i) {
-        const int u = tid + G::NE * 64 * i;
-        const void *s0, *s1;
-        void *d0, *d1;
-        piece(u, 0, 0, s0, d0);
-        piece(u, 1, 1, s1, d1);
-        if (s0) pval |= 1u << i;
-        if (u >= G::NPE) pkind |= 1u << i;
-        psrc[i] = reinterpret_cast<const char*>(s0);
-        pstr[i] = s0 ? (int)(reinterpret_cast<const char*>(s1) - reinterpret_cast<const char*>(s0)) : 0;
-        pdst[i] = s0 ? (int)(reinterpret_cast<char*>(d0) - smem) : 0;
-        pxor[i] = s0 ? (int)(reinterpret_cast<char*>(d0) - smem) ^ (int)(reinterpret_cast<char*>(d1) - smem) : 0;
-        // chunk of the first load_stage(0): expand c + 2 = 2, depthwise / project c + 1 = 1 (buffers 0 / 1)
-        const int k0 = (u >= G::NPE) ? 1 : 2;
-        psrc[i] += (size_t)k0 * pstr[i];
-        if (k0 & 1) pdst[i] ^= pxor[i];
-      }
-    }
     auto load_stage = [&](int c) {
 #if SPEF_X2_ABL_STAGE < 2   // timing ablation only (wrong results): 2 = no stage loads
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
-        if constexpr (PRE) {
-          const int k = ((pkind >> i) & 1u) ? c + 1 : c + 2;
-          v[i] = ((pval >> i) & 1u) && k < G::NCL ? *reinterpret_cast<const uint4*>(psrc[i]) : make_uint4(0, 0, 0, 0);
-        } else {
-          const void* src;
-          void* dst;
-          piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
-          v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
-        }
+        const void* src;
+        void* dst;
+        piece(tid + G::NE * 64 * i, kmod(c + 2), kmod(c + 1), src, dst);
+        v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
       }
 #endif
     };
@@ -824,17 +857,10 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
 #if SPEF_X2_ABL_STAGE < 1   // timing ablation only (wrong results): 1 = no stage stores
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
-        if constexpr (PRE) {
-          const int k = ((pkind >> i) & 1u) ? c + 1 : c + 2;
-          if (((pval >> i) & 1u) && k < G::NCL) *reinterpret_cast<uint4*>(smem + pdst[i]) = v[i];
-          psrc[i] += pstr[i];      // next chunk's source and buffer
-          pdst[i] ^= pxor[i];
-        } else {
-          const void* src;
-          void* dst;
-          piece(tid + G::NE * 64 * i, c + 2, c + 1, src, dst);
-          if (src) *reinterpret_cast<uint4*>(dst) = v[i];
-        }
+        const void* src;
+        void* dst;
+        piece(tid + G::NE * 64 * i, kmod(c + 2), kmod(c + 1), src, dst);
+        if (src) *reinterpret_cast<uint4*>(dst) = v[i];
       }
 #endif
     };
@@ -843,13 +869,15 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     expand(0);
     __syncthreads();                 // slab 0 visible
 #pragma unroll 1
-    for (int c = 0; c < G::NCL; ++c) {
+    for (int c = 0; c < GT; ++c) {
       if (wave == 0) stamp(c, 0);
       store_stage(c);                // expand chunk c + 2, depthwise / project chunk c + 1
       if (wave == 0) stamp(c, 2);
-      if (c + 1 < G::NCL) {
+      if (c + 1 < GT) {
         load_stage(c + 1);
-        expand(c + 1);
+        next_tile(c + 1);
+        expand(kmod(c + 1));
+        fetch_tile(c + 1);
       }
       if (wave == 0) stamp(c, 1);
       __syncthreads();
@@ -988,13 +1016,16 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
     const int d = wave - G::NE;
     const int wp = d % G::WP, wc = d / G::WP;
     f32x4 acc[G::QPW][G::NCTW];
+    auto init_acc = [&]() {
 #pragma unroll
-    for (int t = 0; t < G::NCTW; ++t) {   // (P > 1: the bias is added once, by the reduce)
-      const float4 bb = P == 1 ? *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int t = 0; t < G::NCTW; ++t) {   // (P > 1: the bias is added once, by the reduce)
+        const float4 bb = P == 1 ? *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg)
+                                 : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-      for (int q = 0; q < G::QPW; ++q) acc[q][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
-    }
+        for (int q = 0; q < G::QPW; ++q) acc[q][t] = f32x4{bb.x, bb.y, bb.z, bb.w};
+      }
+    };
+    init_acc();
     int pbase[G::QPW];
 #pragma unroll
     for (int q = 0; q < G::QPW; ++q) {
@@ -1014,14 +1045,63 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         }
       }
     };
+    // epilogue of the tile at (b_, oy0_, ox0_): + residual (the block input, pytorch_layers.py:93-96, added after the
+    // BN bias; PT: fetched two chunks earlier into rres) -> fp32 NHWC
+    constexpr int NRES = (PT && RES) ? G::QPW * G::NCTW : 1;
+    float4 rres[NRES];
+    auto out_pix = [&](int q, int b_, int oy0_, int ox0_, size_t& pix_) {
+      const int o = (wp * G::QPW + q) * 16 + r16;
+      const int oy = o / TW, ox = o - (o / TW) * TW;
+      const int gy = oy0_ + oy, gx = ox0_ + ox;
+      pix_ = ((size_t)b_ * OH + gy) * OW + gx;
+      return gy < OH && gx < OW;
+    };
+    auto fetch_res = [&](int b_, int oy0_, int ox0_) {
+      if constexpr (PT && RES) {
+#pragma unroll
+        for (int q = 0; q < G::QPW; ++q) {
+          size_t pix_;
+          const bool in = out_pix(q, b_, oy0_, ox0_, pix_);
+#pragma unroll
+          for (int t = 0; t < G::NCTW; ++t) {
+            const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
+            rres[q * G::NCTW + t] = in && co < COUT ? *reinterpret_cast<const float4*>(X + pix_ * CIN + co)
+                                                    : make_float4(0.f, 0.f, 0.f, 0.f);
+          }
+        }
+      }
+    };
+    auto epilogue = [&](int b_, int oy0_, int ox0_) {
+#pragma unroll
+      for (int q = 0; q < G::QPW; ++q) {
+        size_t pix;
+        if (!out_pix(q, b_, oy0_, ox0_, pix)) continue;
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) {
+          const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
+          if (co >= COUT) continue;
+          f32x4 v = acc[q][t];
+          if constexpr (P > 1) {   // partial sum of this hidden part
+            *reinterpret_cast<float4*>(Y + part * pstride + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
+            continue;
+          }
+          if constexpr (RES) {
+            const float4 r = PT ? rres[q * G::NCTW + t] : *reinterpret_cast<const float4*>(X + pix * CIN + co);
+            v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+          }
+          *reinterpret_cast<float4*>(Y + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+      }
+    };
     load_pg(0);
     __syncthreads();
     __syncthreads();
 #pragma unroll 1
-    for (int c = 0; c < G::NCL; ++c) {
-      if (wave == G::NE) stamp(c, 4);
+    for (int g = 0; g < GT; ++g) {
+      const int c = kmod(g);
+      if (wave == G::NE) stamp(g, 4);
       if constexpr (G::GL)
-        if (c + 1 < G::NCL) dma(c + 1);   // depthwise + project stage of chunk c + 1 (buffer released by chunk c - 1)
+        if (g + 1 < GT) dma(kmod(g + 1));   // depthwise + project stage of chunk g + 1 (buffer released by g - 1)
       const float* Sl = slab(c & 1);
       const float* D = sd(c & 1);
       f32x2 a[G::QPW][4];
@@ -1051,7 +1131,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
       f16x8 bh[G::QPW], bl[G::QPW];
 #pragma unroll
       for (int q = 0; q < G::QPW; ++q) relu_split8(a[q], bh[q], bl[q]);
-      if (wave == G::NE) stamp(c, 5);
+      if (wave == G::NE) stamp(g, 5);
       if constexpr (PST) {
         const _Float16* Ps = sp(c & 1);
 #pragma unroll
@@ -1067,35 +1147,23 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         for (int t = 0; t < G::NCTW; ++t)
 #pragma unroll
           for (int q = 0; q < G::QPW; ++q) acc[q][t] = mfma_x2(pgh[t], pgl[t], bh[q], bl[q], acc[q][t]);
-        if (c + 1 < G::NCL) load_pg(c + 1);   // next chunk's fragments: in flight across the barrier and its depthwise
+        if (g + 1 < GT) load_pg(kmod(g + 1));   // next chunk's fragments: in flight across the barrier and its depthwise
       }
-      if (wave == G::NE) stamp(c, 6);
+      if constexpr (PT) {
+        const int t = g / G::NCL;
+        int b_, oy_, ox_;
+        tile_of(L0 + (uint32_t)t * nwg, b_, oy_, ox_);
+        if (c == G::NCL - 2) fetch_res(b_, oy_, ox_);
+        if (c == G::NCL - 1) {
+          epilogue(b_, oy_, ox_);
+          init_acc();
+        }
+      }
+      if (wave == G::NE) stamp(g, 6);
       __syncthreads();
     }
-    // epilogue: + residual (fp32 block input) -> fp32 NHWC
-#pragma unroll
-    for (int q = 0; q < G::QPW; ++q) {
-      const int o = (wp * G::QPW + q) * 16 + r16;
-      const int oy = o / TW, ox = o - (o / TW) * TW;
-      const int gy = oy0 + oy, gx = ox0 + ox;
-      if (gy >= OH || gx >= OW) continue;
-      const size_t pix = ((size_t)b * OH + gy) * OW + gx;
-#pragma unroll
-      for (int t = 0; t < G::NCTW; ++t) {
-        const int co = (wc * G::NCTW + t) * 16 + 4 * kg;
-        if (co >= COUT) continue;
-        f32x4 v = acc[q][t];
-        if constexpr (P > 1) {   // partial sum of this hidden part
-          *reinterpret_cast<float4*>(Y + part * pstride + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
-          continue;
-        }
-        if constexpr (RES) {
-          const float4 r = *reinterpret_cast<const float4*>(X + pix * CIN + co);
-          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
-        }
-        *reinterpret_cast<float4*>(Y + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
-      }
-    }
+    if constexpr (!PT) epilogue(b, oy0, ox0);
+    if (wave == G::NE) stamp(0, 7);   // epilogue stores issued
   }
   if constexpr (SPEF_X2_STAMP) {   // every wave: the last barrier, then the stamps over the start of tile 0's output
     __syncthreads();
@@ -1144,6 +1212,12 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
 #ifndef SPEF_X2_MID8
 #define SPEF_X2_MID8 0
 #endif
+// Kind 3 = kind 1 with persistent tiles (x2_irw_kernel's PT: a second tile per CU streams on without a prologue):
+// the maps with more tiles than CUs at 512^2 (blocks 8-14: 512 tiles at B = 64).
+#ifndef SPEF_X2_PERSIST
+#define SPEF_X2_PERSIST 1
+#endif
+#define SPEF_X2_PK (SPEF_X2_PERSIST ? 3 : 1)
 #if SPEF_X2_MID8
 #define SPEF_X2_MID(X)                                           \
   X(64, 384, 64, 1, true, true, 8, 8, 8, 1, 2)      /* 8-10 */   \
@@ -1151,9 +1225,9 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(96, 576, 96, 1, true, true, 8, 8, 8, 1, 2)      /* 12-13 */
 #else
 #define SPEF_X2_MID(X)                                           \
-  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, 1)     /* 8-10 */   \
-  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, 1)    /* 11 */     \
-  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, 1)     /* 12-13 */
+  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK)     /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, SPEF_X2_PK)    /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK)     /* 12-13 */
 #endif
 #define SPEF_X2_TABLE(X)                                         \
   X(32, 32, 16, 1, false, false, 8, 16, 4, 1, 0)    /* 1 */      \
@@ -1163,7 +1237,7 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(32, 192, 32, 1, true, true, 8, 16, 4, 1, 0)     /* 5-6 */    \
   X(32, 192, 64, 2, true, false, 8, 8, 4, 1, 0)     /* 7 */      \
   SPEF_X2_MID(X)                                                 \
-  X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 1)    /* 14 */     \
+  X(96, 576, 160, 2, true, false, 4, 8, 8, 2, SPEF_X2_PK)    /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
 // 16x16 tiles with 8 waves (2 workgroups per CU) where they tile the map exactly: block 3 at 512^2 (interleaved A/B,
@@ -1192,7 +1266,7 @@ template <int CIN, int HID, int COUT, int S, bool EXPAND, bool RES, int TH, int 
           int P = 1, int IO = 0>
 static hipError_t x2_irb_go(const void* x, const void* we, const float* be, const float* wd, const float* bd,
                             const void* wp, const float* bp, void* y, int B, int H, int W, int OH, int OW,
-                            hipStream_t s, float* scratch = nullptr) {
+                            hipStream_t s, float* scratch = nullptr, int num_cu = 256) {
   if constexpr (KIND != 0 && IO != 0) {
     return hipErrorNotSupported;   // fp16 block I/O: the slab kernels (the fp16mx schedule's blocks 1-7) only
   }
@@ -1213,8 +1287,9 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
                                         tiles_x, tiles_y, nwg);
   } else if constexpr (IO == 0) {
     static_assert(EXPAND && NW == 8, "role-split blocks expand, 4 + 4 waves");
-    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND == 1, P>;
-    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND == 1, P>;
+    constexpr bool PT = KIND == 3 && P == 1;   // persistent tiles (kind 3): ceil(tiles / CUs) tiles per workgroup
+    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND != 2, P>;
+    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND != 2, P, PT>;
     if (!attr_set.done()) {
       hipError_t e = x2_set_lds(k, G::LDS_BYTES);
       if (e != hipSuccess) return e;
@@ -1222,8 +1297,13 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
     }
     const size_t pstride = (size_t)B * OH * OW * COUT;   // floats per hidden part (16-B multiple: COUT % 4 == 0)
     if (P > 1 && !scratch) return hipErrorInvalidValue;
-    k<<<nwg, 512, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
-                                    P > 1 ? scratch : (float*)y, H, W, OH, OW, tiles_x, tiles_y, nwg, pstride);
+    uint32_t grid = nwg;
+    if constexpr (PT) {
+      const uint32_t per = (nwg + (uint32_t)num_cu - 1) / (uint32_t)num_cu;
+      grid = (nwg + per - 1) / per;
+    }
+    k<<<grid, 512, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
+                                     P > 1 ? scratch : (float*)y, H, W, OH, OW, tiles_x, tiles_y, grid, pstride, nwg);
     if constexpr (P > 1) {
       const size_t n4 = pstride / 4;
       x2_split_reduce_kernel<P, RES><<<(unsigned)((n4 + 255) / 256), 256, 0, s>>>(scratch, pstride, bp,
@@ -1257,7 +1337,8 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
 #define SPEF_X2_IO_SWITCH(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                    \
   switch (io) {                                                                                               \
     case 0: return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, 1, 0>(x, we, be, wd, bd, wp, bp, y, \
-                                                                               B, H, W, OH, OW, s);           \
+                                                                               B, H, W, OH, OW, s, nullptr,   \
+                                                                               num_cu);                       \
     case 1: return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, 1, 1>(x, we, be, wd, bd, wp, bp, y, \
                                                                                B, H, W, OH, OW, s);           \
     case 2: return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, 1, 2>(x, we, be, wd, bd, wp, bp, y, \
@@ -1270,7 +1351,7 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && scratch && !io &&  \
       (SPEF_X2_SMALL_ALWAYS || (SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)))     \
     return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
-                                                                         OW, s, scratch);
+                                                                         OW, s, scratch, num_cu);
   SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
 #undef SPEF_X2_SMALL
 #ifndef SPEF_X2_EXACT_ON   // A/B aid: 0 = the primary 8 x 16 tiles on exact maps too

@@ -2,7 +2,9 @@
 stamp -DSPEF_X2_STAMP=1). The kernel's tile-0 workgroup records s_memtime (shader cycles) per hidden chunk in LDS and
 writes them over its output; Engine.probe returns that output. Slots per chunk: expand wave 0 -- 0 loop start,
 2 after the stage stores (register staging only), 1 before the barrier; depthwise wave 4 -- 4 loop start, 5 after the
-depthwise (before the project MFMAs), 6 before the barrier. Outputs are wrong by construction."""
+depthwise (before the project MFMAs), 6 before the barrier; slot 3 of chunks 0 / 1: expand wave 0 at kernel entry /
+after the input fragments; slot 7 of chunks 1 / 0: depthwise wave 4 at kernel entry / after the epilogue stores.
+Outputs are wrong by construction."""
 import os
 import sys
 
@@ -34,6 +36,9 @@ for op, nch in ((8, 12), (12, 18), (15, 30), (17, 30)):
     print(f'block {op}: {nch} chunks, total {st[-1, 1] - t0} cycles; per chunk (median): period {int(np.median(per))}, '
           f'expand start->barrier {int(np.median(e_busy))}, stage stores {int(np.median(st[:, 2] - st[:, 0])) if st[0, 2] else "-"}, '
           f'dw start->depthwise done {int(np.median(d_dw))}, dw start->barrier {int(np.median(d_busy))}')
+    e0 = st[0, 3]
+    print(f'   entry->fragments {st[1, 3] - e0}, entry->loop start {t0 - e0}, last prebar->epilogue done '
+          f'{st[0, 7] - st[-1, 6]}, entry->end {st[0, 7] - e0} cycles (dw entry {st[1, 7] - e0:+d})')
     print('   first chunks (expand start, prebar | dw start, mid, prebar) rel. to t0:')
     for c in range(min(4, nch)):
         print('   ', c, st[c, 0] - t0, st[c, 1] - t0, '|', st[c, 4] - t0, st[c, 5] - t0, st[c, 6] - t0)
