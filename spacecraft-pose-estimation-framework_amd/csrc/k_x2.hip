@@ -445,6 +445,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
 #ifndef SPEF_X2_GLDS   // stage the role-split kernels' chunk weights by LDS-DMA (global_load_lds) instead of registers
 #define SPEF_X2_GLDS 1
 #endif
+#ifndef SPEF_X2_GLDS_S2   // ... on block 14 (stride 2) too
+#define SPEF_X2_GLDS_S2 1
+#endif
 template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST, int P = 1>
 struct X2wGeom {
   static constexpr int NE = 4, ND = 4, NW = NE + ND;
@@ -475,7 +478,7 @@ struct X2wGeom {
   // lane-linearly); per buffer the depthwise and project stages are one contiguous region. Interleaved A/B at B = 64:
   // blocks 14 and 15-16 -2 / -5 us per step, block 17 +3, blocks 8-13 no gain (same box, interleaved), so the
   // cout = 160 blocks only.
-  static constexpr bool GL = SPEF_X2_GLDS && COUT == 160;
+  static constexpr bool GL = SPEF_X2_GLDS && COUT == 160 && (S == 1 || SPEF_X2_GLDS_S2);
   static constexpr int SE_BQ = (SE_B + 1023) / 1024 * 1024, SD_BQ = (SD_B + 1023) / 1024 * 1024;
   static constexpr int SP_BQ = (SP_B + 1023) / 1024 * 1024, DP_BQ = SD_BQ + SP_BQ;
   static constexpr int NIE = SE_BQ / 1024, NID = DP_BQ / 1024;                  // pieces per chunk stage
@@ -512,7 +515,21 @@ struct X2wGeom {
 // zeros by every expand (a pixel valid in one tile may be padding in the next). NCL even: the stage / slab parity of
 // global chunk g is that of its chunk c.
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1, bool PT = false>
-__global__ __launch_bounds__(512) void x2_irw_kernel(
+// Interleaved A/B at B = 64 (bit-identical): the occupancy target alone blocks 15-16 140 -> 139 us per step; with
+// column batches one column ahead 140 -> 133, block 14 69 -> 66, blocks 8-13 unchanged (their expand role bounds the
+// chunk period); 53.2k -> 53.5k img/s.
+#ifndef SPEF_X2_DWB   // role-split depthwise: 0 = tap by tap, 1 = column batches, 2 = column batches one column ahead
+#define SPEF_X2_DWB 2
+#endif
+#ifndef SPEF_X2W_WPE   // occupancy target of the role-split kernels (one 8-wave workgroup per CU: 2 waves per SIMD)
+#define SPEF_X2W_WPE 2
+#endif
+#if SPEF_X2W_WPE
+#define SPEF_X2W_ATTR __attribute__((amdgpu_waves_per_eu(SPEF_X2W_WPE, SPEF_X2W_WPE)))
+#else
+#define SPEF_X2W_ATTR
+#endif
+__global__ __launch_bounds__(512) SPEF_X2W_ATTR void x2_irw_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
@@ -1114,6 +1131,45 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
           a[q][2] = f32x2{d1.x, d1.y}; a[q][3] = f32x2{d1.z, d1.w};
         }
       }
+      // (block 17, !PST: no registers to spare for the batches; DWB 2 only where a wave owns one pixel tile)
+      constexpr int DWB = !PST ? 0 : (SPEF_X2_DWB == 2 && G::QPW > 1) ? 1 : SPEF_X2_DWB;
+      if constexpr (DWB > 0) {
+      // column batches: the 3 taps' weights and slab rows of column kx issued together (sched_barrier keeps them
+      // ahead of the FMAs), DWB 2: column kx + 1's batch issued before column kx's FMAs. Same FMA order.
+      float4 wv[DWB][3][2], sv[DWB][3][G::QPW][2];
+      auto col = [&](int kx, int bf) {
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const float* wt = D + (ky * 3 + kx) * 32 + 8 * kg;
+          wv[bf][ky][0] = *reinterpret_cast<const float4*>(wt);
+          wv[bf][ky][1] = *reinterpret_cast<const float4*>(wt + 4);
+#pragma unroll
+          for (int q = 0; q < G::QPW; ++q) {
+            const int p = pbase[q] + ky * G::IW + kx;
+            sv[bf][ky][q][0] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
+            sv[bf][ky][q][1] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
+          }
+        }
+      };
+      col(0, 0);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        const int bf = DWB == 2 ? (kx & 1) : 0;
+        if (DWB == 2 && kx < 2) col(kx + 1, bf ^ 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const float4 w0 = wv[bf][ky][0], w1 = wv[bf][ky][1];
+          const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
+#pragma unroll
+          for (int q = 0; q < G::QPW; ++q) dw_tap8(a[q], sv[bf][ky][q][0], sv[bf][ky][q][1], w4);
+        }
+        if (DWB == 1 && kx < 2) {
+          __builtin_amdgcn_sched_barrier(0);
+          col(kx + 1, 0);
+        }
+      }
+      } else {
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
@@ -1128,6 +1184,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
                     *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1)), w4);
           }
         }
+      }
       f16x8 bh[G::QPW], bl[G::QPW];
 #pragma unroll
       for (int q = 0; q < G::QPW; ++q) relu_split8(a[q], bh[q], bl[q]);
@@ -1150,13 +1207,15 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
         if (g + 1 < GT) load_pg(kmod(g + 1));   // next chunk's fragments: in flight across the barrier and its depthwise
       }
       if constexpr (PT) {
-        const int t = g / G::NCL;
-        int b_, oy_, ox_;
-        tile_of(L0 + (uint32_t)t * nwg, b_, oy_, ox_);
-        if (c == G::NCL - 2) fetch_res(b_, oy_, ox_);
-        if (c == G::NCL - 1) {
-          epilogue(b_, oy_, ox_);
-          init_acc();
+        if (c >= G::NCL - 2) {
+          int b_, oy_, ox_;
+          tile_of(L0 + (uint32_t)(g / G::NCL) * nwg, b_, oy_, ox_);
+          if (c == G::NCL - 2) {
+            fetch_res(b_, oy_, ox_);
+          } else {
+            epilogue(b_, oy_, ox_);
+            init_acc();
+          }
         }
       }
       if (wave == G::NE) stamp(g, 6);
@@ -1168,7 +1227,7 @@ __global__ __launch_bounds__(512) void x2_irw_kernel(
   if constexpr (SPEF_X2_STAMP) {   // every wave: the last barrier, then the stamps over the start of tile 0's output
     __syncthreads();
     if (stamp_wg && tid < 8 * 64) {
-      const int n = 8 * (G::NCL < 64 ? G::NCL : 64);
+      const int n = 8 * (GT < 64 ? GT : 64);
       if (tid < n) reinterpret_cast<uint32_t*>(Y)[tid] = reinterpret_cast<const uint32_t*>(smem + G::OFF_ST)[tid];
     }
   }

@@ -23,7 +23,9 @@ fr = torch.from_numpy(np.random.Generator(np.random.PCG64(0)).integers(0, 256, (
 for _ in range(3):
     eng.forward(fr)
 torch.cuda.synchronize()
-for op, nch in ((8, 12), (12, 18), (15, 30), (17, 30)):
+PT = int(os.environ.get('KSTAMP_TILES', '2'))   # tiles per workgroup of the persistent blocks (8-14) at B = 64
+for op, nch1 in ((8, 12), (12, 18), (15, 30), (17, 30)):
+    nch = nch1 * (PT if op < 15 else 1)
     eng.probe(fr, op)
     y = eng.probe(fr, op)
     torch.cuda.synchronize()
@@ -39,6 +41,6 @@ for op, nch in ((8, 12), (12, 18), (15, 30), (17, 30)):
     e0 = st[0, 3]
     print(f'   entry->fragments {st[1, 3] - e0}, entry->loop start {t0 - e0}, last prebar->epilogue done '
           f'{st[0, 7] - st[-1, 6]}, entry->end {st[0, 7] - e0} cycles (dw entry {st[1, 7] - e0:+d})')
-    print('   first chunks (expand start, prebar | dw start, mid, prebar) rel. to t0:')
-    for c in range(min(4, nch)):
+    print('   chunks (expand start, prebar | dw start, mid, prebar) rel. to t0:')
+    for c in list(range(min(3, nch))) + (list(range(nch1 - 2, nch1 + 3)) if nch > nch1 else []):
         print('   ', c, st[c, 0] - t0, st[c, 1] - t0, '|', st[c, 4] - t0, st[c, 5] - t0, st[c, 6] - t0)
