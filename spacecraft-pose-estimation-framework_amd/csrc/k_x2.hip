@@ -521,6 +521,9 @@ template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, 
 #ifndef SPEF_X2_DWB   // role-split depthwise: 0 = tap by tap, 1 = column batches, 2 = column batches one column ahead
 #define SPEF_X2_DWB 2
 #endif
+#ifndef SPEF_X2_DWB2_CIN   // DWB 2 on two-pixel-tile waves up to this block input width (blocks 12-13 spill at 96;
+#define SPEF_X2_DWB2_CIN 0   // at 64, blocks 8-10 measured 143.6 -> 145.4 us per step: off)
+#endif
 #ifndef SPEF_X2W_WPE   // occupancy target of the role-split kernels (one 8-wave workgroup per CU: 2 waves per SIMD)
 #define SPEF_X2W_WPE 2
 #endif
@@ -1132,7 +1135,7 @@ __global__ __launch_bounds__(512) SPEF_X2W_ATTR void x2_irw_kernel(
         }
       }
       // (block 17, !PST: no registers to spare for the batches; DWB 2 only where a wave owns one pixel tile)
-      constexpr int DWB = !PST ? 0 : (SPEF_X2_DWB == 2 && G::QPW > 1) ? 1 : SPEF_X2_DWB;
+      constexpr int DWB = !PST ? 0 : (SPEF_X2_DWB == 2 && G::QPW > 1 && CIN > SPEF_X2_DWB2_CIN) ? 1 : SPEF_X2_DWB;
       if constexpr (DWB > 0) {
       // column batches: the 3 taps' weights and slab rows of column kx issued together (sched_barrier keeps them
       // ahead of the FMAs), DWB 2: column kx + 1's batch issued before column kx's FMAs. Same FMA order.
