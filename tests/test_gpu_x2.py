@@ -146,3 +146,40 @@ def test_keypoint_head_vs_reference_fixture(golden):
         assert np.abs(raw.cpu().numpy() - ref.numpy()).max() < X2_GOLDEN_TOL
     finally:
         e.close()
+
+
+def _oracle_block(x, sd, op):
+    """Block ``op`` (features.features[op], 1-17) of the oracle on its own input (NCHW fp32)."""
+    fp, cin, idx = 'features.features', 32, 1
+    for t, c, n, s in M._IR:
+        for i in range(n):
+            if idx == op:
+                stride, hidden, j = (s if i == 0 else 1), int(round(cin * t)), 0
+                y = x
+                if t != 1:
+                    y = M._conv_bn_act(y, sd, f'{fp}.{idx}.conv.{j}', 1, 1, True)
+                    j += 1
+                y = M._conv_bn_act(y, sd, f'{fp}.{idx}.conv.{j}', stride, hidden, True)
+                y = M._conv_bn_act(y, sd, f'{fp}.{idx}.conv.{j + 1}', 1, 1, False)
+                return x + y if (stride == 1 and cin == c) else y
+            cin, idx = c, idx + 1
+    raise ValueError(op)
+
+
+@pytest.mark.parametrize('b,h,w', [(33, 512, 512), (257, 100, 136)])
+def test_persistent_tile_blocks_vs_oracle(x2, sd, b, h, w):
+    """Blocks 8-14 with more tiles than CUs run persistent workgroups (x2_irw_kernel PT: ceil(tiles / CUs) tiles per
+    workgroup as one chunk stream). 33 frames at 512^2: 264 tiles of blocks 8-13, two per workgroup; 257 frames at
+    100 x 136: one 7 x 9 tile per frame, 129 workgroups, the last with a single tile (uneven split). Each block's
+    output against the oracle's block applied to the GPU's own input of that block, relative to the map's max."""
+    fr = _frames(b, h, w, 3 + b)
+    xg = torch.from_numpy(fr).cuda()
+    torch.set_num_threads(16)
+    prev = x2.probe(xg, 7).cpu()
+    for op in range(8, 15):
+        got = x2.probe(xg, op).cpu()
+        ref = _oracle_block(prev.permute(0, 3, 1, 2).contiguous(), sd, op).permute(0, 2, 3, 1).numpy()
+        assert got.shape == ref.shape, (op, got.shape, ref.shape)
+        err = np.abs(got.numpy() - ref).max() / max(1e-6, np.abs(ref).max())
+        assert err < 2e-5, (op, err)
+        prev = got
