@@ -448,9 +448,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
 #ifndef SPEF_X2_GLDS_S2   // ... on block 14 (stride 2) too
 #define SPEF_X2_GLDS_S2 1
 #endif
-template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST, int P = 1>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST, int P = 1, int ND_ = 4>
 struct X2wGeom {
-  static constexpr int NE = 4, ND = 4, NW = NE + ND;
+  static constexpr int NE = 4, ND = ND_, NW = NE + ND;
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
   static constexpr int CINP = (CIN + 31) / 32 * 32, KS = CINP / 32;
@@ -458,7 +458,7 @@ struct X2wGeom {
   static constexpr int WPS = 48;                        // staged project row (halves, 32 used)
   // XC: the depthwise waves own a channel group each for every pixel of the tile (wave-uniform weights from scalar
   // loads) and hand the hi / lo depthwise outputs to the project through an exchange buffer, one chunk behind
-  static constexpr bool XC = SPEF_X2_XC && PST && WCO == 1 && S == 1 && P == 1;
+  static constexpr bool XC = SPEF_X2_XC && PST && WCO == 1 && S == 1 && P == 1 && ND == 4;
   using SL = X2Slab<S, PINP, XC>;
   static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
   static constexpr int NCL = NCH / P;                   // chunks of this workgroup's hidden part
@@ -514,12 +514,17 @@ struct X2wGeom {
 // reset), so a second tile per CU costs no prologue, epilogue or dispatch gap. Invalid input pixels are stored as
 // zeros by every expand (a pixel valid in one tile may be padding in the next). NCL even: the stage / slab parity of
 // global chunk g is that of its chunk c.
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1, bool PT = false>
+// ND_ = 8 (kind 4): eight depthwise / project waves, one pixel tile each (three waves per SIMD).
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1, bool PT = false,
+          int ND_ = 4>
 // Interleaved A/B at B = 64 (bit-identical): the occupancy target alone blocks 15-16 140 -> 139 us per step; with
 // column batches one column ahead 140 -> 133, block 14 69 -> 66, blocks 8-13 unchanged (their expand role bounds the
 // chunk period); 53.2k -> 53.5k img/s.
 #ifndef SPEF_X2_DWB   // role-split depthwise: 0 = tap by tap, 1 = column batches, 2 = column batches one column ahead
 #define SPEF_X2_DWB 2
+#endif
+#ifndef SPEF_X2_ROWS   // column batches share input rows between a wave's vertically adjacent pixel tiles
+#define SPEF_X2_ROWS 0
 #endif
 #ifndef SPEF_X2_DWB2_CIN   // DWB 2 on two-pixel-tile waves up to this block input width (blocks 12-13 spill at 96;
 #define SPEF_X2_DWB2_CIN 0   // at 64, blocks 8-10 measured 143.6 -> 145.4 us per step: off)
@@ -527,17 +532,17 @@ template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, 
 #ifndef SPEF_X2W_WPE   // occupancy target of the role-split kernels (one 8-wave workgroup per CU: 2 waves per SIMD)
 #define SPEF_X2W_WPE 2
 #endif
-#if SPEF_X2W_WPE
-#define SPEF_X2W_ATTR __attribute__((amdgpu_waves_per_eu(SPEF_X2W_WPE, SPEF_X2W_WPE)))
+#if SPEF_X2W_WPE   // (one workgroup of 4 + ND_ waves per CU)
+#define SPEF_X2W_ATTR __attribute__((amdgpu_waves_per_eu((4 + ND_) / 4, (4 + ND_) / 4)))
 #else
 #define SPEF_X2W_ATTR
 #endif
-__global__ __launch_bounds__(512) SPEF_X2W_ATTR void x2_irw_kernel(
+__global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
     uint32_t nwg, size_t pstride, uint32_t ntile) {
-  using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST, P>;
+  using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST, P, ND_>;
   using SL = typename G::SL;
   static_assert(!PT || (P == 1 && G::NCL % 2 == 0 && !G::XC), "persistent tiles: one hidden part, even chunk count");
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1139,19 +1144,23 @@ __global__ __launch_bounds__(512) SPEF_X2W_ATTR void x2_irw_kernel(
       if constexpr (DWB > 0) {
       // column batches: the 3 taps' weights and slab rows of column kx issued together (sched_barrier keeps them
       // ahead of the FMAs), DWB 2: column kx + 1's batch issued before column kx's FMAs. Same FMA order.
-      float4 wv[DWB][3][2], sv[DWB][3][G::QPW][2];
+      // ROWS: a wave's pixel tiles are consecutive output rows (16-wide tiles, stride 1), so tap (ky, q) reads input
+      // row q + ky of the column: QPW + 2 row reads per column instead of 3 QPW
+      constexpr bool ROWS = SPEF_X2_ROWS && S == 1 && TW == 16 && G::QPW > 1;
+      constexpr int NR = ROWS ? G::QPW + 2 : 3 * G::QPW;
+      float4 wv[DWB][3][2], sr[DWB][NR][2];
       auto col = [&](int kx, int bf) {
 #pragma unroll
         for (int ky = 0; ky < 3; ++ky) {
           const float* wt = D + (ky * 3 + kx) * 32 + 8 * kg;
           wv[bf][ky][0] = *reinterpret_cast<const float4*>(wt);
           wv[bf][ky][1] = *reinterpret_cast<const float4*>(wt + 4);
+        }
 #pragma unroll
-          for (int q = 0; q < G::QPW; ++q) {
-            const int p = pbase[q] + ky * G::IW + kx;
-            sv[bf][ky][q][0] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
-            sv[bf][ky][q][1] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
-          }
+        for (int r = 0; r < NR; ++r) {
+          const int p = ROWS ? pbase[0] + r * G::IW + kx : pbase[r % G::QPW] + (r / G::QPW) * G::IW + kx;
+          sr[bf][r][0] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
+          sr[bf][r][1] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
         }
       };
       col(0, 0);
@@ -1165,7 +1174,10 @@ __global__ __launch_bounds__(512) SPEF_X2W_ATTR void x2_irw_kernel(
           const float4 w0 = wv[bf][ky][0], w1 = wv[bf][ky][1];
           const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
 #pragma unroll
-          for (int q = 0; q < G::QPW; ++q) dw_tap8(a[q], sv[bf][ky][q][0], sv[bf][ky][q][1], w4);
+          for (int q = 0; q < G::QPW; ++q) {
+            const int r = ROWS ? q + ky : ky * G::QPW + q;
+            dw_tap8(a[q], sr[bf][r][0], sr[bf][r][1], w4);
+          }
         }
         if (DWB == 1 && kx < 2) {
           __builtin_amdgcn_sched_barrier(0);
@@ -1280,6 +1292,11 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
 #define SPEF_X2_PERSIST 1
 #endif
 #define SPEF_X2_PK (SPEF_X2_PERSIST ? 3 : 1)
+#ifndef SPEF_X2_ND8   // eight depthwise / project waves (kind 4): 1 = blocks 8-11, 2 = blocks 8-13 (12-13 spill);
+#define SPEF_X2_ND8 0   // measured at 1: blocks 8-10 142 -> 145 us per step, block 11 unchanged (off)
+#endif
+#define SPEF_X2_PK8 (SPEF_X2_ND8 && SPEF_X2_PERSIST ? 4 : SPEF_X2_PK)
+#define SPEF_X2_PK8B (SPEF_X2_ND8 >= 2 && SPEF_X2_PERSIST ? 4 : SPEF_X2_PK)
 #if SPEF_X2_MID8
 #define SPEF_X2_MID(X)                                           \
   X(64, 384, 64, 1, true, true, 8, 8, 8, 1, 2)      /* 8-10 */   \
@@ -1287,9 +1304,9 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(96, 576, 96, 1, true, true, 8, 8, 8, 1, 2)      /* 12-13 */
 #else
 #define SPEF_X2_MID(X)                                           \
-  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK)     /* 8-10 */   \
-  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, SPEF_X2_PK)    /* 11 */     \
-  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK)     /* 12-13 */
+  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK8)     /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, SPEF_X2_PK8)    /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK8B)    /* 12-13 */
 #endif
 #define SPEF_X2_TABLE(X)                                         \
   X(32, 32, 16, 1, false, false, 8, 16, 4, 1, 0)    /* 1 */      \
@@ -1349,9 +1366,10 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
                                         tiles_x, tiles_y, nwg);
   } else if constexpr (IO == 0) {
     static_assert(EXPAND && NW == 8, "role-split blocks expand, 4 + 4 waves");
-    constexpr bool PT = KIND == 3 && P == 1;   // persistent tiles (kind 3): ceil(tiles / CUs) tiles per workgroup
-    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND != 2, P>;
-    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND != 2, P, PT>;
+    constexpr bool PT = KIND >= 3 && P == 1;   // persistent tiles (kind 3, 4): ceil(tiles / CUs) tiles per workgroup
+    constexpr int ND = KIND == 4 ? 8 : 4;
+    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND != 2, P, ND>;
+    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND != 2, P, PT, ND>;
     if (!attr_set.done()) {
       hipError_t e = x2_set_lds(k, G::LDS_BYTES);
       if (e != hipSuccess) return e;
@@ -1364,7 +1382,7 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
       const uint32_t per = (nwg + (uint32_t)num_cu - 1) / (uint32_t)num_cu;
       grid = (nwg + per - 1) / per;
     }
-    k<<<grid, 512, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
+    k<<<grid, G::NW * 64, G::LDS_BYTES, s>>>((const float*)x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp,
                                      P > 1 ? scratch : (float*)y, H, W, OH, OW, tiles_x, tiles_y, grid, pstride, nwg);
     if constexpr (P > 1) {
       const size_t n4 = pstride / 4;
