@@ -130,6 +130,9 @@ struct X2Slab {
 
 // Geometry. Output tile TH x TW, NW waves; the depthwise/project phase gives wave w the output pixel tiles of group
 // w % WP and the output-channel tiles of group w / WP (WCO groups; WCO > 1 repeats the depthwise to cut accumulators).
+#ifndef SPEF_X2_ROWS0   // slab kernels: input rows shared between a wave's vertically adjacent pixel tiles
+#define SPEF_X2_ROWS0 1   // interleaved A/B, bit-identical: blocks 5-6 117.8 -> 111.0 us per step
+#endif
 template <int CIN, int HID, int COUT, int S, int TH, int TW, bool EXPAND, int NW, int WCO>
 struct X2Geom {
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
@@ -376,6 +379,33 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
         a[q][2] = f32x2{d1.x, d1.y}; a[q][3] = f32x2{d1.z, d1.w};
       }
     }
+    if constexpr (SPEF_X2_ROWS0 && S == 1 && TW == 16 && G::QPW > 1) {
+      // a wave's pixel tiles are consecutive output rows: per column, QPW + 2 input rows read once (tap (ky, q) is
+      // row q + ky); same FMA order as below
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) {
+        float4 wv3[3][2], sr[G::QPW + 2][2];
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const float* wt = Ds + (ky * 3 + kx) * G::HIDP + 32 * c + 8 * kg;
+          wv3[ky][0] = *reinterpret_cast<const float4*>(wt);
+          wv3[ky][1] = *reinterpret_cast<const float4*>(wt + 4);
+        }
+#pragma unroll
+        for (int r = 0; r < G::QPW + 2; ++r) {
+          const int p = pbase[0] + r * G::IW + kx;
+          sr[r][0] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg));
+          sr[r][1] = *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1));
+        }
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky) {
+          const float4 w0 = wv3[ky][0], w1 = wv3[ky][1];
+          const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
+#pragma unroll
+          for (int q = 0; q < G::QPW; ++q) dw_tap8(a[q], sr[q + ky][0], sr[q + ky][1], w4);
+        }
+      }
+    } else {
 #pragma unroll
     for (int kx = 0; kx < 3; ++kx)
 #pragma unroll
@@ -390,6 +420,7 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
                   *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * kg + 1)), w4);
         }
       }
+    }
     f16x8 bh[G::QPW], bl[G::QPW];
 #pragma unroll
     for (int q = 0; q < G::QPW; ++q) relu_split8(a[q], bh[q], bl[q]);
@@ -524,10 +555,13 @@ template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, 
 #define SPEF_X2_DWB 2
 #endif
 #ifndef SPEF_X2_ROWS   // column batches share input rows between a wave's vertically adjacent pixel tiles
-#define SPEF_X2_ROWS 0
+#define SPEF_X2_ROWS 1
 #endif
-#ifndef SPEF_X2_DWB2_CIN   // DWB 2 on two-pixel-tile waves up to this block input width (blocks 12-13 spill at 96;
-#define SPEF_X2_DWB2_CIN 0   // at 64, blocks 8-10 measured 143.6 -> 145.4 us per step: off)
+// DWB 2 on two-pixel-tile waves up to this block input width. Without ROWS blocks 12-13 spilled at 96 and blocks 8-10
+// measured 143.6 -> 145.4 us per step at 64; with ROWS (4 row reads per column instead of 6, interleaved A/B,
+// bit-identical): blocks 12-13 161.6 -> 149.8, 8-10 141.7 -> 137.8, 11 53.0 -> 50.7 us per step.
+#ifndef SPEF_X2_DWB2_CIN
+#define SPEF_X2_DWB2_CIN 96
 #endif
 #ifndef SPEF_X2W_WPE   // occupancy target of the role-split kernels (one 8-wave workgroup per CU: 2 waves per SIMD)
 #define SPEF_X2W_WPE 2
