@@ -379,7 +379,9 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
         a[q][2] = f32x2{d1.x, d1.y}; a[q][3] = f32x2{d1.z, d1.w};
       }
     }
-    if constexpr (SPEF_X2_ROWS0 && S == 1 && TW == 16 && G::QPW > 1) {
+    // (blocks 5-6 only: block 3's 16 x 16 form, capped at 128 VGPRs for four waves per SIMD, spilled 30-44 VGPRs
+    // with it and ran 184 -> 374 us per step in the fp16x2 schedule)
+    if constexpr (SPEF_X2_ROWS0 && S == 1 && TW == 16 && G::QPW > 1 && NW == 4 && EXPAND && CIN >= 32) {
       // a wave's pixel tiles are consecutive output rows: per column, QPW + 2 input rows read once (tap (ky, q) is
       // row q + ky); same FMA order as below
 #pragma unroll
