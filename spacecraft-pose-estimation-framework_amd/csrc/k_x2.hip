@@ -1894,8 +1894,14 @@ __global__ __launch_bounds__(256) void x2_pw_kernel(const float* __restrict__ X,
 #ifndef SPEF_X2_PWS
 #define SPEF_X2_PWS 1
 #endif
-template <bool POOL>
-__global__ __launch_bounds__(256) void x2_pws_kernel(const float* __restrict__ X, const _Float16* __restrict__ Wt,
+// Waves (64 output channels each) per workgroup. 5: 1280 / 320 = 4 channel chunks, 1024 workgroups at B = 64 (two
+// full rounds at two per CU instead of 2.5) -- measured 64 -> 71 us per step (ten waves per CU load the four SIMDs
+// 3 / 3 / 2 / 2): kept at 4.
+#ifndef SPEF_X2_PWS_NWV
+#define SPEF_X2_PWS_NWV 4
+#endif
+template <bool POOL, int NWV = 4>
+__global__ __launch_bounds__(NWV * 64) void x2_pws_kernel(const float* __restrict__ X, const _Float16* __restrict__ Wt,
                                                      const float* __restrict__ bias, float* __restrict__ Y, int64_t M,
                                                      int K, int N, int Np, int Kp, int n_chunks, uint32_t nwg) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -1906,16 +1912,16 @@ __global__ __launch_bounds__(256) void x2_pws_kernel(const float* __restrict__ X
   const int64_t m0 = (int64_t)(L / (uint32_t)n_chunks) * 64;
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
-  const int n0 = chunk * 256 + wave * 64;
+  const int n0 = chunk * (64 * NWV) + wave * 64;
   const _Float16* Wlo = Wt + (size_t)Np * Kp;
   // ---- stage: 64 rows x Kp / 8 granules, 8 fp32 -> hi / lo per piece (batches of 5 pieces per thread, loads first)
   {
     const int GP = Kp >> 3, NP = 64 * GP;
-    for (int u0 = 0; u0 < NP; u0 += 256 * 5) {
+    for (int u0 = 0; u0 < NP; u0 += NWV * 64 * 5) {
       float4 v[5][2];
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const int u = u0 + tid + 256 * i;
+        const int u = u0 + tid + NWV * 64 * i;
         const int px = u / GP, g = u - px * GP;
         const int64_t p = m0 + px;
         v[i][0] = v[i][1] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1927,7 +1933,7 @@ __global__ __launch_bounds__(256) void x2_pws_kernel(const float* __restrict__ X
       }
 #pragma unroll
       for (int i = 0; i < 5; ++i) {
-        const int u = u0 + tid + 256 * i;
+        const int u = u0 + tid + NWV * 64 * i;
         if (u >= NP) break;
         const int px = u / GP, g = u - px * GP;
         const float f[8] = {v[i][0].x, v[i][0].y, v[i][0].z, v[i][0].w, v[i][1].x, v[i][1].y, v[i][1].z, v[i][1].w};
@@ -2014,24 +2020,33 @@ __global__ __launch_bounds__(256) void x2_pws_kernel(const float* __restrict__ X
   }
 }
 
-static bool x2_pws_ok(int Kp, int Np) { return SPEF_X2_PWS && Kp % 64 == 0 && Kp <= 320 && Np % 256 == 0; }
+static bool x2_pws_ok(int Kp, int Np) {
+  return SPEF_X2_PWS && Kp % 64 == 0 && Kp <= 320 && Np % 256 == 0;   // (NWV 5 falls back to 4 unless Np % 320 == 0)
+}
 
 template <bool POOL>
 static hipError_t x2_pws_go(const void* x, const void* wt, const float* bias, float* y, int64_t M, int K, int N, int Np,
                             int Kp, hipStream_t s) {
-  const int n_chunks = Np / 256;
+  const bool five = SPEF_X2_PWS_NWV == 5 && Np % 320 == 0;
+  const int n_chunks = Np / (five ? 320 : 256);
   const int64_t nwg64 = (M + 63) / 64 * n_chunks;
   if (nwg64 > 0x7fffffff) return hipErrorInvalidValue;
   const uint32_t nwg = (uint32_t)nwg64;
   const int lds = 64 * Kp * 2 * (int)sizeof(_Float16);
   static DevOnce attr_set;
   if (!attr_set.done()) {
-    hipError_t e = x2_set_lds(x2_pws_kernel<POOL>, 64 * 320 * 2 * (int)sizeof(_Float16));   // the largest Kp
-    if (e != hipSuccess) return e;
+    for (auto k : {x2_pws_kernel<POOL, 4>, x2_pws_kernel<POOL, 5>}) {
+      hipError_t e = x2_set_lds(k, 64 * 320 * 2 * (int)sizeof(_Float16));   // the largest Kp
+      if (e != hipSuccess) return e;
+    }
     attr_set.set();
   }
-  x2_pws_kernel<POOL><<<nwg, 256, lds, s>>>((const float*)x, (const _Float16*)wt, bias, y, M, K, N, Np, Kp, n_chunks,
-                                            nwg);
+  if (five)
+    x2_pws_kernel<POOL, 5><<<nwg, 320, lds, s>>>((const float*)x, (const _Float16*)wt, bias, y, M, K, N, Np, Kp,
+                                                 n_chunks, nwg);
+  else
+    x2_pws_kernel<POOL, 4><<<nwg, 256, lds, s>>>((const float*)x, (const _Float16*)wt, bias, y, M, K, N, Np, Kp,
+                                                 n_chunks, nwg);
   return hipGetLastError();
 }
 

@@ -15,6 +15,6 @@ for r in (1,2):
     d=json.load(open('gpurun_out/var_'+f+'.json'))
     print(f, d['value'], d['ms_per_step'])
     for k,x in d['kernels'].items():
-        if 'x2_irb' in k: rows.setdefault(k,{})[f]=round(x['ms_per_step']*1e3,1)
+        if 'x2_irb' in k or 'x2_pw' in k: rows.setdefault(k,{})[f]=round(x['ms_per_step']*1e3,1)
 for k,v in rows.items(): print(k, v)
 " "$V"
