@@ -1264,8 +1264,17 @@ __global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
           if (c == G::NCL - 2) {
             fetch_res(b_, oy_, ox_);
           } else {
+            // the next tile's bias loads go out before the epilogue's stores: vmcnt counts both in order, so a
+            // wait for loads issued after the stores would wait for the stores too
+            float4 bn[G::NCTW];
+#pragma unroll
+            for (int t = 0; t < G::NCTW; ++t)
+              bn[t] = *reinterpret_cast<const float4*>(bp + (wc * G::NCTW + t) * 16 + 4 * kg);
             epilogue(b_, oy_, ox_);
-            init_acc();
+#pragma unroll
+            for (int t = 0; t < G::NCTW; ++t)
+#pragma unroll
+              for (int q = 0; q < G::QPW; ++q) acc[q][t] = f32x4{bn[t].x, bn[t].y, bn[t].z, bn[t].w};
           }
         }
       }
