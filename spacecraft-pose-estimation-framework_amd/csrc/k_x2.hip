@@ -130,6 +130,9 @@ struct X2Slab {
 
 // Geometry. Output tile TH x TW, NW waves; the depthwise/project phase gives wave w the output pixel tiles of group
 // w % WP and the output-channel tiles of group w / WP (WCO groups; WCO > 1 repeats the depthwise to cut accumulators).
+#ifndef SPEF_X2_RES_AHEAD   // persistent tiles: chunks before a tile's end at which its residual is fetched (4: no gain)
+#define SPEF_X2_RES_AHEAD 2
+#endif
 #ifndef SPEF_X2_ROWS0   // slab kernels: input rows shared between a wave's vertically adjacent pixel tiles
 #define SPEF_X2_ROWS0 1   // interleaved A/B, bit-identical: blocks 5-6 117.8 -> 111.0 us per step
 #endif
@@ -1258,10 +1261,10 @@ __global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
         if (g + 1 < GT) load_pg(kmod(g + 1));   // next chunk's fragments: in flight across the barrier and its depthwise
       }
       if constexpr (PT) {
-        if (c >= G::NCL - 2) {
+        if (c == G::NCL - SPEF_X2_RES_AHEAD || c == G::NCL - 1) {
           int b_, oy_, ox_;
           tile_of(L0 + (uint32_t)(g / G::NCL) * nwg, b_, oy_, ox_);
-          if (c == G::NCL - 2) {
+          if (c == G::NCL - SPEF_X2_RES_AHEAD) {
             fetch_res(b_, oy_, ox_);
           } else {
             // the next tile's bias loads go out before the epilogue's stores: vmcnt counts both in order, so a
