@@ -20,7 +20,9 @@ runs independent batches of 64 (frame-parallel, weak scaling, no data-path colle
 sync on both sides of exactly K steps, max over ranks; value = all ranks' images / that time.
 ``--dry-run`` runs the same control flow on CPU with gloo (no device work; tests/test_bench_dist.py).
 
-Rank 0 prints ONE JSON line (fields: DESIGN.md section 9).
+Rank 0 prints ONE JSON line, the last line of stdout, kept to a few KB (``compact_record``: contract fields, roofline,
+cpu_baseline, pose errors, one summary per sub-record); the full record with the per-kernel tables and every sub-record
+goes to ``--detail-out`` (default gpurun_out/bench_detail.json). Fields: DESIGN.md section 9.
 """
 from __future__ import annotations
 
@@ -249,6 +251,7 @@ def roofline(prof, steps, B, traffic_path, peaks=None, int8=False):
             'unit': 'TFLOP/s', 'frac': round(ach_tfl / MFMA_PEAK_TFLOPS, 4),
             'traffic': None if traffic is None else round(traffic),
             'traffic_source': os.path.relpath(traffic_path, ROOT) if traffic is not None else None,
+            'traffic_over_algorithmic': None if traffic is None or not byts else round(traffic / (byts / n), 3),
             'algorithmic_flops_per_launch': round(fl / n), 'algorithmic_bytes_per_launch': round(byts / n),
             'avg_launch_us': round(avg_s * 1e6, 2), 'launches_per_step': n / steps,
             'hbm': {'achieved': round(ach_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
@@ -261,6 +264,61 @@ def roofline(prof, steps, B, traffic_path, peaks=None, int8=False):
         rec['peak_measured'], rec['frac_measured'] = pm, round(ach_tfl / pm, 4) if pm else None
         hm = peaks['hbm_read_gbs']
         rec['hbm']['peak_measured'], rec['hbm']['frac_measured'] = hm, round(ach_gbs / hm, 4) if hm else None
+    return rec
+
+
+HEADLINE_MAX_BYTES = 6000   # the driver parses the LAST stdout line from an 8 KB tail (BENCH_r05: a 22.5 KB line failed)
+
+
+def _clock(c):
+    return None if not isinstance(c, dict) else {k: c[k] for k in ('sclk_mhz', 'spread_mhz') if k in c}
+
+
+def compact_record(full: dict, detail_path=None) -> dict:
+    """The headline JSON line: the contract fields, ``roofline``, ``cpu_baseline``, ``peak_measured``, the pose errors
+    and a one-line summary of every sub-record (img/s + tolerance flag). Per-kernel tables and the sub-records
+    themselves stay in ``full`` (written to the sidecar ``detail_path``), so the line stays a few KB."""
+    keep = ('metric', 'value', 'unit', 'n_gpus', 'steps', 'warmup', 'ms_per_step', 'higher_is_better', 'scaling',
+            'vs_baseline', 'dtype', 'arith', 'data', 'config', 'clock_settle_s', 'graphs', 'dry_run',
+            'mfma_utilisation_whole_net', 'mfma_utilisation_whole_net_measured_peak', 'cpu_baseline',
+            'pose_err_vs_fp32', 'within_north_star')
+    rec = {k: full[k] for k in keep if k in full}
+    if 'sclk_timed_region' in full:
+        rec['sclk_timed_region'] = _clock(full['sclk_timed_region'])
+    if isinstance(full.get('peak_measured'), dict):
+        rec['peak_measured'] = {k: v for k, v in full['peak_measured'].items() if not isinstance(v, (dict, str))}
+    if isinstance(full.get('roofline'), dict):
+        rf = dict(full['roofline'])
+        rf.pop('sclk_leg', None)
+        rec['roofline'] = rf
+    sh = full.get('pose_err_vs_fp32_sharp_head')
+    if isinstance(sh, dict):
+        rec['pose_err_vs_fp32_sharp_head'] = {
+            'frames': sh.get('frames'), 'head': sh.get('head'),
+            **({full['dtype']: sh[full['dtype']]} if full.get('dtype') in sh else {}),
+            'within_tolerance_by_dtype': {k: v['within_tolerance'] for k, v in sh.items()
+                                          if isinstance(v, dict) and 'within_tolerance' in v}}
+    subs = {}
+    for k in ('c5', 'fp16x2', 'fp16'):
+        s = full.get(k)
+        if isinstance(s, dict):
+            pe = s.get('pose_err_vs_fp32', {})
+            subs[k] = {'value': s.get('value'), 'dtype': s.get('dtype'),
+                       'roofline_frac': s.get('roofline_kernel', {}).get('frac'),
+                       **{f: pe[f] for f in ('ori_logit_max_abs', 'within_tolerance', 'within_int8_tolerance')
+                          if f in pe}}
+    kp = full.get('keypoint_mode')
+    if isinstance(kp, dict):
+        subs['keypoint_mode'] = {dt: {'value': kp[dt].get('value'),
+                                      'within_tolerance': kp[dt].get('pose_err_vs_fp32', {}).get('within_tolerance'),
+                                      'pos_max_m': kp[dt].get('pose_err_vs_fp32', {}).get('pos_max_m')}
+                                 for dt in ('fp32', 'fp16x2', 'fp16') if isinstance(kp.get(dt), dict)}
+        if isinstance(kp.get('epnp'), dict):
+            subs['epnp'] = {k: kp['epnp'].get(k) for k in ('value', 'unit', 'latency_b64_us', 'kat_max_ori_deg')}
+    if subs:
+        rec['sub_records'] = subs
+    if detail_path:
+        rec['detail'] = detail_path
     return rec
 
 
@@ -512,6 +570,8 @@ def main():
     ap.add_argument('--traffic', default=None,
                     help='committed rocprofv3 FETCH/WRITE summary used for roofline.traffic (default: the newest '
                          'committed profiles/*_pmc_traffic.json of the path)')
+    ap.add_argument('--detail-out', default=os.path.join('gpurun_out', 'bench_detail.json'),
+                    help='sidecar file for the full record (per-kernel tables, every sub-record); \'\' = none')
     ap.add_argument('--dry-run', action='store_true',
                     help='CPU + gloo: the distributed control flow (weight distribution, timing, max over ranks, '
                          'JSON) without device work')
@@ -685,7 +745,21 @@ def main():
                                                     rec['pose_err_vs_fp32']['within_tolerance'])
             if world == 1 and not args.no_keypoint:
                 rec['keypoint_mode'] = run_keypoint(args, dev, with_ref=not args.no_cpu_baseline)
-        print(json.dumps(rec), flush=True)
+        # full record (per-kernel tables, every sub-record) to the sidecar; the LAST stdout line is the compact headline
+        detail = args.detail_out or None
+        if detail:
+            try:
+                os.makedirs(os.path.dirname(os.path.abspath(detail)), exist_ok=True)
+                with open(detail, 'w') as f:
+                    json.dump(rec, f)
+            except OSError as e:
+                print(f'bench: could not write {detail}: {e}', file=sys.stderr)
+                detail = None
+        line = json.dumps(compact_record(rec, detail))
+        if len(line) > HEADLINE_MAX_BYTES:
+            print(f'bench: headline line {len(line)} B exceeds {HEADLINE_MAX_BYTES} B', file=sys.stderr)
+        sys.stderr.flush()
+        print(line, flush=True)
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()

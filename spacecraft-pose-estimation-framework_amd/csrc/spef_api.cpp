@@ -350,7 +350,9 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const bool o16 = out16(op);
         const int io = (cur16 ? 1 : 0) | (o16 ? 2 : 0);
         const double ib = cur16 ? 2 : 4, ob = o16 ? 2 : 4;
-        const double bytes = (double)M * op.cin * ib + (double)M2 * op.cout * (ob + (res ? ib : 0)) +
+        // compulsory bytes: the block input once (a stride-1 residual IS that input: not counted twice), the output,
+        // the weights once (the fp16 formula below counts the same way)
+        const double bytes = (double)M * op.cin * ib + (double)M2 * op.cout * ob +
                              (expand ? hp * ((op.cin + 31) & ~31u) * 4 : 0) + hp * 48 +
                              ((op.cout + 15) & ~15u) * (hp * 4 + 4);
         char key[96];
