@@ -37,36 +37,23 @@ __device__ __forceinline__ double rsq_nr(double x) {   // x > 0
 // Division and square root in the small serial solves (QR least squares, Gauss-Newton, Procrustes): the same
 // hardware-estimate + Newton forms (a x (1/b) is within an ulp or two of a / b, against ~15 dependent instructions of
 // the IEEE division sequence on one lane's critical path).
-#ifndef SPEF_EPNP_FASTDIV
-#define SPEF_EPNP_FASTDIV 1
-#endif
-#if SPEF_EPNP_FASTDIV
 __device__ __forceinline__ double ddiv(double a, double b) { return a * rcp_nr(b); }
 __device__ __forceinline__ double dsqrt(double x) { return x > 0.0 ? x * rsq_nr(x) : 0.0; }   // x >= 0
-#else
-__device__ __forceinline__ double ddiv(double a, double b) { return a / b; }
-__device__ __forceinline__ double dsqrt(double x) { return sqrt(x); }
-#endif
-#ifndef SPEF_EPNP_ROT32
-#define SPEF_EPNP_ROT32 1
-#endif
-#ifndef SPEF_EPNP_FUSEROT
-#define SPEF_EPNP_FUSEROT 0
-#endif
-#ifndef SPEF_EPNP_ROTLOCAL
-#define SPEF_EPNP_ROTLOCAL 0
-#endif
+// The angle in fp32 (fast rcp / sqrt), the rotation itself orthogonal to fp64 for that angle. Where fp32 cannot
+// represent 2 a_pq (|a_pq| below ~1e-38 while the fp64 skip guard let it through) or the fp32 angle is not finite,
+// the rotation is the fp64 form below, so no 0 x inf reaches (c, s).
 __device__ __forceinline__ void jacobi_rot(double app, double aqq, double apq, double& c, double& s) {
-#if SPEF_EPNP_ROT32   // the angle in fp32 (fast rcp / sqrt), the rotation itself orthogonal to fp64 for that angle
-  {
-    const float th = (float)(aqq - app) * __builtin_amdgcn_rcpf((float)(2.0 * apq));
-    const float tf = (th >= 0 ? 1.0f : -1.0f) * __builtin_amdgcn_rcpf(fabsf(th) + __builtin_sqrtf(th * th + 1.0f));
-    const double t = (double)tf;
-    c = rsq_nr(t * t + 1.0);
-    s = t * c;
-    return;
+  const float den = (float)(2.0 * apq);
+  if (fabsf(den) >= 1.17549435e-38f) {   // FLT_MIN: a normal fp32 divisor
+    const float th = (float)(aqq - app) * __builtin_amdgcn_rcpf(den);
+    if (__builtin_isfinite(th)) {
+      const float tf = (th >= 0 ? 1.0f : -1.0f) * __builtin_amdgcn_rcpf(fabsf(th) + __builtin_sqrtf(th * th + 1.0f));
+      const double t = (double)tf;
+      c = rsq_nr(t * t + 1.0);
+      s = t * c;
+      return;
+    }
   }
-#endif
   const double theta = (aqq - app) * rcp_nr(2.0 * apq);
   double t;
   if (fabs(theta) > 1e100) {                             // sqrt(theta^2 + 1) = |theta| to fp64: t = 1 / (2 theta)
@@ -242,7 +229,6 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
                                                    float* __restrict__ pos, int* __restrict__ status) {
   __shared__ double As[2][144], Vs[2][144];
   __shared__ double Cc[12], Cs[12];
-  __shared__ double Cr[2][2][12];   // SPEF_EPNP_FUSEROT: [buffer][c | signed s][index]
   __shared__ double Pal[EPNP_MAXN][4], Pdu[EPNP_MAXN], Pdv[EPNP_MAXN];
   __shared__ double Red[3][2];
   __shared__ double Ls[6][10], Rho[6];
@@ -250,10 +236,6 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
   const int b = blockIdx.x;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   if (b >= B) return;   // uniform per workgroup
-#if defined(SPEF_EPNP_ABL) && SPEF_EPNP_ABL == 4   // timing ablation: launch only
-  if (tid == 0) status[b] = 0;
-  return;
-#endif
   const int nk = 2 * (n + 1);
 
   // ---- points: lane i <= n reads raw point i (origin first); lane j < n then owns keypoint j (every wave)
@@ -310,31 +292,8 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
   __syncthreads();
 
   // ---- parallel cyclic Jacobi (tournament order): sweeps of 11 rounds x 6 disjoint rotations
-#ifndef SPEF_EPNP_ABL   // timing ablations only (wrong results): 1 = no Jacobi sweeps, 2 = approximation 1 only
-#define SPEF_EPNP_ABL 0
-#endif
-#if SPEF_EPNP_ABL == 3   // timing ablation: set-up (points, M^T M) only
-  if (tid == 0) status[b] = (int)(As[0][0] != 0.0);
-  return;
-#endif
   int cur = 0;
-#if SPEF_EPNP_FUSEROT
-  // One barrier per round: the six threads owning the next round's pivots a_pq (p < q) also form that round's a_pp and
-  // a_qq from this round's inputs and compute the next rotation right after their own update (coefficients
-  // double-buffered in Cr[cb]); the first round's rotations come from the initial matrix.
-  int cb = 0;
-  if (tid < 12) {
-    const int j = rr_partner(0, tid);
-    const int p = tid < j ? tid : j, q = tid < j ? j : tid;
-    const double apq = As[0][12 * p + q];
-    double c = 1.0, sn = 0.0;
-    if (fabs(apq) >= 1e-300) jacobi_rot(As[0][13 * p], As[0][13 * q], apq, c, sn);
-    Cr[0][0][tid] = c;
-    Cr[0][1][tid] = tid == p ? -sn : sn;
-  }
-  __syncthreads();
-#endif
-  for (int sweep = 0; sweep < (SPEF_EPNP_ABL == 1 ? 0 : 40); ++sweep) {
+  for (int sweep = 0; sweep < 40; ++sweep) {
     double off = 0.0, diag = 0.0;
     if (ent) {
       const double a = As[cur][e];
@@ -354,49 +313,7 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
 #define SPEF_EPNP_JTOL 1e-26
 #endif
     if (off <= SPEF_EPNP_JTOL * diag || off == 0.0) break;   // uniform: every thread read the same sums
-#if SPEF_EPNP_FUSEROT
     for (int r = 0; r < 11; ++r) {
-      if (ent) {
-        const int i2 = rr_partner(r, ei), j2 = rr_partner(r, ej);
-        const double ci = Cr[cb][0][ei], si = Cr[cb][1][ei], cj = Cr[cb][0][ej], sj = Cr[cb][1][ej];
-        const double* a = As[cur];
-        const double anew = ci * (cj * a[12 * ei + ej] + sj * a[12 * ei + j2]) + si * (cj * a[12 * i2 + ej] + sj * a[12 * i2 + j2]);
-        As[cur ^ 1][e] = anew;
-        const double* v = Vs[cur];
-        Vs[cur ^ 1][e] = cj * v[12 * ei + ej] + sj * v[12 * ei + j2];
-        const int rn = r == 10 ? 0 : r + 1;
-        if (ei < ej && rr_partner(rn, ei) == ej) {   // pivot (ei, ej) of the next round: a_pp', a_qq' as above
-          const double pp = ci * (ci * a[13 * ei] + si * a[12 * ei + i2]) + si * (ci * a[12 * i2 + ei] + si * a[13 * i2]);
-          const double qq = cj * (cj * a[13 * ej] + sj * a[12 * ej + j2]) + sj * (cj * a[12 * j2 + ej] + sj * a[13 * j2]);
-          double c = 1.0, sn = 0.0;
-          if (fabs(anew) >= 1e-300) jacobi_rot(pp, qq, anew, c, sn);
-          Cr[cb ^ 1][0][ei] = c;
-          Cr[cb ^ 1][1][ei] = -sn;
-          Cr[cb ^ 1][0][ej] = c;
-          Cr[cb ^ 1][1][ej] = sn;
-        }
-      }
-      cur ^= 1;
-      cb ^= 1;
-      __syncthreads();
-    }
-#else
-    for (int r = 0; r < 11; ++r) {
-#if SPEF_EPNP_ROTLOCAL   // every thread computes the two rotations it applies (one barrier per round instead of two)
-      const int i2 = rr_partner(r, ei), j2 = rr_partner(r, ej);
-      auto coef = [&](int i, int j, double& c, double& sg) {   // index i's signed coefficient of pair (i, j)
-        const int p = i < j ? i : j, q = i < j ? j : i;
-        const double apq = As[cur][12 * p + q];
-        double sn = 0.0;
-        c = 1.0;
-        if (fabs(apq) >= 1e-300) jacobi_rot(As[cur][13 * p], As[cur][13 * q], apq, c, sn);
-        sg = i == p ? -sn : sn;
-      };
-      if (ent) {
-        double ci, si, cj, sj;
-        coef(ei, i2, ci, si);
-        coef(ej, j2, cj, sj);
-#else
       if (tid < 12) {   // thread i: the rotation of its pair, its own signed coefficient
         const int j = rr_partner(r, tid);
         const int p = tid < j ? tid : j, q = tid < j ? j : tid;
@@ -410,7 +327,6 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
       if (ent) {
         const int i2 = rr_partner(r, ei), j2 = rr_partner(r, ej);
         const double ci = Cc[ei], si = Cs[ei], cj = Cc[ej], sj = Cs[ej];
-#endif
         const double* a = As[cur];
         As[cur ^ 1][e] = ci * (cj * a[12 * ei + ej] + sj * a[12 * ei + j2]) + si * (cj * a[12 * i2 + ej] + sj * a[12 * i2 + j2]);
         const double* v = Vs[cur];
@@ -419,7 +335,6 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
       cur ^= 1;
       __syncthreads();
     }
-#endif
   }
   // the 4 eigenvectors of smallest eigenvalue, ascending (ties keep the lower index); static loops only (a
   // dynamically indexed private array would live in scratch)
@@ -486,7 +401,7 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
 
   // ---- approximation ap = wave + 1 (epnp.cpp compute_pose: find_betas_approx_1/2/3 + gauss_newton + compute_R_and_t)
   const int ap = wave + 1;
-  if (SPEF_EPNP_ABL != 2 || ap == 1) {
+  {
     double be[4] = {0, 0, 0, 0};
     double rr[6];
 #pragma unroll
@@ -608,8 +523,6 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
         Res[wave][10 + i] = t[i];
       }
     }
-  } else if (lane == 0) {
-    Res[wave][0] = INFINITY;
   }
   __syncthreads();
   if (tid != 0) return;

@@ -28,22 +28,6 @@
 #include "spef_common.hpp"
 #include "spef_kernels.hpp"
 
-#ifndef SPEF_MX_ALIAS
-#define SPEF_MX_ALIAS 1
-#endif
-#ifndef SPEF_MX_HALF_LAST   // HID % 32 == 16: skip the empty half of the last hidden chunk
-#define SPEF_MX_HALF_LAST 0
-#endif
-#ifndef SPEF_MX_FRONT_F32W   // front kernel: block-1 depthwise with fp32 weights (one v_fma_mix per tap)
-#define SPEF_MX_FRONT_F32W 1
-#endif
-#ifndef SPEF_MX_DEINTERLEAVE
-#define SPEF_MX_DEINTERLEAVE 0
-#endif
-#ifndef SPEF_MX_PACK16
-#define SPEF_MX_PACK16 1
-#endif
-
 namespace spef {
 
 namespace {
@@ -95,10 +79,10 @@ struct MxGeom {
   static constexpr int SLAB_B = PINP * SPB;
   static constexpr int DX_B = POUT * DXB + 16;            // one exchange plane (+ the odd-row-group skew)
   static constexpr int TRASH_B = 16 * SPB;                // dummy rows for invalid pixels' expand stores
-  // SPEF_MX_ALIAS: the exchange planes overlay the slab (two more barriers per chunk, ~35 % less LDS: 3 workgroups per CU
-  // instead of 2 at stride 2)
-  static constexpr int OFF_DX = SPEF_MX_ALIAS ? 0 : SLAB_B;
-  static constexpr int OFF_TR = SPEF_MX_ALIAS ? (SLAB_B > 2 * DX_B ? SLAB_B : 2 * DX_B) : OFF_DX + 2 * DX_B;
+  // the exchange planes overlay the slab (two more barriers per chunk, ~35 % less LDS: 3 workgroups per CU instead of
+  // 2 at stride 2)
+  static constexpr int OFF_DX = 0;
+  static constexpr int OFF_TR = SLAB_B > 2 * DX_B ? SLAB_B : 2 * DX_B;
   static constexpr int LDS_BYTES = OFF_TR + TRASH_B;
   static constexpr int WAVES_PER_EU = (163840 / LDS_BYTES) > 4 ? 4 : (163840 / LDS_BYTES);   // (> 4: spills)
   static_assert(CIN <= 32 && CIN % 8 == 0, "blocks 2-7: one K = 32 step");
@@ -117,8 +101,8 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
   constexpr int TW = G::TW;
   // CIN = 16 (block 2): W_hi x + W_lo x as ONE K = 32 MFMA -- A = [W_hi | W_lo] along k, B = [x ; x] (lanes kg = 2, 3
   // repeat the channels of kg = 0, 1): half the expand MFMAs of the two-product form, the same sums.
-  constexpr bool PK = IN16 && CIN == 16 && SPEF_MX_PACK16;
-  constexpr bool HALF_LAST = HID % 32 == 16 && SPEF_MX_HALF_LAST;
+  static_assert(IN16, "fp16 block input (blocks 2-4; blocks 5-7 run the fp16x2 slab kernel)");
+  constexpr bool PK = CIN == 16;
   constexpr int KX = PK ? 16 : 32;   // channel span of the B fragment's k groups
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
@@ -134,21 +118,9 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
   const size_t xb = (size_t)b * H * W * CIN;   // element offset of this image's input
 
   // ---- expand operands: this wave's input-tile pixel tiles pt = wave + 4 j (lane: pixel r16, channels 8kg..8kg+7);
-  // an fp32 input (blocks 5-7) is split hi / lo once (three MFMAs per product), an fp16 input is exact (two)
-  // slab slot of input-tile pixel p: row-major, except that at stride 2 a row holds its even columns, then its odd ones
-  // (the depthwise's 16 lanes then read 16 consecutive slots -- 80-B steps, conflict-free -- instead of every other)
-  constexpr bool DEI = S == 2 && SPEF_MX_DEINTERLEAVE;
-  constexpr int HALF = (G::IW + 1) / 2;
-  auto slab_slot = [&](int p) {
-    if constexpr (DEI) {
-      const int py = p / G::IW, px = p - py * G::IW;
-      return py * G::IW + ((px & 1) ? HALF + (px >> 1) : (px >> 1));
-    } else {
-      return p;
-    }
-  };
-  f16x8 bx[G::EPT], bxl[IN16 ? 1 : G::EPT];
-  uint32_t zmask = 0;   // SPEF_MX_ALIAS: the lane's padding pixels (per expand tile)
+  // the fp16 input is exact (two MFMAs per product); slab slot of input-tile pixel p: p (row-major)
+  f16x8 bx[G::EPT];
+  uint32_t zmask = 0;   // the lane's padding pixels (per expand tile)
   const bool edge = iy0 < 0 || ix0 < 0 || iy0 + G::IH > H || ix0 + G::IW > W;   // workgroup-uniform
   int soff[G::EPT];   // slab byte offset of the lane's pixel (channels 4kg.. of h = 0), or its dummy row
 #pragma unroll
@@ -164,28 +136,13 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     }
     const int kc = 8 * kg % KX;   // the lane's first input channel
     const size_t e0 = xb + ((size_t)iy * W + ix) * CIN + kc;
-    if constexpr (IN16) {
+    {
       uint4 v = make_uint4(0u, 0u, 0u, 0u);
       if (ok && kc < CIN) v = *reinterpret_cast<const uint4*>(reinterpret_cast<const _Float16*>(X) + e0);
       bx[j] = __builtin_bit_cast(f16x8, v);
-    } else {
-      float4 v0 = make_float4(0.f, 0.f, 0.f, 0.f), v1 = v0;
-      if (ok && 8 * kg < CIN) {
-        v0 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + e0);
-        v1 = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + e0 + 4);
-      }
-      const float f[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-      uint32_t hh[4], ll[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        hh[e] = pack_h2((_Float16)f[2 * e], (_Float16)f[2 * e + 1]);
-        ll[e] = lo_pair_mx(hh[e], f[2 * e], f[2 * e + 1]);
-      }
-      bx[j] = __builtin_bit_cast(f16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
-      bxl[j] = __builtin_bit_cast(f16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
     }
-    const int ps = slab_slot(p);
-    if (!ok && p < G::PIN) zmask |= 1u << j;   // (SPEF_MX_ALIAS: re-zeroed every chunk on edge tiles)
+    const int ps = p;
+    if (!ok && p < G::PIN) zmask |= 1u << j;   // (re-zeroed every chunk on edge tiles: the exchange overlays the slab)
     soff[j] = ok ? ps * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
     if (!ok && p < G::PIN) {   // the depthwise's zero padding: stored once, never overwritten
       *reinterpret_cast<uint2*>(smem + ps * G::SPB + 8 * kg) = make_uint2(0u, 0u);
@@ -196,8 +153,8 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
   // ---- depthwise lane geometry: (row group ry, column cx) from the ds_read_b128 lane groups
   int ry, cx;
   b128_group(lane, ry, cx);
-  const int dbase = (S * ry * G::PPL * G::IW + (DEI ? cx : S * cx)) * G::SPB + 16 * wave;   // input row 0, kx 0
-  constexpr int KXO[3] = {0, (DEI ? HALF : 1) * G::SPB, (DEI ? 1 : 2) * G::SPB};   // slab byte step of tap kx
+  const int dbase = (S * ry * G::PPL * G::IW + S * cx) * G::SPB + 16 * wave;   // input row 0, kx 0
+  constexpr int KXO[3] = {0, G::SPB, 2 * G::SPB};   // slab byte step of tap kx
   char* Dh = smem + G::OFF_DX;
   char* Dl = Dh + G::DX_B;
   const int skw = (ry & 1) * 16;
@@ -239,11 +196,6 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
 
 #pragma unroll 1
   for (int c = 0; c < G::NCH; ++c) {
-    // HID = 144 (blocks 3, 4): the last chunk holds 16 real channels. Its upper half is skipped -- no expand MFMAs or
-    // stores for hidden rows 16-31, no depthwise on waves 2-3 -- so those slab / exchange rows keep the previous
-    // chunk's finite values, which meet the zero-padded project weights of rows >= HID (0 x finite = 0).
-    const bool half = HALF_LAST && c == G::NCH - 1;
-    const bool dw_on = !(half && wave >= 2);
     // wave-uniform depthwise weights + bias of this wave's 8 channels (scalar loads; fp32, exact)
     const float* wdc = Wd + 32 * c + 8 * wave;
     float wd[9][8], db[8];
@@ -266,24 +218,17 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       for (int j = 0; j < G::EPT; ++j) {
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          if (h == 1 && half) continue;
           f32x4 e = f32x4{eb[h].x, eb[h].y, eb[h].z, eb[h].w};
-          if constexpr (PK) {
-            e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e, 0, 0, 0);
-          } else if constexpr (IN16) {
-            e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e, 0, 0, 0);
-            e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eal[h], bx[j], e, 0, 0, 0);
-          } else {
-            e = mfma3(eah[h], eal[h], bx[j], bxl[IN16 ? 0 : j], e);
-          }
+          e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e, 0, 0, 0);
+          if constexpr (!PK) e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eal[h], bx[j], e, 0, 0, 0);
           *reinterpret_cast<uint2*>(smem + soff[j] + 32 * h) = make_uint2(relu_pk2(e[0], e[1]), relu_pk2(e[2], e[3]));
         }
       }
-      if (SPEF_MX_ALIAS && edge && c > 0) {   // the exchange overlaid the slab: restore the depthwise's zero padding
+      if (edge && c > 0) {   // the exchange overlaid the slab: restore the depthwise's zero padding
 #pragma unroll
         for (int j = 0; j < G::EPT; ++j)
           if ((zmask >> j) & 1u) {
-            const int zo = slab_slot((wave + G::NW * j) * 16 + r16) * G::SPB + 8 * kg;
+            const int zo = ((wave + G::NW * j) * 16 + r16) * G::SPB + 8 * kg;
             *reinterpret_cast<uint2*>(smem + zo) = make_uint2(0u, 0u);
             *reinterpret_cast<uint2*>(smem + zo + 32) = make_uint2(0u, 0u);
           }
@@ -294,7 +239,6 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
 
     // ---- depthwise: PPL output rows of column cx, channels 8 wave .. +7, fp32 accumulation, exact weights
     float a[G::PPL][8];
-    if (dw_on) {
 #pragma unroll
     for (int t = 0; t < G::PPL; ++t)
 #pragma unroll
@@ -317,10 +261,8 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
         }
       }
     }
-    }   // dw_on
-    if constexpr (SPEF_MX_ALIAS) __syncthreads();   // every wave's slab reads done before the exchange overlays it
+    __syncthreads();   // every wave's slab reads done before the exchange overlays it
     // ReLU, hi / lo split -> exchange buffer (pixel (row ry PPL + t, column cx), channels 8 wave ..)
-    if (dw_on) {
 #pragma unroll
     for (int t = 0; t < G::PPL; ++t) {
       uint32_t hh[4], ll[4];
@@ -335,7 +277,6 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       *reinterpret_cast<uint4*>(Dh + o) = make_uint4(hh[0], hh[1], hh[2], hh[3]);
       *reinterpret_cast<uint4*>(Dl + o) = make_uint4(ll[0], ll[1], ll[2], ll[3]);
     }
-    }   // dw_on
     __syncthreads();   // exchange buffer of chunk c complete (and the slab consumed)
 
     // ---- project: output rows q = wave QPW + i, three MFMAs per product
@@ -349,7 +290,7 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       for (int t = 0; t < G::NCT; ++t) acc[i][t] = mfma3(pah[t], pal[t], bh, bl, acc[i][t]);
     }
     if (c + 1 < G::NCH) load_p(c + 1);
-    if constexpr (SPEF_MX_ALIAS) __syncthreads();   // exchange reads done before the next expand overlays them
+    __syncthreads();   // exchange reads done before the next expand overlays them
   }
 
   // ---- epilogue: + residual (fp16 block input, added after the BN bias, pytorch_layers.py:93-96)
@@ -365,13 +306,8 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
       if (co >= COUT) continue;
       f32x4 v = acc[i][t];
       if constexpr (RES) {
-        if constexpr (IN16) {
-          const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const _Float16*>(X) + pix * CIN + co);
-          v[0] += h_lo(r.x); v[1] += h_hi(r.x); v[2] += h_lo(r.y); v[3] += h_hi(r.y);
-        } else {
-          const float4 r = *reinterpret_cast<const float4*>(reinterpret_cast<const float*>(X) + pix * CIN + co);
-          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
-        }
+        const uint2 r = *reinterpret_cast<const uint2*>(reinterpret_cast<const _Float16*>(X) + pix * CIN + co);
+        v[0] += h_lo(r.x); v[1] += h_hi(r.x); v[2] += h_lo(r.y); v[3] += h_hi(r.y);
       }
       if constexpr (OUT16)
         *reinterpret_cast<uint2*>(reinterpret_cast<_Float16*>(Y) + pix * COUT + co) =
@@ -404,33 +340,15 @@ static hipError_t mx_go(const void* x, const void* we, const float* be, const fl
   return hipGetLastError();
 }
 
-// (cin, hidden, cout, stride, residual, fp16 input, fp16 output, tile rows): blocks 2-7 of MobileNet-V2
+// (cin, hidden, cout, stride, residual, fp16 input, fp16 output, tile rows): blocks 2-4 of MobileNet-V2
 // (mobilenet_v2.py:240-249) in the fp16mx schedule -- fp16 block outputs for blocks 1-3 (the 256^2 / 128^2 maps),
-// fp32 from block 4 on; the output tile is TH x 16.
-#ifndef SPEF_MX_TH_S2
-#define SPEF_MX_TH_S2 8
-#endif
-#ifndef SPEF_MX_TH_S1
-#define SPEF_MX_TH_S1 16
-#endif
-// Blocks 5-7 keep an fp32 hidden tensor (the fp16x2 slab kernel, k_x2.hip): their fp16 hidden storage would add 31 % to
-// the schedule's logit error variance (tools/precision_budget.py: rms 1.21e-4 -> 1.46e-4 on the parity tests' frames)
-// for 32 us of a ~1.3 ms step. (SPEF_MX_LATE_HIDDEN16 = 1 puts them on this kernel: the fp32-input path below.)
-#ifndef SPEF_MX_LATE_HIDDEN16
-#define SPEF_MX_LATE_HIDDEN16 0
-#endif
-#if SPEF_MX_LATE_HIDDEN16
-#define SPEF_MX_LATE(X)                                                 \
-  X(32, 192, 32, 1, true, false, false, SPEF_MX_TH_S1)   /* 5-6 */   \
-  X(32, 192, 64, 2, false, false, false, SPEF_MX_TH_S2)  /* 7 */
-#else
-#define SPEF_MX_LATE(X)
-#endif
-#define SPEF_MX_TABLE(X)                                            \
-  X(16, 96, 24, 2, false, true, true, SPEF_MX_TH_S2)     /* 2 */     \
-  X(24, 144, 24, 1, true, true, true, SPEF_MX_TH_S1)     /* 3 */     \
-  X(24, 144, 32, 2, false, true, false, SPEF_MX_TH_S2)   /* 4 */     \
-  SPEF_MX_LATE(X)
+// fp32 from block 4 on; the output tile is TH x 16. Blocks 5-7 keep an fp32 hidden tensor (the fp16x2 slab kernel,
+// k_x2.hip): their fp16 hidden storage would add 31 % to the schedule's logit error variance
+// (tools/precision_budget.py: rms 1.21e-4 -> 1.46e-4 on the parity tests' frames) for 32 us of a ~1.3 ms step.
+#define SPEF_MX_TABLE(X)                                \
+  X(16, 96, 24, 2, false, true, true, 8)     /* 2 */     \
+  X(24, 144, 24, 1, true, true, true, 16)    /* 3 */     \
+  X(24, 144, 32, 2, false, true, false, 8)   /* 4 */
 
 bool mx_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res, bool in16, bool out16) {
 #define SPEF_MX_HAS(CI, HI, CO, ST, RS, I16, O16, TH_)                                                   \
@@ -483,11 +401,7 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
   __shared__ __attribute__((aligned(16))) uint8_t In[IH * IRS];
   __shared__ __attribute__((aligned(16))) uint32_t Lr[SH * RSL + 4];
   __shared__ __attribute__((aligned(16))) char Ps[4 * RSB];
-#if SPEF_MX_FRONT_F32W
   __shared__ __attribute__((aligned(16))) float Sw[9 * 32];          // dw weights fp32 [kx][ky][32] (exact)
-#else
-  __shared__ __attribute__((aligned(16))) uint32_t Sv[2][3 * 64];   // dw weight pairs [hi|lo][kx][(w0,w1)|(w1,w2)][32]
-#endif
   __shared__ __attribute__((aligned(16))) float Sb[32];
 
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
@@ -529,18 +443,10 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
         }
       }
     }
-    // dw weight pairs: the last wave's threads 0..47 (kx = t / 16, pair (ky, ky+1), ky = (t / 8) % 2, 4 channels)
+    // dw weights: the last wave's threads 0..71 (tap vt / 8, channels 4 (vt % 8))
     const int vt = NW * 64 - 1 - tid;
-    float4 wa = make_float4(0.f, 0.f, 0.f, 0.f), wb = wa;
-#if SPEF_MX_FRONT_F32W
-    if (vt < 72) wa = *reinterpret_cast<const float4*>(Wd + 4 * vt);   // [ky*3+kx][32]: tap vt / 8, channels 4 (vt % 8)
-#else
-    if (vt < 48) {
-      const int kx = vt >> 4, ky = (vt >> 3) & 1, ch = 4 * (vt & 7);
-      wa = *reinterpret_cast<const float4*>(Wd + (ky * 3 + kx) * 32 + ch);
-      wb = *reinterpret_cast<const float4*>(Wd + ((ky + 1) * 3 + kx) * 32 + ch);
-    }
-#endif
+    float4 wa = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (vt < 72) wa = *reinterpret_cast<const float4*>(Wd + 4 * vt);   // [ky*3+kx][32]
     if (fast) {
       static_assert(TW == 16, "fast-path byte phase assumes 16-wide tiles");
 #pragma unroll
@@ -582,26 +488,10 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
         }
       }
     }
-#if SPEF_MX_FRONT_F32W
     if (vt < 72) {   // -> [kx][ky][32]
       const int tap = vt >> 3, ky = tap / 3, kx = tap - 3 * ky;
       *reinterpret_cast<float4*>(&Sw[(kx * 3 + ky) * 32 + 4 * (vt & 7)]) = wa;
     }
-#else
-    if (vt < 48) {   // hi / lo split of the fp32 weights, packed as (ky, ky + 1) fp16 pairs
-      const int kx = vt >> 4, ky = (vt >> 3) & 1;
-      const float xa[4] = {wa.x, wa.y, wa.z, wa.w}, xb[4] = {wb.x, wb.y, wb.z, wb.w};
-      uint32_t ph[4], pl[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const _Float16 ha = (_Float16)xa[e], hb = (_Float16)xb[e];
-        ph[e] = pack_h2(ha, hb);
-        pl[e] = pack_h2((_Float16)(xa[e] - (float)ha), (_Float16)(xb[e] - (float)hb));
-      }
-      *reinterpret_cast<uint4*>(&Sv[0][kx * 64 + ky * 32 + 4 * (vt & 7)]) = make_uint4(ph[0], ph[1], ph[2], ph[3]);
-      *reinterpret_cast<uint4*>(&Sv[1][kx * 64 + ky * 32 + 4 * (vt & 7)]) = make_uint4(pl[0], pl[1], pl[2], pl[3]);
-    }
-#endif
     if (tid < 32) Sb[tid] = bd[tid];
     if (tid < 4) Lr[SH * RSL + tid] = 0;   // pad dwords read (zero weight) by the last position of the last row
   }
@@ -706,7 +596,6 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
       const uint4 x = *reinterpret_cast<const uint4*>(p), y = *(reinterpret_cast<const uint4*>(p) + 1);
       v[0] = x.x; v[1] = x.y; v[2] = x.z; v[3] = x.w; v[4] = y.x; v[5] = y.y; v[6] = y.z; v[7] = y.w;
     };
-#if SPEF_MX_FRONT_F32W
     // rows oy (a0) and oy + 1 (a1) of column ox: stem rows oy .. oy + 3 are the pairs pc (oy, oy + 1), pn (oy + 2,
     // oy + 3); fp32 weights, one v_fma_mix per tap and channel
 #pragma unroll
@@ -732,27 +621,6 @@ __global__ __launch_bounds__(NW * 64) void front_mx_kernel(
         a1[e] = fmaf(h_hi(pn[e]), w[2][e], a1[e]);
       }
     }
-#else
-#pragma unroll
-    for (int kx = 0; kx < 3; ++kx) {
-      uint32_t pc[8], pn[8];
-      rd8(pbase + kx * 32, pc);
-      rd8(pbase + (SW + kx) * 32, pn);
-#pragma unroll
-      for (int hl = 0; hl < 2; ++hl) {   // the weights' hi, then lo halves
-        uint32_t w01[8], w12[8];
-        rd8(&Sv[hl][kx * 64 + 8 * kg], w01);
-        rd8(&Sv[hl][kx * 64 + 32 + 8 * kg], w12);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) {   // the vertical-pair order of k_front.hip's block 1
-          a1[e] = fmaf(h_hi(pc[e]), h_lo(w01[e]), a1[e]);
-          a0[e] = dot2h(pc[e], w01[e], a0[e]);
-          a0[e] = fmaf(h_lo(pn[e]), h_hi(w12[e]), a0[e]);
-          a1[e] = dot2h(pn[e], w12[e], a1[e]);
-        }
-      }
-    }
-#endif
     f32x4 acc[2] = {f32x4{pb.x, pb.y, pb.z, pb.w}, f32x4{pb.x, pb.y, pb.z, pb.w}};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {

@@ -111,16 +111,10 @@ __device__ __forceinline__ void st_act4(void* p, size_t i, f32x4 v, bool f16) {
 // MI355X_MICROARCH.md (LDS): 24 floats make the 16 consecutive rows of a 16-wide stride-1 pixel tile conflict-free
 // (2-way on 8-wide tiles), 20 floats the stride-2 rows; the plane-1 base is offset to keep the expand's mixed-plane
 // stores conflict-free.
-// XC (channel-split depthwise, below): 20-float rows with the plane-1 base at granule 0 keep the expand's stores
-// conflict-free and its pixel-major reads at most 1.6-way (checked against the lane groups).
-#ifndef SPEF_X2_XC_SSP24   // A/B aid: XC on the pixel-split form's 24-float rows
-#define SPEF_X2_XC_SSP24 0
-#endif
-template <int S, int PINP, bool XC_ = false>
+template <int S, int PINP>
 struct X2Slab {
-  static constexpr bool XC = XC_ && !SPEF_X2_XC_SSP24;
-  static constexpr int SSP = (S == 2 || XC) ? 20 : 24;           // floats per pixel row of a plane
-  static constexpr int TGT = (S == 2 || XC) ? 0 : 1;             // plane-1 base, granules mod 16
+  static constexpr int SSP = S == 2 ? 20 : 24;                   // floats per pixel row of a plane
+  static constexpr int TGT = S == 2 ? 0 : 1;                     // plane-1 base, granules mod 16
   static constexpr int PLANE = PINP * SSP + ((TGT - PINP * SSP / 4) % 16 + 16) % 16 * 4;
   static constexpr int FLOATS = 2 * PLANE;
   static __device__ __forceinline__ int at(int p, int c4) {      // float offset of channels 4 c4 .. 4 c4 + 3 of pixel p
@@ -475,41 +469,32 @@ __global__ __launch_bounds__(NW * 64) __attribute__((
 #ifndef SPEF_X2_STAMP   // timing builds only (outputs overwritten): s_memtime stamps per chunk of one workgroup
 #define SPEF_X2_STAMP 0
 #endif
-#ifndef SPEF_X2_XC   // channel-split depthwise + exchange + lagged project in the role-split kernels
-#define SPEF_X2_XC 0
-#endif
 #ifndef SPEF_X2_GLDS   // stage the role-split kernels' chunk weights by LDS-DMA (global_load_lds) instead of registers
 #define SPEF_X2_GLDS 1
 #endif
 #ifndef SPEF_X2_GLDS_S2   // ... on block 14 (stride 2) too
 #define SPEF_X2_GLDS_S2 1
 #endif
-template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST, int P = 1, int ND_ = 4>
+template <int CIN, int HID, int COUT, int S, int TH, int TW, int WCO, bool PST, int P = 1>
 struct X2wGeom {
-  static constexpr int NE = 4, ND = ND_, NW = NE + ND;
+  static constexpr int NE = 4, ND = 4, NW = NE + ND;
   static constexpr int IH = (TH - 1) * S + 3, IW = (TW - 1) * S + 3;
   static constexpr int PIN = IH * IW, PIN16 = (PIN + 15) / 16, PINP = PIN16 * 16;
   static constexpr int CINP = (CIN + 31) / 32 * 32, KS = CINP / 32;
   static constexpr int WES = CINP + 16;                 // staged expand row (halves): 2 mod 4 granules
   static constexpr int WPS = 48;                        // staged project row (halves, 32 used)
-  // XC: the depthwise waves own a channel group each for every pixel of the tile (wave-uniform weights from scalar
-  // loads) and hand the hi / lo depthwise outputs to the project through an exchange buffer, one chunk behind
-  static constexpr bool XC = SPEF_X2_XC && PST && WCO == 1 && S == 1 && P == 1 && ND == 4;
-  using SL = X2Slab<S, PINP, XC>;
+  using SL = X2Slab<S, PINP>;
   static constexpr int NCH = (HID + 31) / 32, HIDP = NCH * 32;
   static constexpr int NCL = NCH / P;                   // chunks of this workgroup's hidden part
   static constexpr int NCT = (COUT + 15) / 16, NPC = NCT * 16;
   static constexpr int POUT16 = TH * TW / 16;
-  static constexpr int POUT = TH * TW, PPX = POUT / 64;   // XC: output pixels per depthwise lane
-  static constexpr int CTW = (NCT + 3) / 4;               // XC: output-channel tiles per depthwise wave
-  static constexpr int XPL = POUT * 96 + 32;              // XC: one exchange plane (96-B pixel rows, 16-B skew)
   static constexpr int WP = ND / WCO, QPW = POUT16 / WP, NCTW = NCT / WCO;
   static constexpr int EPT = (PIN16 + NE - 1) / NE;     // expand pixel tiles per expand wave
   // LDS: slabs | expand stage [2] | depthwise stage [2] | project stage [2]
   static constexpr int SLAB_B = SL::FLOATS * 4;
   static constexpr int SE_B = 2 * 32 * WES * 2 + 32 * 4;   // hi / lo weight planes + expand bias
-  static constexpr int SD_B = XC ? 0 : (9 * 32 + 32) * 4;   // depthwise weights [9][32] + depthwise bias
-  static constexpr int SP_B = (PST && !XC) ? 2 * NPC * WPS * 2 : 0;
+  static constexpr int SD_B = (9 * 32 + 32) * 4;        // depthwise weights [9][32] + depthwise bias
+  static constexpr int SP_B = PST ? 2 * NPC * WPS * 2 : 0;
   // LDS-DMA staging (GL): every stage region a whole number of 1-KiB wave-instruction pieces (a piece writes 64 x 16 B
   // lane-linearly); per buffer the depthwise and project stages are one contiguous region. Interleaved A/B at B = 64:
   // blocks 14 and 15-16 -2 / -5 us per step, block 17 +3, blocks 8-13 no gain (same box, interleaved), so the
@@ -524,11 +509,10 @@ struct X2wGeom {
   static constexpr int OFF_SD = GL ? OFF_SE + 2 * SE_BQ : OFF_SE + 2 * SE_B;
   static constexpr int OFF_SP = GL ? OFF_SD + SD_BQ : OFF_SD + 2 * SD_B;
   static constexpr int OFF_TR = GL ? OFF_SD + 2 * DP_BQ : OFF_SP + 2 * SP_B;   // dummy rows: invalid pixels' stores
-  static constexpr int OFF_XC = OFF_TR + 16 * 24 * 4;     // XC: exchange [buffer][hi | lo] planes
-  static constexpr int OFF_ST = OFF_XC + (XC ? 4 * XPL : 0);   // SPEF_X2_STAMP: per-chunk clock stamps
+  static constexpr int OFF_ST = OFF_TR + 16 * 24 * 4;     // SPEF_X2_STAMP: per-chunk clock stamps
   static constexpr int LDS_BYTES = OFF_ST + (SPEF_X2_STAMP ? 8 * 4 * 64 : 0);
   // 16-B stage pieces per chunk
-  static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = XC ? 0 : 9 * 8 + 8, NPP = (PST && !XC) ? 2 * NPC * 4 : 0;
+  static constexpr int NPE = 2 * 32 * (CINP / 8) + 8, NPD = 9 * 8 + 8, NPP = PST ? 2 * NPC * 4 : 0;
   static constexpr int NPIECE = (NPE + NPD + NPP + NE * 64 - 1) / (NE * 64);
   static_assert(CIN % 8 == 0 && COUT % 4 == 0 && HID % 8 == 0, "channel counts");
   static_assert(TH * TW % 16 == 0 && POUT16 % WP == 0 && ND % WCO == 0 && NCT % WCO == 0, "tile split");
@@ -537,9 +521,6 @@ struct X2wGeom {
   static_assert(LDS_BYTES <= 163840, "LDS budget");
 };
 
-#ifndef SPEF_X2_ABL_STAGE
-#define SPEF_X2_ABL_STAGE 0
-#endif
 // P > 1 (hidden split): the P workgroups of a tile each run NCH / P consecutive hidden chunks and store their
 // project partial sums (no bias, no residual) to Y + part * pstride; x2_split_reduce_kernel adds the P parts in order,
 // the bias and the residual. Small maps get P times the workgroups while every workgroup streams only 1 / P of the
@@ -550,9 +531,6 @@ struct X2wGeom {
 // reset), so a second tile per CU costs no prologue, epilogue or dispatch gap. Invalid input pixels are stored as
 // zeros by every expand (a pixel valid in one tile may be padding in the next). NCL even: the stage / slab parity of
 // global chunk g is that of its chunk c.
-// ND_ = 8 (kind 4): eight depthwise / project waves, one pixel tile each (three waves per SIMD).
-template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1, bool PT = false,
-          int ND_ = 4>
 // Interleaved A/B at B = 64 (bit-identical): the occupancy target alone blocks 15-16 140 -> 139 us per step; with
 // column batches one column ahead 140 -> 133, block 14 69 -> 66, blocks 8-13 unchanged (their expand role bounds the
 // chunk period); 53.2k -> 53.5k img/s.
@@ -568,22 +546,16 @@ template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, 
 #ifndef SPEF_X2_DWB2_CIN
 #define SPEF_X2_DWB2_CIN 96
 #endif
-#ifndef SPEF_X2W_WPE   // occupancy target of the role-split kernels (one 8-wave workgroup per CU: 2 waves per SIMD)
-#define SPEF_X2W_WPE 2
-#endif
-#if SPEF_X2W_WPE   // (one workgroup of 4 + ND_ waves per CU)
-#define SPEF_X2W_ATTR __attribute__((amdgpu_waves_per_eu((4 + ND_) / 4, (4 + ND_) / 4)))
-#else
-#define SPEF_X2W_ATTR
-#endif
-__global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
+// occupancy target: one 8-wave workgroup per CU = 2 waves per SIMD (the VGPR budget is held to it)
+template <int CIN, int HID, int COUT, int S, int TH, int TW, bool RES, int WCO, bool PST, int P = 1, bool PT = false>
+__global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void x2_irw_kernel(
     const float* __restrict__ X, const _Float16* __restrict__ We, const float* __restrict__ be,
     const float* __restrict__ Wd, const float* __restrict__ bd, const _Float16* __restrict__ Wp,
     const float* __restrict__ bp, float* __restrict__ Y, int H, int W, int OH, int OW, int tiles_x, int tiles_y,
     uint32_t nwg, size_t pstride, uint32_t ntile) {
-  using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST, P, ND_>;
+  using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, PST, P>;
   using SL = typename G::SL;
-  static_assert(!PT || (P == 1 && G::NCL % 2 == 0 && !G::XC), "persistent tiles: one hidden part, even chunk count");
+  static_assert(!PT || (P == 1 && G::NCL % 2 == 0), "persistent tiles: one hidden part, even chunk count");
   extern __shared__ __attribute__((aligned(16))) char smem[];
   const int tid = threadIdx.x, wave = tid >> 6, lane = tid & 63;
   const int r16 = lane & 15, kg = lane >> 4;
@@ -907,7 +879,6 @@ __global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
     } else {
     uint4 v[G::NPIECE];
     auto load_stage = [&](int c) {
-#if SPEF_X2_ABL_STAGE < 2   // timing ablation only (wrong results): 2 = no stage loads
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
         const void* src;
@@ -915,10 +886,8 @@ __global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
         piece(tid + G::NE * 64 * i, kmod(c + 2), kmod(c + 1), src, dst);
         v[i] = src ? *reinterpret_cast<const uint4*>(src) : make_uint4(0, 0, 0, 0);
       }
-#endif
     };
     auto store_stage = [&](int c) {
-#if SPEF_X2_ABL_STAGE < 1   // timing ablation only (wrong results): 1 = no stage stores
 #pragma unroll
       for (int i = 0; i < G::NPIECE; ++i) {
         const void* src;
@@ -926,7 +895,6 @@ __global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
         piece(tid + G::NE * 64 * i, kmod(c + 2), kmod(c + 1), src, dst);
         if (src) *reinterpret_cast<uint4*>(dst) = v[i];
       }
-#endif
     };
     load_stage(0);
     __syncthreads();                 // prologue stages visible
@@ -946,134 +914,6 @@ __global__ __launch_bounds__((4 + ND_) * 64) SPEF_X2W_ATTR void x2_irw_kernel(
       if (wave == 0) stamp(c, 1);
       __syncthreads();
     }
-    }
-  } else if constexpr (G::XC) {
-    // ================= depthwise / project waves, channel-split (XC)
-    // Depthwise: wave d owns channels 8d..8d+7 of each chunk for every output pixel (lane l: pixels l + 64 t); its 72
-    // fp32 weights are wave-uniform (loaded from L2 per chunk, no LDS stage); the ReLU'd sums go to the exchange buffer of the chunk's
-    // parity as hi / lo fp16 (pixel o at byte o * 96 + 16 ((o >> 4) & 1) + 16 d: conflict-free for these pixel-major
-    // stores and for the fragment reads below). Project: wave d takes output-channel tiles d, d + 4, ... of every pixel
-    // tile, one chunk behind the depthwise (its B fragments from the exchange buffer written before the last barrier,
-    // its A fragments from L2 one chunk ahead), so no barrier is added. Same operations per output as the pixel-split
-    // form (fp32 depthwise in kx / ky order, hi / lo split, three MFMAs per product), in the same order.
-    const int d = __builtin_amdgcn_readfirstlane(wave - G::NE);
-    int pin[G::PPX];
-#pragma unroll
-    for (int t = 0; t < G::PPX; ++t) {
-      const int o = lane + 64 * t;
-      pin[t] = (o / TW) * G::IW + (o % TW);
-    }
-    f32x4 acc[G::CTW][G::POUT16];
-#pragma unroll
-    for (int j = 0; j < G::CTW; ++j) {
-      float4 bb = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (d + 4 * j < G::NCT) bb = *reinterpret_cast<const float4*>(bp + (d + 4 * j) * 16 + 4 * kg);
-#pragma unroll
-      for (int q = 0; q < G::POUT16; ++q) acc[j][q] = f32x4{bb.x, bb.y, bb.z, bb.w};
-    }
-    const _Float16* WpLo = Wp + (size_t)G::NPC * G::HIDP;
-    f16x8 pgh[G::CTW], pgl[G::CTW];
-    auto load_pg = [&](int k) {
-#pragma unroll
-      for (int j = 0; j < G::CTW; ++j)
-        if (d + 4 * j < G::NCT) {
-          const size_t off = (size_t)((d + 4 * j) * 16 + r16) * G::HIDP + 32 * (cb + k) + 8 * kg;
-          pgh[j] = *reinterpret_cast<const f16x8*>(Wp + off);
-          pgl[j] = *reinterpret_cast<const f16x8*>(WpLo + off);
-        }
-    };
-    char* Xc = smem + G::OFF_XC;   // [chunk parity][hi | lo] planes
-    auto xoff = [](int o) { return o * 96 + ((o >> 4) & 1) * 16; };
-    auto project = [&](int k) {
-      const char* Xh = Xc + (k & 1) * 2 * G::XPL;
-      const char* Xl = Xh + G::XPL;
-#pragma unroll
-      for (int q = 0; q < G::POUT16; ++q) {
-        const int o = 16 * q + r16;
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(Xh + xoff(o) + 16 * kg);
-        const f16x8 bl = *reinterpret_cast<const f16x8*>(Xl + xoff(o) + 16 * kg);
-#pragma unroll
-        for (int j = 0; j < G::CTW; ++j)
-          if (d + 4 * j < G::NCT) acc[j][q] = mfma_x2(pgh[j], pgl[j], bh, bl, acc[j][q]);
-      }
-    };
-    load_pg(0);
-    __syncthreads();
-    __syncthreads();
-#pragma unroll 1
-    for (int c = 0; c < G::NCL; ++c) {
-      if (wave == G::NE) stamp(c, 4);
-      // this chunk's 72 weights + 8 biases as vector loads (a uniform address through the lane-varying wave index:
-      // scalar loads share lgkmcnt with the LDS reads, and their lgkmcnt(0) waits serialised the depthwise), issued
-      // before the lagged project so its MFMAs cover their latency
-      const int dv = wave - G::NE;
-      const float* wdc = Wd + 32 * (cb + c) + 8 * dv;
-      float4 wv[9][2];
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        wv[tap][0] = *reinterpret_cast<const float4*>(wdc + tap * G::HIDP);
-        wv[tap][1] = *reinterpret_cast<const float4*>(wdc + tap * G::HIDP + 4);
-      }
-      const float4 bv0 = *reinterpret_cast<const float4*>(bd + 32 * (cb + c) + 8 * dv);
-      const float4 bv1 = *reinterpret_cast<const float4*>(bd + 32 * (cb + c) + 8 * dv + 4);
-      if (c >= 1) {
-        project(c - 1);   // chunk c - 1: its exchange buffer is complete (last barrier)
-        load_pg(c);       // chunk c's fragments, used after the next barrier
-      }
-      const float* Sl = slab(c & 1);
-      f32x2 a[G::PPX][4];
-#pragma unroll
-      for (int t = 0; t < G::PPX; ++t) {
-        a[t][0] = f32x2{bv0.x, bv0.y}; a[t][1] = f32x2{bv0.z, bv0.w};
-        a[t][2] = f32x2{bv1.x, bv1.y}; a[t][3] = f32x2{bv1.z, bv1.w};
-      }
-#pragma unroll
-      for (int kx = 0; kx < 3; ++kx)
-#pragma unroll
-        for (int ky = 0; ky < 3; ++ky) {
-          const float4 w0 = wv[ky * 3 + kx][0], w1 = wv[ky * 3 + kx][1];
-          const f32x2 w4[4] = {f32x2{w0.x, w0.y}, f32x2{w0.z, w0.w}, f32x2{w1.x, w1.y}, f32x2{w1.z, w1.w}};
-#pragma unroll
-          for (int t = 0; t < G::PPX; ++t) {
-            const int p = pin[t] + ky * G::IW + kx;
-            dw_tap8(a[t], *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * d)),
-                    *reinterpret_cast<const float4*>(Sl + SL::at(p, 2 * d + 1)), w4);
-          }
-        }
-      {
-        char* Xh = Xc + (c & 1) * 2 * G::XPL;
-        char* Xl = Xh + G::XPL;
-#pragma unroll
-        for (int t = 0; t < G::PPX; ++t) {
-          f16x8 bh, bl;
-          relu_split8(a[t], bh, bl);
-          const int o = lane + 64 * t;
-          *reinterpret_cast<f16x8*>(Xh + xoff(o) + 16 * d) = bh;
-          *reinterpret_cast<f16x8*>(Xl + xoff(o) + 16 * d) = bl;
-        }
-      }
-      if (wave == G::NE) stamp(c, 6);
-      __syncthreads();
-    }
-    project(G::NCL - 1);
-    // epilogue: + residual (fp32 block input) -> fp32 NHWC
-#pragma unroll
-    for (int q = 0; q < G::POUT16; ++q) {
-      const int o = 16 * q + r16;
-      const int gy = oy0 + o / TW, gx = ox0 + o % TW;
-      if (gy >= OH || gx >= OW) continue;
-      const size_t pix = ((size_t)b * OH + gy) * OW + gx;
-#pragma unroll
-      for (int j = 0; j < G::CTW; ++j) {
-        const int co = (d + 4 * j) * 16 + 4 * kg;
-        if (d + 4 * j >= G::NCT || co >= COUT) continue;
-        f32x4 v = acc[j][q];
-        if constexpr (RES) {
-          const float4 r = *reinterpret_cast<const float4*>(X + pix * CIN + co);
-          v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
-        }
-        *reinterpret_cast<float4*>(Y + pix * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
-      }
     }
   } else {
     // ================= depthwise / project waves
@@ -1329,33 +1169,13 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
 // (8x8, g 2) -> 125 (8x16, g 2) -> 89 us (8x16, g 1); blocks 15-16 93 -> 91 us (g 2 -> 1); block 17 142 us at g 4,
 // 125 at g 2, 322 at g 1 (80 accumulator registers per wave: spills). URSONet step 2.11 -> 1.85 ms, keypoint mode
 // 1.27 -> 1.05 ms (with the small-map table below).
-// Blocks 8-13. SPEF_X2_MID8 = 1: 8 x 8 tiles with the project weights from L2 (kind 2): 68-76 KB of LDS, two
-// workgroups per CU, against 8 x 16 tiles with LDS-staged project weights at 123-144 KB (one per CU).
-#ifndef SPEF_X2_MID8
-#define SPEF_X2_MID8 0
-#endif
 // Kind 3 = kind 1 with persistent tiles (x2_irw_kernel's PT: a second tile per CU streams on without a prologue):
-// the maps with more tiles than CUs at 512^2 (blocks 8-14: 512 tiles at B = 64).
-#ifndef SPEF_X2_PERSIST
-#define SPEF_X2_PERSIST 1
-#endif
-#define SPEF_X2_PK (SPEF_X2_PERSIST ? 3 : 1)
-#ifndef SPEF_X2_ND8   // eight depthwise / project waves (kind 4): 1 = blocks 8-11, 2 = blocks 8-13 (12-13 spill);
-#define SPEF_X2_ND8 0   // measured at 1: blocks 8-10 142 -> 145 us per step, block 11 unchanged (off)
-#endif
-#define SPEF_X2_PK8 (SPEF_X2_ND8 && SPEF_X2_PERSIST ? 4 : SPEF_X2_PK)
-#define SPEF_X2_PK8B (SPEF_X2_ND8 >= 2 && SPEF_X2_PERSIST ? 4 : SPEF_X2_PK)
-#if SPEF_X2_MID8
+// the maps with more tiles than CUs at 512^2 (blocks 8-14: 512 tiles at B = 64). Blocks 8-13 run 8 x 16 tiles with
+// LDS-staged project weights at 123-144 KB (one workgroup per CU).
 #define SPEF_X2_MID(X)                                           \
-  X(64, 384, 64, 1, true, true, 8, 8, 8, 1, 2)      /* 8-10 */   \
-  X(64, 384, 96, 1, true, false, 8, 8, 8, 1, 2)     /* 11 */     \
-  X(96, 576, 96, 1, true, true, 8, 8, 8, 1, 2)      /* 12-13 */
-#else
-#define SPEF_X2_MID(X)                                           \
-  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK8)     /* 8-10 */   \
-  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, SPEF_X2_PK8)    /* 11 */     \
-  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, SPEF_X2_PK8B)    /* 12-13 */
-#endif
+  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, 3)      /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, 3)     /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, 3)      /* 12-13 */
 #define SPEF_X2_TABLE(X)                                         \
   X(32, 32, 16, 1, false, false, 8, 16, 4, 1, 0)    /* 1 */      \
   X(16, 96, 24, 2, true, false, 8, 8, 4, 1, 0)      /* 2 */      \
@@ -1364,7 +1184,7 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(32, 192, 32, 1, true, true, 8, 16, 4, 1, 0)     /* 5-6 */    \
   X(32, 192, 64, 2, true, false, 8, 8, 4, 1, 0)     /* 7 */      \
   SPEF_X2_MID(X)                                                 \
-  X(96, 576, 160, 2, true, false, 4, 8, 8, 2, SPEF_X2_PK)    /* 14 */     \
+  X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 3)     /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
 // 16x16 tiles with 8 waves (2 workgroups per CU) where they tile the map exactly: block 3 at 512^2 (interleaved A/B,
@@ -1376,9 +1196,6 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
 // Maps whose primary tiling leaves CUs idle (fewer workgroups than CUs; the role-split kernels run one workgroup
 // per CU): blocks 15-17 at 240x384 (8x12 maps: 128 workgroups of 8x8 at B = 64) split the hidden dimension over P
 // workgroups per tile (last field; partial sums joined by x2_split_reduce_kernel in the caller's scratch).
-#ifndef SPEF_X2_SMALL_ALWAYS   // A/B aid: the hidden split on every map size
-#define SPEF_X2_SMALL_ALWAYS 0
-#endif
 #define SPEF_X2_SMALL_TABLE(X)                                      \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 1, 2)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2, 2)   /* 17 */
@@ -1414,10 +1231,9 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
                                         tiles_x, tiles_y, nwg);
   } else if constexpr (IO == 0) {
     static_assert(EXPAND && NW == 8, "role-split blocks expand, 4 + 4 waves");
-    constexpr bool PT = KIND >= 3 && P == 1;   // persistent tiles (kind 3, 4): ceil(tiles / CUs) tiles per workgroup
-    constexpr int ND = KIND == 4 ? 8 : 4;
-    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND != 2, P, ND>;
-    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND != 2, P, PT, ND>;
+    constexpr bool PT = KIND == 3 && P == 1;   // persistent tiles (kind 3): ceil(tiles / CUs) tiles per workgroup
+    using G = X2wGeom<CIN, HID, COUT, S, TH, TW, WCO, KIND != 2, P>;
+    auto k = x2_irw_kernel<CIN, HID, COUT, S, TH, TW, RES, WCO, KIND != 2, P, PT>;
     if (!attr_set.done()) {
       hipError_t e = x2_set_lds(k, G::LDS_BYTES);
       if (e != hipSuccess) return e;
@@ -1477,7 +1293,7 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
 #define SPEF_X2_TILES(TH_, TW_) ((int64_t)((OW + (TW_)-1) / (TW_)) * ((OH + (TH_)-1) / (TH_)) * B)
 #define SPEF_X2_SMALL(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_)                                    \
   if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && scratch && !io &&  \
-      (SPEF_X2_SMALL_ALWAYS || (SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)))     \
+      SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)                                \
     return x2_irb_go<CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_>(x, we, be, wd, bd, wp, bp, y, B, H, W, OH, \
                                                                          OW, s, scratch, num_cu);
   SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
