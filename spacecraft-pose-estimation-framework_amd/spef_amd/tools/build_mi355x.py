@@ -20,6 +20,11 @@ spe_finn.py:116-149 statistics, tools/compare.py) and, when the caller passes th
 Needs a GPU; skipped (with a note in build.json) when none is visible. Keypoint experiments asking for fp16 or
 fp16mx (the default) get the fp16x2 blob: EPnP amplifies keypoint error (test_gpu_keypoints.py), and the fp16
 keypoint head exceeds the 1e-3 output bound.
+
+The build refuses to ship a floating-point blob that misses the north star's bound (raw head outputs 1e-3, pose
+0.1 deg / 1 mm) against the fp32 variant on the evaluation frames: it rebuilds as fp16x2 when that variant is within
+the bound (``build.json`` records the ``fallback``), and otherwise exits with status 3 -- unless
+``--allow-out-of-bound`` is given, which keeps the requested blob with a warning (int8 has its own, wider bound).
 """
 from __future__ import annotations
 
@@ -138,6 +143,12 @@ def main(argv=None):
                     help="comma list of fp32,fp16mx,fp16x2,fp16,bf16,int8 to evaluate on the host after the build, 'none', or "
                          "'auto' (all that apply, when a GPU is visible)")
     ap.add_argument('--eval-batches', type=int, default=2)
+    ap.add_argument('--allow-out-of-bound', action='store_true',
+                    help='keep the requested floating-point blob even when it misses the 1e-3 / 0.1 deg / 1 mm bound '
+                         'against the fp32 variant (default: fall back to fp16x2, or fail)')
+    ap.add_argument('--synthetic-head-std', type=float, default=None,
+                    help='--synthetic: orientation Linear init std (default: the reference init, 0.01); 0.3 gives the '
+                         'trained-scale heads of the reference-generated predict fixtures')
     a = ap.parse_args(argv)
     import torch
     from ..config import load_config
@@ -162,7 +173,9 @@ def main(argv=None):
                       h.N_POS_BINS_PER_DIM, cfg.DATA.POS_SMOOTH_FACTOR)
         n_ori = su.orientation.n_bins if h.ORI == 'classification' else 4
         n_pos = su.position.n_bins if h.POS == 'classification' else 3
-        sd = synthetic_state_dict(mobilenet_v2('ursonet', n_ori, n_pos), seed=1001)
+        sd = synthetic_state_dict(mobilenet_v2('ursonet', n_ori, n_pos), seed=1001,
+                                  **({} if a.synthetic_head_std is None else
+                                     {'head_std': a.synthetic_head_std, 'pos_std': 0.01, 'pos_bias': (0.3, -0.2, 12.0)}))
         name = 'synthetic'
     else:
         ap.error('--experiment or --synthetic')
@@ -171,9 +184,12 @@ def main(argv=None):
     out = a.out or os.path.join('experiments', 'build', 'mi355x', name)
     calib = synth_frames(cfg.MI355X.CALIB_FRAMES, *cfg.DATA.IMG_SIZE, 900)
     info = build(sd, cfg, out, dtype, calib if dtype == 'int8' else None, bit_width)
+    rc = 0
     if a.eval_variants != 'none':
         variants = (['fp32', 'fp16mx', 'fp16x2', 'fp16', 'bf16'] + ([] if keypoints else ['int8'])) if a.eval_variants == 'auto' else \
             [v for v in a.eval_variants.split(',') if v]
+        if dtype not in ('int8', 'fp32'):   # the bound check needs the fp32 reference, the built dtype and the fallback
+            variants += [v for v in ('fp32', dtype, 'fp16x2') if v not in variants]
         if torch.cuda.is_available():
             from ..arch import arch_from_state_dict
             from ..spe.camera import CAMERAS
@@ -183,15 +199,27 @@ def main(argv=None):
                                                   camera=camera)
             ok = info['eval_host'].get('within_north_star')
             if ok is not None and dtype not in ok and dtype != 'int8':
-                info['warning'] = (f'the built {dtype} blob exceeds the 1e-3 / 0.1 deg / 1 mm bound against the fp32 '
-                                   f'variant on the evaluation frames; variants within it: {ok}')
-                print('warning:', info['warning'], file=sys.stderr)
+                miss = (f'the built {dtype} blob exceeds the 1e-3 / 0.1 deg / 1 mm bound against the fp32 variant on the '
+                        f'evaluation frames ({info["eval_host"]["variants"][dtype]["vs_fp32_variant"]["max_abs"]:.2e} max '
+                        f'|d raw output|); variants within it: {ok}')
+                if a.allow_out_of_bound:
+                    info['warning'] = miss + '; kept (--allow-out-of-bound)'
+                    print('warning:', info['warning'], file=sys.stderr)
+                elif 'fp16x2' in ok:
+                    requested = dtype
+                    info = dict(build(sd, cfg, out, 'fp16x2', None, bit_width), eval_host=info['eval_host'])
+                    info['fallback'] = {'requested': requested, 'built': 'fp16x2', 'reason': miss}
+                    print(f'note: {miss}; rebuilt as fp16x2', file=sys.stderr)
+                else:
+                    info['error'] = miss + '; no variant to fall back to (pass --allow-out-of-bound to keep it)'
+                    print('error:', info['error'], file=sys.stderr)
+                    rc = 3
         else:
             info['eval_host'] = 'skipped: no GPU visible (run the build on the MI355X box to evaluate the variants)'
         with open(os.path.join(out, 'build.json'), 'w') as f:
             json.dump(info, f, indent=1)
     print(json.dumps(info))
-    return 0
+    return rc
 
 
 if __name__ == '__main__':

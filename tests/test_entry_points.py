@@ -113,3 +113,26 @@ def test_build_tool_evaluates_precision_variants(tmp_path):
     assert v['variants']['bf16']['vs_fp32_variant']['max_abs'] < 6e-3          # test_gpu_c2_precision bound
     assert v['variants']['fp16']['vs_fp32_variant']['ori_max_deg'] < 0.1
     assert v['variants']['int8']['vs_fp32_variant']['max_abs'] < 0.05          # INT8_BOUND (bench.py)
+
+
+@pytest.mark.gpu
+def test_build_tool_refuses_out_of_bound_blob(tmp_path):
+    """A trained-scale head (orientation Linear std 0.3) makes the fp16 schedule miss the north star's 1e-3 on the raw
+    head outputs: the build does not ship that blob -- it rebuilds as fp16x2 and records the
+    fallback -- unless --allow-out-of-bound keeps it (with a warning)."""
+    from spef_amd import blob as Bl
+    from spef_amd.tools.build_mi355x import main
+    args = ['--synthetic', '--synthetic-head-std', '0.3', '--dtype', 'fp16', '--eval-variants', 'fp32,fp16,fp16x2',
+            '--eval-batches', '1']
+    out = str(tmp_path / 'a')
+    assert main(args + ['--out', out]) == 0
+    info = json.load(open(os.path.join(out, 'build.json')))
+    assert info['fallback']['requested'] == 'fp16' and info['fallback']['built'] == 'fp16x2', info
+    assert info['dtype'] == 'fp16x2' and Bl.describe(open(os.path.join(out, 'model.spef'), 'rb').read())['dtype'] == 5
+    v = info['eval_host']['variants']
+    assert v['fp16']['vs_fp32_variant']['max_abs'] > 1e-3 and v['fp16x2']['within_north_star']
+    out = str(tmp_path / 'b')
+    assert main(args + ['--out', out, '--allow-out-of-bound']) == 0
+    info = json.load(open(os.path.join(out, 'build.json')))
+    assert 'fallback' not in info and 'warning' in info and info['dtype'] == 'fp16'
+    assert Bl.describe(open(os.path.join(out, 'model.spef'), 'rb').read())['dtype'] == 1

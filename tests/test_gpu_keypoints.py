@@ -216,22 +216,41 @@ def test_stream_pipeline_keypoint_mode_matches_single_engine(kp_sd, golden):
         pipe.close()
 
 
-def test_keypoint_mode_b64_pipeline_vs_oracle(kp_sd, golden):
-    """keypoint mode at the bench workload -- B = 64 synthetic SPEED-style 240 x 384 frames
-    (bench.py's generator), the fp16x2 keypoint blob (build_mi355x's keypoint default), StreamPipeline.submit_keypoints
-    on three streams (forward + sigmoid + batched EPnP) -- against the FP32 oracle forward (oracle/model_ref.py) and
-    the EPnP restatement (oracle/epnp_ref.py) at the north-star bounds: raw outputs 1e-3, orientation < 0.1 deg,
-    position < 1 mm, for every batch of the pipeline. With the random-weight head the keypoints are poorly conditioned
-    for EPnP (their 2-D spread is small), so the 5e-6 raw-output difference becomes up to ~0.95 mm at 3-35 m (measured,
-    printed); the EPnP kernel itself is checked separately on the GPU's own keypoints."""
+def _planted_kp_sd(golden):
+    """Keypoint head whose sigmoid outputs are real keypoints: the head bias is logit() of the reference projection
+    (KeyPoints.project, tests/golden/keypoints.npz) of the valid.json pose at the median distance, and the weights are
+    small (std 2e-4: W . features moves each normalised keypoint by ~1e-2, ~20 px, per frame), so every frame's 11
+    keypoints span the spacecraft's image as in the reference's keypoint mode (keypoints_utils.py:112-174) instead of
+    the clustered, ill-conditioned points of a random head."""
+    g = golden('keypoints.npz')
+    i = int(np.argmin(np.abs(g['t'][:, 2] - np.median(g['t'][:, 2]))))
+    sd = synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=2e-4)
+    k = np.clip(g['kp2d'][i].astype(np.float64), 1e-6, 1 - 1e-6)
+    sd['head.layer.1.bias'] = np.log(k / (1 - k)).astype(np.float32)
+    return sd, g, i
+
+
+def test_keypoint_mode_b64_pipeline_vs_oracle(golden):
+    """keypoint mode at the bench workload -- B = 64 synthetic SPEED-style 240 x 384
+    frames (bench.py's generator), the fp16x2 keypoint blob (build_mi355x's keypoint default), StreamPipeline
+    .submit_keypoints on three streams (forward + sigmoid + batched EPnP) -- against the FP32 oracle forward
+    (oracle/model_ref.py) and the EPnP restatement (oracle/epnp_ref.py) at the north-star bounds (raw outputs 1e-3,
+    orientation < 0.1 deg, position < 1 mm), for every batch of the pipeline, with a head that outputs real keypoints
+    (_planted_kp_sd), so the pose bound is held with margin: the position error must stay under 0.3 mm. The EPnP kernel
+    alone (on the GPU's own keypoints, against the oracle EPnP) is reported and bounded separately."""
     from spef_amd.data.synthetic import synth_frames
     from spef_amd.pipeline import StreamPipeline
-    g = golden('keypoints.npz')
+    sd, g, i = _planted_kp_sd(golden)
     fr = synth_frames(64, 240, 384, 20_000)
     torch.set_num_threads(16)
-    raw_ref = M.forward(M.u8_nhwc_to_nchw_f32(fr), kp_sd, head='keypoints').numpy()
-    rq, rt = E.decode_batch(D.sigmoid_f32(raw_ref), g['kp3d'], g['K'])
-    pipe = StreamPipeline(Bl.pack(kp_sd, mobilenet_v2('keypoints'), dtype='fp16x2'), 'cuda:0', depth=3)
+    raw_ref = M.forward(M.u8_nhwc_to_nchw_f32(fr), sd, head='keypoints').numpy()
+    kp_ref = D.sigmoid_f32(raw_ref)
+    rq, rt = E.decode_batch(kp_ref, g['kp3d'], g['K'])
+    # the planted head gives frames spread around the planted pose (not one degenerate cluster)
+    spread_px = (kp_ref[:, 2::2].max(1) - kp_ref[:, 2::2].min(1)) * float(g['nu'])
+    assert spread_px.min() > 50, spread_px.min()
+    assert D.angle_deg_stable(rq, np.repeat(g['q'][i:i + 1], 64, 0)).max() < 20
+    pipe = StreamPipeline(Bl.pack(sd, mobilenet_v2('keypoints'), dtype='fp16x2'), 'cuda:0', depth=3)
     try:
         pipe.set_keypoints(g['kp3d'], g['K'], float(g['nu']), float(g['nv']))
         pipe.reserve(64, 240, 384)
@@ -248,9 +267,11 @@ def test_keypoint_mode_b64_pipeline_vs_oracle(kp_sd, golden):
             sq, st = E.decode_batch(D.sigmoid_f32(raw), g['kp3d'], g['K'])
             s_ang = D.angle_deg_stable(o['ori'].cpu().numpy().astype(np.float64), sq)
             s_pos = np.linalg.norm(o['pos'].cpu().numpy().astype(np.float64) - st, axis=1)
-            print(f'B=64 keypoint step: raw {d_raw:.2e}, ori max {ang.max():.2e} deg, pos max {dpos.max():.2e} m; '
+            print(f'B=64 keypoint step (pose {i}, z {g["t"][i, 2]:.1f} m, keypoint spread >= {spread_px.min():.0f} px): '
+                  f'raw {d_raw:.2e}, ori max {ang.max():.2e} deg, pos max {dpos.max():.2e} m; '
                   f'EPnP alone {s_ang.max():.2e} deg, {s_pos.max():.2e} m')
             assert d_raw < KP_TOL and ang.max() < 0.1 and dpos.max() < 1e-3
+            assert dpos.max() < 3e-4 and ang.max() < 0.03      # the bound with margin
             assert s_ang.max() < 0.01 and s_pos.max() < 1e-4
     finally:
         pipe.close()
