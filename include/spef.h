@@ -63,7 +63,8 @@ int spef_load_weights_device(spef_ctx* ctx, const void* dev_blob, size_t bytes);
 /* Query the loaded model: head (0 URSONet, 1 keypoints), output widths, storage dtype (1 fp16, 2 bf16, 3 int8,
  * 4 fp32 = the reference's own arithmetic: exact-fp32 MFMA, one kernel per conv; 5 fp16x2 = fp32 activations with
  * hi + lo fp16 MFMA operands, the fp32-accurate fused schedule; 6 fp16mx = the fp16x2 weights and kernels with the
- * block outputs of blocks 1-6 stored fp16: the headline schedule, within 1e-3 of float32 at trained head scales). */
+ * stem map, the block outputs of blocks 1-3 and the hidden tensors of blocks 2-4 stored fp16: the headline schedule,
+ * within 1e-3 of float32 at trained head scales). */
 int spef_model_info(const spef_ctx* ctx, int* head, int* n_out0, int* n_out1, int* dtype, int* n_ops);
 
 /* Allocate activation workspace for batches up to B of H x W frames. Must precede spef_forward for that

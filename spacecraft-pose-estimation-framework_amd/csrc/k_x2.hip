@@ -1243,13 +1243,13 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     }
   };
   if (wave == 0) stamp(0, 3);
-  if (wave == 4) stamp(1, 7);
+  if (wave == G::NE) stamp(1, 7);
 
-  // Stage pieces, all moved by the VALU waves (the MFMA waves' critical path then carries none of it): the expand stage
-  // (weights hi / lo + bias, 1-KiB pieces d + ND j) and the depthwise stage (weights + bias); lane l of piece i fills
-  // slot 64 i + l of the region from src0 + k * kstr at chunk k (pad slots read a valid address of the same tensor).
-  // The first stages go by LDS-DMA; in the loop a chunk's pieces are loaded into registers an iteration before they are
-  // stored (LDS-DMA pieces cost the VALU role ~1.2k cycles of issue per chunk: tools/kstamp_irp.py).
+  // Stage pieces, all moved by LDS-DMA from the VALU waves (the MFMA waves' critical path then carries none of it): the
+  // expand stage (weights hi / lo + bias, 1-KiB pieces d + ND j) and the depthwise stage (weights + bias); lane l of
+  // piece i fills slot 64 i + l of the region from src0 + k * kstr at chunk k (pad slots read a valid address of the
+  // same tensor). Measured per step at B = 64 (tools/ktime.sh): blocks 15-16 with the expand stage issued by the MFMA
+  // waves 102.9 -> 116.6 us, register staging (global loads an iteration ahead + ds_write) instead of LDS-DMA 181 us.
   const bool ewave = wave < G::NE;
   const int wr = ewave ? wave : wave - G::NE;
   constexpr int NJE = (G::NIE + G::ND - 1) / G::ND, NJD = (G::NID + G::ND - 1) / G::ND;
@@ -1294,33 +1294,10 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
                                          (__attribute__((address_space(3))) void*)(base + (wr + G::ND * j) * 1024), 16,
                                          0, 0);
   };
-  uint4 re[NJE], rd[NJD];
-  auto ld_e = [&](int k) {
-#pragma unroll
-    for (int j = 0; j < NJE; ++j)
-      if (wr + G::ND * j < G::NIE) re[j] = *reinterpret_cast<const uint4*>(esrc[j] + (size_t)k * ekstr[j]);
-  };
-  auto st_e = [&](char* base) {
-#pragma unroll
-    for (int j = 0; j < NJE; ++j)
-      if (wr + G::ND * j < G::NIE) *reinterpret_cast<uint4*>(base + ((wr + G::ND * j) * 64 + lane) * 16) = re[j];
-  };
-  auto ld_d = [&](int k) {
-#pragma unroll
-    for (int j = 0; j < NJD; ++j)
-      if (wr + G::ND * j < G::NID) rd[j] = *reinterpret_cast<const uint4*>(dsrc[j] + (size_t)k * 128);
-  };
-  auto st_d = [&](char* base) {
-#pragma unroll
-    for (int j = 0; j < NJD; ++j)
-      if (wr + G::ND * j < G::NID) *reinterpret_cast<uint4*>(base + ((wr + G::ND * j) * 64 + lane) * 16) = rd[j];
-  };
   if (!ewave) {
     dma_e(0, Se0);
     dma_e(1, Se1);
     dma_d(0, Sd0);
-    ld_e(kmod(2));
-    ld_d(kmod(1));
   }
 
   if (ewave) {
@@ -1454,36 +1431,60 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
           pal[t] = *reinterpret_cast<const f16x8*>(WpLo + off);
         }
     };
+    // the B fragments of pixel tile q + 1 are read before tile q's MFMAs (each read pair's LDS latency hides behind
+    // the previous tile's MFMAs instead of stalling the MFMA role)
     auto project = [&](const char* Dh) {
+      f16x8 bh[2], bl[2];
+      bh[0] = *reinterpret_cast<const f16x8*>(Dh + r16 * 64 + dsx);
+      bl[0] = *reinterpret_cast<const f16x8*>(Dh + G::DS_PL + r16 * 64 + dsx);
 #pragma unroll
       for (int q = 0; q < G::POUT16; ++q) {
-        const f16x8 bh = *reinterpret_cast<const f16x8*>(Dh + (q * 16 + r16) * 64 + dsx);
-        const f16x8 bl = *reinterpret_cast<const f16x8*>(Dh + G::DS_PL + (q * 16 + r16) * 64 + dsx);
+        if (q + 1 < G::POUT16) {
+          bh[(q + 1) & 1] = *reinterpret_cast<const f16x8*>(Dh + ((q + 1) * 16 + r16) * 64 + dsx);
+          bl[(q + 1) & 1] = *reinterpret_cast<const f16x8*>(Dh + G::DS_PL + ((q + 1) * 16 + r16) * 64 + dsx);
+        }
 #pragma unroll
         for (int t = 0; t < G::NCTW; ++t)
-          if (e + G::NE * t < G::NCT) acc[q][t] = mfma_x2(pah[t], pal[t], bh, bl, acc[q][t]);
+          if (e + G::NE * t < G::NCT) acc[q][t] = mfma_x2(pah[t], pal[t], bh[q & 1], bl[q & 1], acc[q][t]);
       }
     };
-    // + residual (the block input, pytorch_layers.py:93-96, added after the BN bias) -> fp32 NHWC, tile t
+    // + residual (the block input, pytorch_layers.py:93-96, added after the BN bias) -> fp32 NHWC, tile t; the residual
+    // loads of four pixel tiles are issued together (one memory round trip per group, not per value)
     auto epilogue = [&](int t) {
       int b_, oy_, ox_;
       tile_of(t, b_, oy_, ox_);
+      constexpr int QG = G::POUT16 < 4 ? G::POUT16 : 4;
 #pragma unroll
-      for (int q = 0; q < G::POUT16; ++q) {
-        const int o = q * 16 + r16;
-        const int gy = oy_ + o / TW, gx = ox_ + o % TW;
-        if (gy >= OH || gx >= OW) continue;
-        const size_t pix_ = ((size_t)b_ * OH + gy) * OW + gx;
+      for (int q0 = 0; q0 < G::POUT16; q0 += QG) {
+        float4 r[QG][G::NCTW];
+        size_t pix_[QG];
+        bool in[QG];
 #pragma unroll
-        for (int tt = 0; tt < G::NCTW; ++tt) {
-          if (e + G::NE * tt >= G::NCT) continue;
-          const int co = (e + G::NE * tt) * 16 + 4 * kg;
-          f32x4 v = acc[q][tt];
-          if constexpr (RES) {
-            const float4 r = *reinterpret_cast<const float4*>(X + pix_ * CIN + co);
-            v[0] += r.x; v[1] += r.y; v[2] += r.z; v[3] += r.w;
+        for (int qq = 0; qq < QG; ++qq) {
+          const int o = (q0 + qq) * 16 + r16;
+          const int gy = oy_ + o / TW, gx = ox_ + o % TW;
+          in[qq] = gy < OH && gx < OW;
+          pix_[qq] = ((size_t)b_ * OH + gy) * OW + gx;
+#pragma unroll
+          for (int tt = 0; tt < G::NCTW; ++tt) {
+            r[qq][tt] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (RES && in[qq] && e + G::NE * tt < G::NCT)
+              r[qq][tt] = *reinterpret_cast<const float4*>(X + pix_[qq] * CIN + (e + G::NE * tt) * 16 + 4 * kg);
           }
-          *reinterpret_cast<float4*>(Y + pix_ * COUT + co) = make_float4(v[0], v[1], v[2], v[3]);
+        }
+#pragma unroll
+        for (int qq = 0; qq < QG; ++qq) {
+          if (!in[qq]) continue;
+#pragma unroll
+          for (int tt = 0; tt < G::NCTW; ++tt) {
+            if (e + G::NE * tt >= G::NCT) continue;
+            f32x4 v = acc[q0 + qq][tt];
+            if constexpr (RES) {
+              v[0] += r[qq][tt].x; v[1] += r[qq][tt].y; v[2] += r[qq][tt].z; v[3] += r[qq][tt].w;
+            }
+            *reinterpret_cast<float4*>(Y + pix_[qq] * COUT + (e + G::NE * tt) * 16 + 4 * kg) =
+                make_float4(v[0], v[1], v[2], v[3]);
+          }
         }
       }
     };
@@ -1505,8 +1506,8 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
           epilogue((g - 1) / G::NCH);
           init_acc();
         }
-        load_pa(kmod(g));
       }
+      if (g >= 1) load_pa(kmod(g));
       if (wave == 0) stamp(g, 1);
       if (g + 1 < GT) {
         if (PT && kmod(g + 1) == 0) split_mask((g + 1) / G::NCH);
@@ -1541,11 +1542,9 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     // expand chunk g + 3 and depthwise chunk g + 2; V(g) from slab p and stage p into Ds[p]
     auto iter = [&](auto par, int g) {
       using Q = std::integral_constant<int, decltype(par)::value ^ 1>;
-      if (wave == 4) stamp(g, 4);
-      if (g + 2 < GT) st_e(se(par));
-      if (g + 1 < GT) st_d(sd(Q{}));
-      if (g + 3 < GT) ld_e(kmod(g + 3));
-      if (g + 2 < GT) ld_d(kmod(g + 2));
+      if (wave == G::NE) stamp(g, 4);
+      if (g + 2 < GT) dma_e(kmod(g + 2), se(par));
+      if (g + 1 < GT) dma_d(kmod(g + 1), sd(Q{}));
       const float* Sl = slab(par);
       const float* D = reinterpret_cast<const float*>(sd(par));
       char* Dh = dsb(par);
@@ -1596,7 +1595,8 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
         *reinterpret_cast<f16x8*>(Dh + o * 64 + dsx) = bh;
         *reinterpret_cast<f16x8*>(Dh + G::DS_PL + o * 64 + dsx) = bl;
       }
-      if (wave == 4) stamp(g, 6);
+      if (wave == G::NE) stamp(g, 6);
+      __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0): the DMA pieces landed (read by every wave next)
       lds_barrier();
     };
 #pragma unroll 1
@@ -1648,19 +1648,14 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
 // 125 at g 2, 322 at g 1 (80 accumulator registers per wave: spills). URSONet step 2.11 -> 1.85 ms, keypoint mode
 // 1.27 -> 1.05 ms (with the small-map table below).
 // Kind 3 = kind 1 with persistent tiles (x2_irw_kernel's PT: a second tile per CU streams on without a prologue):
-// the maps with more tiles than CUs at 512^2 (blocks 8-14: 512 tiles at B = 64). Blocks 8-13 run 8 x 16 tiles with
-// LDS-staged project weights at 123-144 KB (one workgroup per CU).
-#ifndef SPEF_X2_KMID   // A/B aid: blocks 8-13's kind (3 role-split, 6 three-stage)
-#define SPEF_X2_KMID 3
-#endif
+// the maps with more tiles than CUs at 512^2 (blocks 8-14: 512 tiles at B = 64). Kind 5 / 6: the three-stage kernel
+// (x2_irp_kernel) without / with persistent tiles. Measured per step at B = 64 (tools/ktime.sh, bit-identical
+// outputs): blocks 15-16 131.4 -> 101.9 us on kind 5, blocks 12-13 147.9 -> 142.0 and block 11 51.8 -> 49.1 on kind
+// 6; blocks 8-10 130.7 -> 138.5 on kind 6 (their VALU role is the longer one there), so they stay on kind 3.
 #define SPEF_X2_MID(X)                                           \
-  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, SPEF_X2_KMID)      /* 8-10 */   \
-  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, SPEF_X2_KMID)     /* 11 */     \
-  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, SPEF_X2_KMID)      /* 12-13 */
-// Kind 5: the three-stage kernel (x2_irp_kernel). SPEF_X2_K1516: blocks 15-16's kind (A/B aid).
-#ifndef SPEF_X2_K1516
-#define SPEF_X2_K1516 1
-#endif
+  X(64, 384, 64, 1, true, true, 8, 16, 8, 1, 3)      /* 8-10 */   \
+  X(64, 384, 96, 1, true, false, 8, 16, 8, 1, 6)     /* 11 */     \
+  X(96, 576, 96, 1, true, true, 8, 16, 8, 1, 6)      /* 12-13 */
 #define SPEF_X2_TABLE(X)                                         \
   X(32, 32, 16, 1, false, false, 8, 16, 4, 1, 0)    /* 1 */      \
   X(16, 96, 24, 2, true, false, 8, 8, 4, 1, 0)      /* 2 */      \
@@ -1670,7 +1665,7 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(32, 192, 64, 2, true, false, 8, 8, 4, 1, 0)     /* 7 */      \
   SPEF_X2_MID(X)                                                 \
   X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 3)     /* 14 */     \
-  X(160, 960, 160, 1, true, true, 8, 8, 8, 1, SPEF_X2_K1516)    /* 15-16 */  \
+  X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 5)    /* 15-16 */  \
   X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
 // 16x16 tiles with 8 waves (2 workgroups per CU) where they tile the map exactly: block 3 at 512^2 (interleaved A/B,
 // round 4: 165 -> 153 us per step); on maps they do not divide (60x96, 30x48 at 240x384) the partial tiles cost more
@@ -1715,7 +1710,7 @@ static hipError_t x2_irb_go(const void* x, const void* we, const float* be, cons
     k<<<nwg, NW * 64, G::LDS_BYTES, s>>>(x, (const _Float16*)we, be, wd, bd, (const _Float16*)wp, bp, y, H, W, OH, OW,
                                         tiles_x, tiles_y, nwg);
   } else if constexpr ((KIND == 5 || KIND == 6) && IO == 0) {
-    static_assert(EXPAND && NW == 8 && P == 1, "three-stage blocks expand, 4 + 4 waves, one part");
+    static_assert(EXPAND && P == 1, "three-stage blocks expand, one part");
     constexpr bool PT = KIND == 6;   // persistent tiles: ceil(tiles / CUs) tiles per workgroup
     using G = X2pGeom<CIN, HID, COUT, S, TH, TW>;   // static LDS (G::LDS_BYTES)
     auto k = x2_irp_kernel<CIN, HID, COUT, S, TH, TW, RES, PT>;

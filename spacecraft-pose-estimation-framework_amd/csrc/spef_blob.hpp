@@ -35,8 +35,8 @@
 // plane = fp16(w - hi)), expand rows padded to H32 = hidden rounded up to 32; depthwise fp32 [9][H32], expand and
 // depthwise biases fp32 [H32]; stem x0 = [2][3 ky][32 ch][32 k] fp16 hi / lo of the /255-folded weights, k = 4 kx + ci.
 // fp16mx blob (dtype 6): the dtype-5 layout; OP_STEM x1 = [2][32 ch][32 k] fp16 hi / lo of the /255-folded weights in
-// the fp16 front kernel's row-triple k order (front_mx_kernel). The schedule stores the stem map, block outputs with
-// <= 32 channels and the hidden tensors of blocks 2-7 in fp16.
+// the fp16 front kernel's row-triple k order (front_mx_kernel). The schedule stores the stem map, the block outputs of
+// blocks 1-3 and the hidden tensors of blocks 2-4 in fp16.
 // BatchNorm (eps 1e-5) is folded: w' = w*g/sqrt(v+eps), b' = beta - mean*g/sqrt(v+eps).
 #pragma once
 #include <stdint.h>

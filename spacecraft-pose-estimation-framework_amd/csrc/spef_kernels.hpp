@@ -14,7 +14,7 @@ int report_error(int code, const std::string& msg);
 enum Dtype : int {
   DT_F16 = 1, DT_BF16 = 2, DT_I8 = 3, DT_F32 = 4,
   DT_X2 = 5,   // fp32 I/O, split-fp16 MFMA (k_x2.hip)
-  DT_MX = 6    // fp16mx: the fp16x2 kernels and weights, block outputs with <= 32 channels (blocks 1-6) stored fp16
+  DT_MX = 6    // fp16mx: the fp16x2 weights; stem map, block outputs of blocks 1-3, hidden of blocks 2-4 stored fp16
 };
 enum Epi : int { EPI_NONE = 0, EPI_RELU = 1, EPI_RES = 2, EPI_RELU_F32 = 3 /* ReLU, fp32 output */ };
 enum InLayout : int { IN_U8_NHWC = 0, IN_F32_NCHW = 1 };
@@ -94,8 +94,8 @@ bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool 
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
                          const float* be, const float* wd, const float* bd, const void* wp, const float* bp, void* y,
                          int B, int H, int W, int OH, int OW, hipStream_t s, float* scratch = nullptr, int io = 0);
-// fp16mx blocks 2-7 (k_mx.hip): fp16 (in16) or fp32 input, hi + lo fp16 weights (blob dtype 5 / 6 layout), fp16
-// hidden slab, fp32 depthwise, hi + lo project operand; fp16 (out16) or fp32 output.
+// fp16mx blocks 2-4 (k_mx.hip): fp16 input, hi + lo fp16 weights (blob dtype 5 / 6 layout), fp16 hidden slab, fp32
+// depthwise, hi + lo project operand; fp16 (out16: blocks 2-3) or fp32 (block 4) output.
 bool mx_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res, bool in16, bool out16);
 hipError_t launch_mx_irb(int cin, int hid, int cout, int stride, bool res, bool in16, bool out16, const void* x,
                          const void* we,

@@ -19,7 +19,7 @@ planes with k = 4 kx + ci (the front kernel's fragment order).
 
 ``fp16mx`` (dtype 6, the headline schedule): the fp16x2 layout, plus the stem operand in the fp16 front kernel's
 row-triple k order as a second tensor (x1, hi / lo [2][32][32]); the schedule stores the stem map, the block
-outputs of blocks 1-6 and the hidden tensors of blocks 2-7 in fp16 and every other activation in fp32, with every
+outputs of blocks 1-3 and the hidden tensors of blocks 2-4 in fp16 and every other activation in fp32, with every
 weight exact (tools/precision_budget.py: ~5e-4 max |d logit| at head std 0.3 against 1.3e-2 for the fp16 schedule).
 """
 from __future__ import annotations
@@ -35,7 +35,7 @@ MAGIC = b'SPEFMI35'
 VERSION = 2   # 2: fp16 stem MFMA operand in the front_vp_kernel row-triple k order (csrc/spef_blob.hpp)
 DTYPES = {'fp16': 1, 'bf16': 2, 'fp32': 4, 'fp16x2': 5, 'fp16mx': 6}   # fp32: the reference's own arithmetic
 # (k_f32.hip); fp16x2: fp32 activations with hi + lo fp16 MFMA operands (k_x2.hip); fp16mx: the same weights,
-# fp16 block outputs on blocks 1-6
+# fp16 stem map, block outputs of blocks 1-3, hidden tensors of blocks 2-4
 X2_DTYPES = ('fp16x2', 'fp16mx')   # the split-fp16 weight layout
 DT_I8 = 3
 OP_STEM, OP_IRB, OP_LAST, OP_FC, OP_FCKP = 1, 2, 3, 4, 5

@@ -20,7 +20,8 @@ fr = torch.from_numpy(np.random.Generator(np.random.PCG64(0)).integers(0, 256, (
 for _ in range(3):
     eng.forward(fr)
 torch.cuda.synchronize()
-for op, nch in ((15, 30),):
+OPS = [tuple(int(v) for v in a.split(':')) for a in (sys.argv[1:] or ['15:30'])]   # op:chunks (PT: x tiles)
+for op, nch in OPS:
     eng.probe(fr, op)
     y = eng.probe(fr, op)
     torch.cuda.synchronize()
@@ -33,5 +34,5 @@ for op, nch in ((15, 30),):
           f'barrier wait {med(st[1:, 0] - st[:-1, 2])}; VALU start->dw done {med(st[:, 5] - st[:, 4])}, '
           f'->prebar {med(st[:, 6] - st[:, 4])}, barrier wait {med(st[1:, 4] - st[:-1, 6])}')
     print(f'   entry->fragments {st[1, 3] - st[0, 3]}, entry->loop {t0 - st[0, 3]}, loop end->epilogue {st[0, 7] - st[-1, 2]}')
-    for c in (0, 1, 2, 15, 28, 29):
+    for c in sorted(set([0, 1, 2, nch // 2 - 1, nch // 2, nch // 2 + 1, nch - 2, nch - 1])):
         print('   ', c, st[c, 0] - t0, st[c, 1] - t0, st[c, 2] - t0, '|', st[c, 4] - t0, st[c, 5] - t0, st[c, 6] - t0)
