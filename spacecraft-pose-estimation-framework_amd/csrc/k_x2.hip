@@ -1190,7 +1190,15 @@ struct X2pGeom {
   static constexpr int DS_PL = POUT16 * 16 * 64;        // one Ds plane (bytes)
   static constexpr int NIE = SE_BQ / 1024, NID = SD_BQ / 1024;
   static constexpr int SLF = SL::FLOATS + 16 * 24;    // a slab + its dummy rows (invalid pixels' expand stores)
-  static constexpr int LDS_BYTES = 2 * SLF * 4 + 2 * SE_BQ + 2 * SD_BQ + 4 * DS_PL;
+  // PAL: the project A fragments staged in LDS, each MFMA wave's own tiles (by its own LDS-DMA, one chunk ahead),
+  // instead of registers held across the expand -- where those registers (8 per output-channel tile) would spill:
+  // block 17 (5 tiles per wave) 244 VGPRs, no spill, 101.5 -> 67.3 us per step at B = 64 on this kernel (from the
+  // role-split kernel; tools/ktime.sh, bit-identical); blocks 15-16 (3 tiles) 102 -> 105 us with it, so they keep
+  // the registers. Block 14 (EPT 5: 120 registers of input fragments) spills either way and has no LDS left for it.
+  static constexpr int LDS_BASE = 2 * SLF * 4 + 2 * SE_BQ + 2 * SD_BQ + 4 * DS_PL;
+  static constexpr bool PAL = NCTW >= 4 && POUT16 <= 4 && LDS_BASE + NE * NCTW * 2048 <= 163840;
+  static constexpr int SP_B = PAL ? NE * NCTW * 2048 : 0;
+  static constexpr int LDS_BYTES = LDS_BASE + SP_B;
   static_assert(CIN % 8 == 0 && COUT % 16 == 0 && HID % 32 == 0, "channel counts");
   static_assert(TH * TW % 16 == 0 && POUT16 % ND == 0 && NCH >= 4 && NCH % 2 == 0, "tile split / pipeline depth");
   static_assert(EPT <= 32 && LDS_BYTES <= 163840, "validity mask / LDS budget");
@@ -1213,6 +1221,7 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
   __shared__ __attribute__((aligned(1024))) char Se0[G::SE_BQ], Se1[G::SE_BQ];       // expand stages
   __shared__ __attribute__((aligned(1024))) char Sd0[G::SD_BQ], Sd1[G::SD_BQ];       // depthwise stages
   __shared__ __attribute__((aligned(16))) char Ds0[2 * G::DS_PL], Ds1[2 * G::DS_PL]; // depthwise outputs hi | lo
+  __shared__ __attribute__((aligned(1024))) char Sp[G::PAL ? G::SP_B : 16];          // project A stage (PAL)
   __shared__ uint32_t Stamps[SPEF_X2_STAMP ? 8 * 64 : 1];
   using I0 = std::integral_constant<int, 0>;
   using I1 = std::integral_constant<int, 1>;
@@ -1422,18 +1431,44 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     init_acc();
     const _Float16* WpLo = Wp + (size_t)G::NPC * G::HIDP;
     f16x8 pah[G::NCTW], pal[G::NCTW];
+    char* const spw = Sp + wr * (G::NCTW * 2048);   // PAL: this wave's A stage (tile t: hi at 2048 t, lo + 1024)
     auto load_pa = [&](int k) {
 #pragma unroll
       for (int t = 0; t < G::NCTW; ++t)
         if (e + G::NE * t < G::NCT) {
           const size_t off = (size_t)((e + G::NE * t) * 16 + r16) * G::HIDP + 32 * k + 8 * kg;
-          pah[t] = *reinterpret_cast<const f16x8*>(Wp + off);
-          pal[t] = *reinterpret_cast<const f16x8*>(WpLo + off);
+          if constexpr (G::PAL) {
+            __builtin_amdgcn_global_load_lds((const void*)(Wp + off),
+                                             (__attribute__((address_space(3))) void*)(spw + t * 2048), 16, 0, 0);
+            __builtin_amdgcn_global_load_lds((const void*)(WpLo + off),
+                                             (__attribute__((address_space(3))) void*)(spw + t * 2048 + 1024), 16, 0,
+                                             0);
+          } else {
+            pah[t] = *reinterpret_cast<const f16x8*>(Wp + off);
+            pal[t] = *reinterpret_cast<const f16x8*>(WpLo + off);
+          }
         }
     };
     // the B fragments of pixel tile q + 1 are read before tile q's MFMAs (each read pair's LDS latency hides behind
     // the previous tile's MFMAs instead of stalling the MFMA role)
     auto project = [&](const char* Dh) {
+      if constexpr (G::PAL) {   // all pixel tiles' B fragments, then output-channel tile by tile (its A from the stage)
+        f16x8 bh[G::POUT16], bl[G::POUT16];
+#pragma unroll
+        for (int q = 0; q < G::POUT16; ++q) {
+          bh[q] = *reinterpret_cast<const f16x8*>(Dh + (q * 16 + r16) * 64 + dsx);
+          bl[q] = *reinterpret_cast<const f16x8*>(Dh + G::DS_PL + (q * 16 + r16) * 64 + dsx);
+        }
+#pragma unroll
+        for (int t = 0; t < G::NCTW; ++t) {
+          if (e + G::NE * t >= G::NCT) continue;
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(spw + t * 2048 + 16 * lane);
+          const f16x8 al = *reinterpret_cast<const f16x8*>(spw + t * 2048 + 1024 + 16 * lane);
+#pragma unroll
+          for (int q = 0; q < G::POUT16; ++q) acc[q][t] = mfma_x2(ah, al, bh[q], bl[q], acc[q][t]);
+        }
+        return;
+      }
       f16x8 bh[2], bl[2];
       bh[0] = *reinterpret_cast<const f16x8*>(Dh + r16 * 64 + dsx);
       bl[0] = *reinterpret_cast<const f16x8*>(Dh + G::DS_PL + r16 * 64 + dsx);
@@ -1545,6 +1580,7 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
       if (wave == G::NE) stamp(g, 4);
       if (g + 2 < GT) dma_e(kmod(g + 2), se(par));
       if (g + 1 < GT) dma_d(kmod(g + 1), sd(Q{}));
+      if (wave == G::NE) stamp(g, 5);
       const float* Sl = slab(par);
       const float* D = reinterpret_cast<const float*>(sd(par));
       char* Dh = dsb(par);
@@ -1664,9 +1700,9 @@ __global__ __launch_bounds__(256) void x2_split_reduce_kernel(const float* __res
   X(32, 192, 32, 1, true, true, 8, 16, 4, 1, 0)     /* 5-6 */    \
   X(32, 192, 64, 2, true, false, 8, 8, 4, 1, 0)     /* 7 */      \
   SPEF_X2_MID(X)                                                 \
-  X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 3)     /* 14 */     \
+  X(96, 576, 160, 2, true, false, 4, 8, 8, 2, 3)    /* 14 */     \
   X(160, 960, 160, 1, true, true, 8, 8, 8, 1, 5)    /* 15-16 */  \
-  X(160, 960, 320, 1, true, false, 8, 8, 8, 2, 2)   /* 17 */
+  X(160, 960, 320, 1, true, false, 8, 8, 8, 1, 5)    /* 17 */
 // 16x16 tiles with 8 waves (2 workgroups per CU) where they tile the map exactly: block 3 at 512^2 (interleaved A/B,
 // round 4: 165 -> 153 us per step); on maps they do not divide (60x96, 30x48 at 240x384) the partial tiles cost more
 // than the occupancy gains. Blocks 5-6 left this table in round 5: behind the fp16mx front end 8 x 16 tiles measured

@@ -31,7 +31,7 @@ for op, nch in OPS:
     med = lambda v: int(np.median(v))  # noqa: E731
     print(f'block {op}: {nch} chunks, loop {st[-1, 2] - t0} cycles; per chunk (median): period {med(per)}, '
           f'MFMA start->P issued {med(st[:, 1] - st[:, 0])}, ->E issued {med(st[:, 2] - st[:, 0])}, '
-          f'barrier wait {med(st[1:, 0] - st[:-1, 2])}; VALU start->dw done {med(st[:, 5] - st[:, 4])}, '
+          f'barrier wait {med(st[1:, 0] - st[:-1, 2])}; VALU start->DMA issued {med(st[:, 5] - st[:, 4])}, '
           f'->prebar {med(st[:, 6] - st[:, 4])}, barrier wait {med(st[1:, 4] - st[:-1, 6])}')
     print(f'   entry->fragments {st[1, 3] - st[0, 3]}, entry->loop {t0 - st[0, 3]}, loop end->epilogue {st[0, 7] - st[-1, 2]}')
     for c in sorted(set([0, 1, 2, nch // 2 - 1, nch // 2, nch // 2 + 1, nch - 2, nch - 1])):

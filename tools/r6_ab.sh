@@ -16,6 +16,6 @@ for r in $(seq $N); do
       --no-x2 --no-fp16 --no-cpu-baseline --sharp-frames 0 --detail-out gpurun_out/ab_$v$r.json $EXTRA > /dev/null 2> gpurun_out/ab_$v$r.err || { tail -20 gpurun_out/ab_$v$r.err; exit 1; }
     python -c "
 import json; d=json.load(open('gpurun_out/ab_$v$r.json')); print('$v', d['value'], d['ms_per_step'], d['sclk_timed_region']['sclk_mhz'], 'leg', d['roofline']['sclk_mhz'])
-print('   ', {k.split('_kernel')[0][:4]+'<'+k.split('<')[1]: round(x['ms_per_step']*1e3,1) for k,x in d['kernels'].items()})"
+print('   ', {k.split('_kernel')[0][:4]+'<'+k.split('<')[-1]: round(x['ms_per_step']*1e3,1) for k,x in d['kernels'].items()})"
   done
 done
