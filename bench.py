@@ -50,7 +50,7 @@ INT8_TOLERANCE = ('int8 contract: bit-exact vs the integer oracle (oracle/int8_r
 INT8_BOUND = (0.05, 0.030, 0.25)   # logits, position (m), orientation (deg)
 # committed rocprofv3 FETCH_SIZE / WRITE_SIZE summaries, newest first (profiles/)
 FP16_TRAFFIC = ['r04_pmc_traffic.json', 'r03f_pmc_traffic.json']
-MX_TRAFFIC = ['r05_mx_pmc_traffic.json']
+MX_TRAFFIC = ['r06_mx_pmc_traffic.json', 'r05_mx_pmc_traffic.json']
 INT8_TRAFFIC = ['r03_int8_pmc_traffic.json']
 X2_TRAFFIC = ['r05_x2_pmc_traffic.json', 'r04_x2_pmc_traffic.json']
 TRAFFIC = {'fp16': FP16_TRAFFIC, 'bf16': FP16_TRAFFIC, 'int8': INT8_TRAFFIC, 'fp16x2': X2_TRAFFIC, 'fp16mx': MX_TRAFFIC}
@@ -77,7 +77,7 @@ def pmc_traffic(kernel_key: str, path: str):
     m = re.fullmatch(r'(x2_irb_kernel|mx_irb_kernel|ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
     if m:   # fused block key -> the one template instantiation profiled for that geometry (fp16x2: slab or role-split)
         geo = ','.join(m.groups()[1:]) + ','
-        kind = {'x2_irb_kernel': r'x2_ir[bw]_kernel<', 'mx_irb_kernel': r'mx_irb_kernel<'}.get(m.group(1),
+        kind = {'x2_irb_kernel': r'x2_ir[bwp]_kernel<', 'mx_irb_kernel': r'mx_irb_kernel<'}.get(m.group(1),
                                                                                              m.group(1) + r'<B?F16,')
         hits = [v for k, v in kernels.items() if re.match(kind + re.escape(geo), k)]
     else:   # e.g. front_kernel<stem+block1> -> front_kernel<...> or its fp16 form front_vp_kernel<...>

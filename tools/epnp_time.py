@@ -22,6 +22,8 @@ for P in (64, 512, 1800):
     kp = torch.from_numpy(np.ascontiguousarray(g['kp2d'][:P], np.float32)).cuda()
     o = eng.decode_keypoints(kp, apply_sigmoid=False)
     torch.cuda.synchronize()
+    if os.environ.get('EPNP_DUMP'):   # outputs for a bit-identity check of two builds
+        np.savez(f"{os.environ['EPNP_DUMP']}_{P}.npz", ori=o['ori'].cpu().numpy(), pos=o['pos'].cpu().numpy())
     kat = float(np.max(angle_deg(o['ori'].cpu().numpy(), g['q'][:P])))
     katp = float(np.linalg.norm(o['pos'].cpu().numpy() - g['t'][:P], axis=1).max())
     for _ in range(5):
