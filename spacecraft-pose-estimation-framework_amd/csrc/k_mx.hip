@@ -243,23 +243,44 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     for (int t = 0; t < G::PPL; ++t)
 #pragma unroll
       for (int e = 0; e < 8; ++e) a[t][e] = db[e];
+    // one input row r, tap column kx: its contributions to the lane's PPL output rows (ky = r - S t)
+    auto dw_col = [&](int r, int kx, const uint4 xv) {
+      const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
 #pragma unroll
-    for (int r = 0; r < G::NR; ++r) {
+      for (int t = 0; t < G::PPL; ++t) {
+        const int ky = r - S * t;
+        if (ky < 0 || ky > 2) continue;
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) {
-        const uint4 xv = *reinterpret_cast<const uint4*>(smem + dbase + r * G::IW * G::SPB + KXO[kx]);
-        const uint32_t xs[4] = {xv.x, xv.y, xv.z, xv.w};
-#pragma unroll
-        for (int t = 0; t < G::PPL; ++t) {
-          const int ky = r - S * t;
-          if (ky < 0 || ky > 2) continue;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            a[t][2 * e] = fmaf(h_lo(xs[e]), wd[ky * 3 + kx][2 * e], a[t][2 * e]);
-            a[t][2 * e + 1] = fmaf(h_hi(xs[e]), wd[ky * 3 + kx][2 * e + 1], a[t][2 * e + 1]);
-          }
+        for (int e = 0; e < 4; ++e) {
+          a[t][2 * e] = fmaf(h_lo(xs[e]), wd[ky * 3 + kx][2 * e], a[t][2 * e]);
+          a[t][2 * e + 1] = fmaf(h_hi(xs[e]), wd[ky * 3 + kx][2 * e + 1], a[t][2 * e + 1]);
         }
       }
+    };
+    auto rd = [&](int r, int kx) { return *reinterpret_cast<const uint4*>(smem + dbase + r * G::IW * G::SPB + KXO[kx]); };
+    if constexpr (S == 2) {
+      // stride 2 (blocks 2, 4): a row's three tap columns read together and the next row's issued before this row's
+      // FMAs (up to six reads in flight per lane instead of one; the same FMAs per accumulator in the same order,
+      // bit-identical: interleaved A/B, block 2 122.3 -> 119.7 us, block 4 62.5 -> 59.4). Stride 1 (block 3) keeps one
+      // read in flight: its 168-register budget (3 waves per SIMD) spills with the row buffers, and at two waves per SIMD
+      // (180 registers, no spill) it measured 133 -> 148 us.
+      uint4 xr[2][3];
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) xr[0][kx] = rd(0, kx);
+#pragma unroll
+      for (int r = 0; r < G::NR; ++r) {
+        if (r + 1 < G::NR) {
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) xr[(r + 1) & 1][kx] = rd(r + 1, kx);
+        }
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) dw_col(r, kx, xr[r & 1][kx]);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < G::NR; ++r)
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) dw_col(r, kx, rd(r, kx));
     }
     __syncthreads();   // every wave's slab reads done before the exchange overlays it
     // ReLU, hi / lo split -> exchange buffer (pixel (row ry PPL + t, column cx), channels 8 wave ..)
