@@ -213,15 +213,6 @@ __device__ __forceinline__ int rr_partner(int r, int i) {
   return (2 * r - i + 22) % 11;
 }
 
-// entry (x, y) of J^T A J for a round's rotation J: row x pairs with x2, column y with y2 (signed coefficients)
-__device__ __forceinline__ double rot_entry(double cx, double sx, double cy, double sy, double axy, double axy2,
-                                            double ax2y, double ax2y2) {
-  return cx * (cy * axy + sy * axy2) + sx * (cy * ax2y + sy * ax2y2);
-}
-
-#ifndef SPEF_EPNP_1BAR   // look-ahead Jacobi rounds on a fourth (rotation) wave
-#define SPEF_EPNP_1BAR 0
-#endif
 #ifndef SPEF_EPNP_JTOL   // Jacobi stops once off-diagonal^2 <= JTOL x diagonal^2
 #define SPEF_EPNP_JTOL 1e-26
 #endif
@@ -233,7 +224,7 @@ __device__ __forceinline__ double rot_entry(double cx, double sx, double cy, dou
 #else
 #define SPEF_EPNP_ATTR
 #endif
-__global__ __launch_bounds__(SPEF_EPNP_1BAR ? 256 : 192) SPEF_EPNP_ATTR void epnp_kernel(const float* __restrict__ raw, int B, int n,
+__global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* __restrict__ raw, int B, int n,
                                                    const float* __restrict__ kp3d, const double* __restrict__ model,
                                                    double fu, double fv, double uc,
                                                    double vc, float nu, float nv, EpnpDist dist, int apply_sigmoid,
@@ -241,9 +232,6 @@ __global__ __launch_bounds__(SPEF_EPNP_1BAR ? 256 : 192) SPEF_EPNP_ATTR void epn
                                                    float* __restrict__ pos, int* __restrict__ status) {
   __shared__ double As[2][144], Vs[2][144];
   __shared__ double Cc[12], Cs[12];
-#if SPEF_EPNP_1BAR
-  __shared__ double Cc2[2][12], Cs2[2][12];
-#endif
   __shared__ double Pal[EPNP_MAXN][4], Pdu[EPNP_MAXN], Pdv[EPNP_MAXN];
   __shared__ double Red[3][2];
   __shared__ double Ls[6][10], Rho[6];
@@ -317,67 +305,14 @@ __global__ __launch_bounds__(SPEF_EPNP_1BAR ? 256 : 192) SPEF_EPNP_ATTR void epn
     }
     off = warp_sum_d(off);
     diag = warp_sum_d(diag);
-    if (lane == 0 && wave < 3) {
+    if (lane == 0) {
       Red[wave][0] = off;
       Red[wave][1] = diag;
     }
-#if SPEF_EPNP_1BAR
-    if (tid < 12) {   // J(-1) = identity
-      Cc2[0][tid] = 1.0;
-      Cs2[0][tid] = 0.0;
-    }
-#endif
     __syncthreads();
     off = Red[0][0] + Red[1][0] + Red[2][0];
     diag = Red[0][1] + Red[1][1] + Red[2][1];
     if (off <= SPEF_EPNP_JTOL * diag || off == 0.0) break;   // uniform: every thread read the same sums
-#if SPEF_EPNP_1BAR
-    // look-ahead rounds, one barrier each: round r's entry threads apply J(r-1) (A(r) = J^T A(r-1) J, V(r) = V(r-1) J)
-    // while lanes 0..11 of a fourth wave compute the three entries of A(r) their pair needs straight from A(r-1) and J(r-1) -- the same
-    // expression, so the same values -- and J(r) from them; J(-1) = identity, J(10) applied after the last round
-    int jb = 0;
-    for (int r = 0; r < 11; ++r) {
-      const int rp = r == 0 ? 10 : r - 1;   // the pairing of J(r - 1) (any at r = 0: identity)
-      const double* a = As[cur];
-      const double* cc = Cc2[jb];
-      const double* cs = Cs2[jb];
-      if (ent) {
-        const int i2 = rr_partner(rp, ei), j2 = rr_partner(rp, ej);
-        As[cur ^ 1][e] = rot_entry(cc[ei], cs[ei], cc[ej], cs[ej], a[12 * ei + ej], a[12 * ei + j2], a[12 * i2 + ej],
-                                   a[12 * i2 + j2]);
-        const double* v = Vs[cur];
-        Vs[cur ^ 1][e] = cc[ej] * v[12 * ei + ej] + cs[ej] * v[12 * ei + j2];
-      }
-      if (wave == 3 && lane < 12) {   // the rotation wave (no entry of its own)
-        const int j = rr_partner(r, lane);
-        const int p = lane < j ? lane : j, q = lane < j ? j : lane;
-        auto ar = [&](int x, int y) {
-          const int x2 = rr_partner(rp, x), y2 = rr_partner(rp, y);
-          return rot_entry(cc[x], cs[x], cc[y], cs[y], a[12 * x + y], a[12 * x + y2], a[12 * x2 + y], a[12 * x2 + y2]);
-        };
-        const double apq = ar(p, q), app = ar(p, p), aqq = ar(q, q);
-        double c = 1.0, sn = 0.0;
-        if (fabs(apq) >= 1e-300) jacobi_rot(app, aqq, apq, c, sn);
-        Cc2[jb ^ 1][lane] = c;
-        Cs2[jb ^ 1][lane] = lane == p ? -sn : sn;
-      }
-      cur ^= 1;
-      jb ^= 1;
-      __syncthreads();
-    }
-    if (ent) {   // J(10)
-      const double* a = As[cur];
-      const double* cc = Cc2[jb];
-      const double* cs = Cs2[jb];
-      const int i2 = rr_partner(10, ei), j2 = rr_partner(10, ej);
-      As[cur ^ 1][e] = rot_entry(cc[ei], cs[ei], cc[ej], cs[ej], a[12 * ei + ej], a[12 * ei + j2], a[12 * i2 + ej],
-                                 a[12 * i2 + j2]);
-      const double* v = Vs[cur];
-      Vs[cur ^ 1][e] = cc[ej] * v[12 * ei + ej] + cs[ej] * v[12 * ei + j2];
-    }
-    cur ^= 1;
-    __syncthreads();
-#else
     for (int r = 0; r < 11; ++r) {
       if (tid < 12) {   // thread i: the rotation of its pair, its own signed coefficient
         const int j = rr_partner(r, tid);
@@ -400,11 +335,7 @@ __global__ __launch_bounds__(SPEF_EPNP_1BAR ? 256 : 192) SPEF_EPNP_ATTR void epn
       cur ^= 1;
       __syncthreads();
     }
-#endif
   }
-#if SPEF_EPNP_1BAR
-  if (wave == 3) return;   // (the rotation wave's work is done; later barriers count the three remaining waves)
-#endif
   // the 4 eigenvectors of smallest eigenvalue, ascending (ties keep the lower index); static loops only (a
   // dynamically indexed private array would live in scratch)
   double ev[12];
@@ -640,7 +571,7 @@ hipError_t launch_epnp(const float* raw, int B, int n, const float* kp3d, const 
                        float nu, float nv, const EpnpDist& dist, int apply_sigmoid, float* kp_out, float* quat,
                        float* pos, int* status, hipStream_t s) {
   if (n < 4 || n > EPNP_MAXN) return hipErrorInvalidValue;
-  epnp_kernel<<<B, SPEF_EPNP_1BAR ? 256 : 192, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, dist, apply_sigmoid, kp_out,
+  epnp_kernel<<<B, 192, 0, s>>>(raw, B, n, kp3d, model, K[0], K[4], K[2], K[5], nu, nv, dist, apply_sigmoid, kp_out,
                                 quat, pos, status);
   return hipGetLastError();
 }

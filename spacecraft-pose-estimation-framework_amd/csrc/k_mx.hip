@@ -122,7 +122,15 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
   f16x8 bx[G::EPT];
   uint32_t zmask = 0;   // the lane's padding pixels (per expand tile)
   const bool edge = iy0 < 0 || ix0 < 0 || iy0 + G::IH > H || ix0 + G::IW > W;   // workgroup-uniform
-  int soff[G::EPT];   // slab byte offset of the lane's pixel (channels 4kg.. of h = 0), or its dummy row
+  // Expand MFMA row m of half h is hidden channel 8 (m / 4) + 4 h + m % 4 of the chunk (expand weight rows and bias
+  // read in that order), so a lane's two C fragments are channels 8 kg .. 8 kg + 7 and leave as one 16-B store; the
+  // natural order's two 8-B stores per fragment pair were 2-way bank-conflicted (16 consecutive 80-B pixel slots).
+  // The slab keeps the natural channel order; every hidden value is the same sum, bit-identical (interleaved A/B: LDS
+  // conflict / active cycles of block 3 0.20 -> 0.02, blocks 2 / 4 -1.6 / -0.4 us).
+  constexpr int KGB = 16;   // slab bytes per k group of a lane's store
+  auto erow = [&](int h) { return 8 * (r16 >> 2) + 4 * h + (r16 & 3); };
+  auto zero_slot = [&](int o) { *reinterpret_cast<uint4*>(smem + o) = make_uint4(0u, 0u, 0u, 0u); };
+  int soff[G::EPT];   // slab byte offset of the lane's pixel (its first channel of h = 0), or its dummy row
 #pragma unroll
   for (int j = 0; j < G::EPT; ++j) {
     const int p = (wave + G::NW * j) * 16 + r16;
@@ -143,11 +151,8 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     }
     const int ps = p;
     if (!ok && p < G::PIN) zmask |= 1u << j;   // (re-zeroed every chunk on edge tiles: the exchange overlays the slab)
-    soff[j] = ok ? ps * G::SPB + 8 * kg : G::OFF_TR + r16 * G::SPB + 8 * kg;
-    if (!ok && p < G::PIN) {   // the depthwise's zero padding: stored once, never overwritten
-      *reinterpret_cast<uint2*>(smem + ps * G::SPB + 8 * kg) = make_uint2(0u, 0u);
-      *reinterpret_cast<uint2*>(smem + ps * G::SPB + 32 + 8 * kg) = make_uint2(0u, 0u);
-    }
+    soff[j] = ok ? ps * G::SPB + KGB * kg : G::OFF_TR + r16 * G::SPB + KGB * kg;
+    if (!ok && p < G::PIN) zero_slot(ps * G::SPB + KGB * kg);   // the depthwise's zero padding
   }
 
   // ---- depthwise lane geometry: (row group ry, column cx) from the ds_read_b128 lane groups
@@ -174,10 +179,10 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
       if constexpr (PK) {   // k groups 0, 1: W_hi channels 0-15; 2, 3: W_lo channels 0-15
-        const size_t off = (size_t)(32 * k + 16 * h + r16) * 32 + 8 * (kg & 1);
+        const size_t off = (size_t)(32 * k + erow(h)) * 32 + 8 * (kg & 1);
         eah[h] = *reinterpret_cast<const f16x8*>((kg < 2 ? We : WeLo) + off);
       } else {
-        const size_t off = (size_t)(32 * k + 16 * h + r16) * 32 + 8 * kg;
+        const size_t off = (size_t)(32 * k + erow(h)) * 32 + 8 * kg;
         eah[h] = *reinterpret_cast<const f16x8*>(We + off);
         eal[h] = *reinterpret_cast<const f16x8*>(WeLo + off);
       }
@@ -213,24 +218,27 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     {
       float4 eb[2];
 #pragma unroll
-      for (int h = 0; h < 2; ++h) eb[h] = *reinterpret_cast<const float4*>(be + 32 * c + 16 * h + 4 * kg);
+      for (int h = 0; h < 2; ++h)
+        eb[h] = *reinterpret_cast<const float4*>(be + 32 * c + 8 * kg + 4 * h);
 #pragma unroll
       for (int j = 0; j < G::EPT; ++j) {
+        f32x4 e[2];
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          f32x4 e = f32x4{eb[h].x, eb[h].y, eb[h].z, eb[h].w};
-          e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e, 0, 0, 0);
-          if constexpr (!PK) e = __builtin_amdgcn_mfma_f32_16x16x32_f16(eal[h], bx[j], e, 0, 0, 0);
-          *reinterpret_cast<uint2*>(smem + soff[j] + 32 * h) = make_uint2(relu_pk2(e[0], e[1]), relu_pk2(e[2], e[3]));
+          e[h] = f32x4{eb[h].x, eb[h].y, eb[h].z, eb[h].w};
+          e[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(eah[h], bx[j], e[h], 0, 0, 0);
+          if constexpr (!PK) e[h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(eal[h], bx[j], e[h], 0, 0, 0);
         }
+        // the lane's 8 hidden channels 8 kg .. 8 kg + 7
+        *reinterpret_cast<uint4*>(smem + soff[j]) = make_uint4(relu_pk2(e[0][0], e[0][1]), relu_pk2(e[0][2], e[0][3]),
+                                                               relu_pk2(e[1][0], e[1][1]), relu_pk2(e[1][2], e[1][3]));
       }
       if (edge && c > 0) {   // the exchange overlaid the slab: restore the depthwise's zero padding
 #pragma unroll
         for (int j = 0; j < G::EPT; ++j)
           if ((zmask >> j) & 1u) {
-            const int zo = ((wave + G::NW * j) * 16 + r16) * G::SPB + 8 * kg;
-            *reinterpret_cast<uint2*>(smem + zo) = make_uint2(0u, 0u);
-            *reinterpret_cast<uint2*>(smem + zo + 32) = make_uint2(0u, 0u);
+            const int pz = (wave + G::NW * j) * 16 + r16;
+            zero_slot(pz * G::SPB + KGB * kg);
           }
       }
       if (c + 1 < G::NCH) load_e(c + 1);
@@ -261,9 +269,9 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
     if constexpr (S == 2) {
       // stride 2 (blocks 2, 4): a row's three tap columns read together and the next row's issued before this row's
       // FMAs (up to six reads in flight per lane instead of one; the same FMAs per accumulator in the same order,
-      // bit-identical: interleaved A/B, block 2 122.3 -> 119.7 us, block 4 62.5 -> 59.4). Stride 1 (block 3) keeps one
-      // read in flight: its 168-register budget (3 waves per SIMD) spills with the row buffers, and at two waves per SIMD
-      // (180 registers, no spill) it measured 133 -> 148 us.
+      // bit-identical: interleaved A/B, block 2 122.3 -> 119.7 us, block 4 62.5 -> 59.4). Stride 1 (block 3) has no
+      // registers for the next row's buffers in its 168-register budget (3 waves per SIMD); at two waves per SIMD (180
+      // registers) it measured 133 -> 148 us.
       uint4 xr[2][3];
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) xr[0][kx] = rd(0, kx);
@@ -276,11 +284,16 @@ void mx_irb_kernel(const void* __restrict__ X, const _Float16* __restrict__ We, 
 #pragma unroll
         for (int kx = 0; kx < 3; ++kx) dw_col(r, kx, xr[r & 1][kx]);
       }
-    } else {
+    } else {   // stride 1 (block 3): a row's three tap columns read together (block 3 132.4 -> 123.2 us, with the
+      // 16-B expand stores' register savings: 164 of its 168 registers)
 #pragma unroll
-      for (int r = 0; r < G::NR; ++r)
+      for (int r = 0; r < G::NR; ++r) {
+        uint4 xr[3];
 #pragma unroll
-        for (int kx = 0; kx < 3; ++kx) dw_col(r, kx, rd(r, kx));
+        for (int kx = 0; kx < 3; ++kx) xr[kx] = rd(r, kx);
+#pragma unroll
+        for (int kx = 0; kx < 3; ++kx) dw_col(r, kx, xr[kx]);
+      }
     }
     __syncthreads();   // every wave's slab reads done before the exchange overlays it
     // ReLU, hi / lo split -> exchange buffer (pixel (row ry PPL + t, column cx), channels 8 wave ..)

@@ -1517,12 +1517,8 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
             if constexpr (RES) {
               v[0] += r[qq][tt].x; v[1] += r[qq][tt].y; v[2] += r[qq][tt].z; v[3] += r[qq][tt].w;
             }
-#if SPEF_X2_NTST
-            __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(Y + pix_[qq] * COUT + (e + G::NE * tt) * 16 + 4 * kg));
-#else
             *reinterpret_cast<float4*>(Y + pix_[qq] * COUT + (e + G::NE * tt) * 16 + 4 * kg) =
                 make_float4(v[0], v[1], v[2], v[3]);
-#endif
           }
         }
       }
