@@ -74,11 +74,13 @@ def pmc_traffic(kernel_key: str, path: str):
     if kernel_key in kernels:
         return kernels[kernel_key]['hbm_bytes_per_launch']
     import re
-    m = re.fullmatch(r'(x2_irb_kernel|mx_irb_kernel|ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
-    if m:   # fused block key -> the one template instantiation profiled for that geometry (fp16x2: slab or role-split)
+    m = re.fullmatch(r'(x2_ir[bwp]_kernel|mx_irb_kernel|ir[bwp]_kernel)<(\d+),(\d+),(\d+),s(\d+)>', kernel_key)
+    if m:   # fused block key -> the one template instantiation profiled for that geometry (fp16x2: slab, role-split or
+        # three-stage; the key names the kernel the library launched)
         geo = ','.join(m.groups()[1:]) + ','
-        kind = {'x2_irb_kernel': r'x2_ir[bwp]_kernel<', 'mx_irb_kernel': r'mx_irb_kernel<'}.get(m.group(1),
-                                                                                             m.group(1) + r'<B?F16,')
+        kind = {'x2_irb_kernel': r'x2_ir[bwp]_kernel<', 'x2_irw_kernel': r'x2_irw_kernel<',
+                'x2_irp_kernel': r'x2_irp_kernel<', 'mx_irb_kernel': r'mx_irb_kernel<'}.get(m.group(1),
+                                                                                         m.group(1) + r'<B?F16,')
         hits = [v for k, v in kernels.items() if re.match(kind + re.escape(geo), k)]
     else:   # e.g. front_kernel<stem+block1> -> front_kernel<...> or its fp16 form front_vp_kernel<...>
         base = kernel_key.split('<')[0]

@@ -1846,6 +1846,33 @@ hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bo
   return hipErrorNotSupported;
 }
 
+// The kernel launch_x2_irb runs for these arguments (the same table walk): "x2_irb_kernel" (slab), "x2_irw_kernel"
+// (role-split), "x2_irp_kernel" (three-stage); nullptr when none. Profiling labels only.
+const char* x2_irb_kernel_name(int cin, int hid, int cout, int stride, bool expand, bool res, int B, int OH, int OW,
+                               bool scratch, int io, int num_cu) {
+  auto name = [](int kind) { return kind == 0 ? "x2_irb_kernel" : kind >= 5 ? "x2_irp_kernel" : "x2_irw_kernel"; };
+#define SPEF_X2_TILES(TH_, TW_) ((int64_t)((OW + (TW_)-1) / (TW_)) * ((OH + (TH_)-1) / (TH_)) * B)
+#define SPEF_X2_SMALL(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_, P_)                                    \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS && scratch && !io &&  \
+      SPEF_X2_TILES(8, 8) < num_cu && SPEF_X2_TILES(TH_, TW_) * P_ <= num_cu)                                \
+    return name(KD_);
+  SPEF_X2_SMALL_TABLE(SPEF_X2_SMALL)
+#undef SPEF_X2_SMALL
+#undef SPEF_X2_TILES
+#define SPEF_X2_NAME_EXACT(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                   \
+  if (SPEF_X2_EXACT_ON && cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS &&  \
+      OH % (TH_) == 0 && OW % (TW_) == 0)                                                                     \
+    return (KD_ != 0 && io) ? nullptr : name(KD_);
+  SPEF_X2_EXACT_TABLE(SPEF_X2_NAME_EXACT)
+#undef SPEF_X2_NAME_EXACT
+#define SPEF_X2_NAME(CI, HI, CO, ST, EX, RS, TH_, TW_, NW_, WC_, KD_)                                         \
+  if (cin == CI && hid == HI && cout == CO && stride == ST && expand == EX && res == RS)                      \
+    return (KD_ != 0 && io) ? nullptr : name(KD_);
+  SPEF_X2_TABLE(SPEF_X2_NAME)
+#undef SPEF_X2_NAME
+  return nullptr;
+}
+
 // ------------------------------------------------------------------------------------------ front: stem + block 1
 // uint8 NHWC frames -> stem ConvBnAct 3 -> 32, 3x3 / 2 (mobilenet_v2.py:252-254; ToTensor's /255 folded into the
 // weights) -> block 1 (depthwise 3x3 + project 32 -> 16, pytorch_layers.py:65-98) -> fp32 block-1 output, one kernel:

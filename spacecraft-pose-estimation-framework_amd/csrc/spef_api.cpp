@@ -185,6 +185,16 @@ inline const T* ptr(const spef_ctx* c, uint64_t off) {
 
 // quantizer bit width of an int8 op (spef_blob.hpp qbits; 0 = 8)
 static inline int qbits(const OpDesc& op, int i) { return op.qbits[i] ? op.qbits[i] : 8; }
+// compute units of the current device (cached per device; launch_x2_irb sizes its tiles by the same query)
+static int num_cus() {
+  static int cus[32] = {};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) dev = 0;
+  dev &= 31;
+  if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    cus[dev] = 256;
+  return cus[dev];
+}
 
 // QuantAvgPool2d + TruncTo8bit (ursonet.py:61-62, 88): the HW-pixel sum of last_conv's b_last-bit codes has
 // b_last + ceil(log2 HW) bits; truncation to the pooling width drops the rest (oracle/int8_ref.py pool_shift).
@@ -359,8 +369,11 @@ int run_backbone(spef_ctx* c, const void* input, int layout, int B, int H, int W
         const bool mxk = mx && c->mx_kernels &&
                          mx_irb_supported((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand, res, cur16,
                                           o16);
-        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", mxk ? "mx_irb_kernel" : "x2_irb_kernel", op.cin, op.hidden,
-                 op.cout, op.stride);
+        const char* kn = mxk ? "mx_irb_kernel"
+                             : x2_irb_kernel_name((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, expand,
+                                                  res, B, OH, OW, true, io, num_cus());
+        snprintf(key, sizeof(key), "%s<%u,%u,%u,s%u>", kn ? kn : "x2_irb_kernel", op.cin, op.hidden, op.cout,
+                 op.stride);
         HIP_TRY(prof_launch(c, s, key, bytes, flops, [&] {
           if (mxk)
             return launch_mx_irb((int)op.cin, (int)op.hidden, (int)op.cout, (int)op.stride, res, cur16, o16, x,

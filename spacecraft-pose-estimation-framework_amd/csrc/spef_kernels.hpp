@@ -89,6 +89,10 @@ const char* gemm_f32_key(int N);
 // operands (3 MFMAs per product). we: [2][r32(hid)][r32(cin)] fp16 (hi plane, lo plane), be fp32 [r32(hid)],
 // wd fp32 [9][r32(hid)], bd fp32 [r32(hid)], wp [2][r16(cout)][r32(hid)] fp16, bp fp32 [r16(cout)]; zero padded.
 bool x2_irb_supported(int cin, int hid, int cout, int stride, bool expand, bool res);
+// the kernel launch_x2_irb runs for these arguments ("x2_irb_kernel" / "x2_irw_kernel" / "x2_irp_kernel"; profiling
+// labels), nullptr when none
+const char* x2_irb_kernel_name(int cin, int hid, int cout, int stride, bool expand, bool res, int B, int OH, int OW,
+                               bool scratch, int io, int num_cu);
 // scratch (nullable): B * OH * OW * cout * 2 floats for the hidden-split form of the late blocks on small maps.
 // io: bit 0 = fp16 input x, bit 1 = fp16 output y (the fp16mx schedule; slab-kernel geometries, blocks 1-7, only).
 hipError_t launch_x2_irb(int cin, int hid, int cout, int stride, bool expand, bool res, const void* x, const void* we,
