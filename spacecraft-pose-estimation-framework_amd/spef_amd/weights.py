@@ -86,6 +86,18 @@ def synthetic_state_dict(arch: Arch | None = None, seed: int = 1001, head_std: f
     return {k: (v.astype(np.float32) if v.dtype != np.int64 else v) for k, v in sd.items()}
 
 
+def plant_keypoint_head(sd: Dict[str, np.ndarray], kp_norm: np.ndarray) -> Dict[str, np.ndarray]:
+    """A keypoint-regression head (head/keypoints.py:10-27) whose sigmoid outputs are real keypoints: the head bias
+    becomes logit() of ``kp_norm`` (one frame's normalised keypoints, origin first, as KeyPoints.project returns them,
+    spe/keypoints_utils.py:47-110), so with small head weights every frame's keypoints spread over the spacecraft's
+    image as in the reference's keypoint mode instead of clustering where a random head puts them (an ill-conditioned
+    EPnP input). Returns ``sd`` with the bias replaced."""
+    k = np.clip(np.asarray(kp_norm, np.float64).reshape(-1), 1e-6, 1 - 1e-6)
+    assert sd['head.layer.1.bias'].shape == k.shape, (sd['head.layer.1.bias'].shape, k.shape)
+    sd['head.layer.1.bias'] = np.log(k / (1 - k)).astype(np.float32)
+    return sd
+
+
 def state_dict_digest(sd: Dict[str, np.ndarray]) -> str:
     """sha256 over keys and float32 bytes in key order -- pins the generator in the fixtures."""
     import hashlib

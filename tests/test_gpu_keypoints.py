@@ -8,7 +8,7 @@ from oracle import epnp_ref as E
 from oracle import model_ref as M
 from spef_amd import blob as Bl
 from spef_amd.arch import mobilenet_v2
-from spef_amd.weights import synthetic_state_dict
+from spef_amd.weights import plant_keypoint_head, synthetic_state_dict
 
 pytestmark = pytest.mark.gpu
 
@@ -224,9 +224,7 @@ def _planted_kp_sd(golden):
     the clustered, ill-conditioned points of a random head."""
     g = golden('keypoints.npz')
     i = int(np.argmin(np.abs(g['t'][:, 2] - np.median(g['t'][:, 2]))))
-    sd = synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=2e-4)
-    k = np.clip(g['kp2d'][i].astype(np.float64), 1e-6, 1 - 1e-6)
-    sd['head.layer.1.bias'] = np.log(k / (1 - k)).astype(np.float32)
+    sd = plant_keypoint_head(synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=2e-4), g['kp2d'][i])
     return sd, g, i
 
 
