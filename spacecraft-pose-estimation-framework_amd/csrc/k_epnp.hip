@@ -231,6 +231,9 @@ __device__ __forceinline__ int rr_partner(int r, int i) {
 #ifndef SPEF_EPNP_OSJ   // one-sided Jacobi on M (one wave) instead of the two-sided one on M^T M
 #define SPEF_EPNP_OSJ 0
 #endif
+#ifndef SPEF_EPNP_JTOL_OS   // one-sided form: off^2 <= JTOL_OS x diagonal^2
+#define SPEF_EPNP_JTOL_OS 1e-20
+#endif
 #ifndef SPEF_EPNP_JTOL   // Jacobi stops once off-diagonal^2 <= JTOL x diagonal^2
 #define SPEF_EPNP_JTOL 1e-26
 #endif
@@ -321,7 +324,7 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
     const int g = lane >> 3, l = lane & 7;
     const bool act = g < 6;
     for (int sweep = 0; sweep < 40; ++sweep) {
-      bool rotated = false;
+      double off = 0.0, dg = 0.0;   // this sweep's pre-rotation sums of c^2 and a^2 + b^2 over its 66 pairs
       for (int r = 0; r < 11; ++r) {
         int p = r, q = 11;
         if (g > 0) {
@@ -354,9 +357,12 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
         b = group8_sum(b);
         c = group8_sum(c);
         double cs = 1.0, sn = 0.0;
-        const bool rot = act && fabs(c) >= 1e-300 && c * c > SPEF_EPNP_JTOL * a * b;
+        const bool rot = act && fabs(c) >= 1e-300 && c * c > 1e-32 * a * b;
         if (rot) jacobi_rot(a, b, c, cs, sn);
-        rotated |= rot;
+        if (act && l == 0) {
+          off = fma(c, c, off);
+          dg = fma(a, a, fma(b, b, dg));
+        }
         if (rot) {   // (group-uniform: the 8 lanes hold the same sums)
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -372,7 +378,11 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
         }
         __asm__ volatile("" ::: "memory");
       }
-      if (!__any(rotated)) break;   // a sweep without a rotation: every pair orthogonal to the tolerance
+      // every column meets 11 pairs a sweep: dg / 11 = the squared diagonal of M^T M (the two-sided form's measure,
+      // here taken during the sweep, before its rotations); numpy restatement on the reference poses: 6.3 sweeps
+      off = warp_sum_d(off);
+      dg = warp_sum_d(dg);
+      if (off <= SPEF_EPNP_JTOL_OS * dg * (1.0 / 11.0)) break;
     }
     if (lane < 12) {   // eigenvalues: squared column norms of M V
       double ss = 0.0;
