@@ -206,21 +206,6 @@ __device__ __forceinline__ void undistort_point(const EpnpDist& d, double fu, do
 // sums are wave reductions. Latency per problem is what all this buys (a B = 64 batch is 64 concurrent problems):
 // one wave per problem took 134 us per launch, the former one-thread-per-problem kernel ~2 ms.
 
-// sum over the 8 lanes of a lane group (lanes 8 g .. 8 g + 7): xor-1 and xor-2 quad permutes, then the half-row
-// mirror (lane i <-> 7 - i within 8); fp64 as two 32-bit DPP moves
-template <int CTRL>
-__device__ __forceinline__ double dpp_f64(double x) {
-  const uint64_t u = __builtin_bit_cast(uint64_t, x);
-  const int lo = __builtin_amdgcn_mov_dpp((int)(uint32_t)u, CTRL, 0xF, 0xF, false);
-  const int hi = __builtin_amdgcn_mov_dpp((int)(uint32_t)(u >> 32), CTRL, 0xF, 0xF, false);
-  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
-}
-__device__ __forceinline__ double group8_sum(double x) {
-  x += dpp_f64<0xB1>(x);    // quad_perm [1, 0, 3, 2]
-  x += dpp_f64<0x4E>(x);    // quad_perm [2, 3, 0, 1]
-  return x + dpp_f64<0x141>(x);   // row_half_mirror
-}
-
 // partner of index i in round r of the 12-player round robin: pairs (r, 11) and (r + k, r - k) mod 11, k = 1..5
 __device__ __forceinline__ int rr_partner(int r, int i) {
   if (i == 11) return r;
@@ -228,12 +213,6 @@ __device__ __forceinline__ int rr_partner(int r, int i) {
   return (2 * r - i + 22) % 11;
 }
 
-#ifndef SPEF_EPNP_OSJ   // one-sided Jacobi on M (one wave) instead of the two-sided one on M^T M
-#define SPEF_EPNP_OSJ 0
-#endif
-#ifndef SPEF_EPNP_JTOL_OS   // one-sided form: off^2 <= JTOL_OS x diagonal^2
-#define SPEF_EPNP_JTOL_OS 1e-20
-#endif
 #ifndef SPEF_EPNP_JTOL   // Jacobi stops once off-diagonal^2 <= JTOL x diagonal^2
 #define SPEF_EPNP_JTOL 1e-26
 #endif
@@ -295,103 +274,6 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
   // control points: model[0..11] (model-only, spef_set_keypoints), read where used
   __syncthreads();
 
-#if SPEF_EPNP_OSJ
-  // ---- one-sided Jacobi on M itself (2n x 12, column-major in LDS, rows >= 2n zero): M V has orthogonal columns,
-  // V = the eigenvectors of M^T M, the squared column norms its eigenvalues (the subspaces of epnp.cpp's cvSVD of
-  // M^T M, without squaring M's condition). Wave 0 alone, no s_barrier inside: per round six disjoint column pairs
-  // (the tournament schedule), lane group g = lane / 8 owns pair g: its 8 lanes hold 4 rows of the two columns and 1-2
-  // rows of V's two columns, reduce the pair's dot products with DPP inside the group, compute the rotation
-  // redundantly and write the rotated columns back (a wave's LDS operations execute in issue order, so the next
-  // round's reads see every lane's writes).
-  __shared__ double Mc[12][32];
-  __shared__ double Ev[12];
-  double* const Vrm = Vs[0];   // V row-major: V[k][i] at 12 k + i (component k of eigenvector i)
-  for (int t = tid; t < 12 * 32; t += 192) {
-    const int col = t / 32, row = t - 32 * col;
-    const int cp = col / 3, dp = col - 3 * cp, i = row >> 1;
-    double v = 0.0;
-    if (i < n) {
-      const double a = Pal[i][cp];
-      v = (row & 1) == 0 ? (dp == 0 ? a * fu : dp == 2 ? a * Pdu[i] : 0.0)
-                         : (dp == 1 ? a * fv : dp == 2 ? a * Pdv[i] : 0.0);
-    }
-    Mc[col][row] = v;
-  }
-  if (tid < 144) Vrm[tid] = tid / 12 == tid % 12 ? 1.0 : 0.0;
-  __syncthreads();
-  const int cur = 0;
-  if (wave == 0) {
-    const int g = lane >> 3, l = lane & 7;
-    const bool act = g < 6;
-    for (int sweep = 0; sweep < 40; ++sweep) {
-      double off = 0.0, dg = 0.0;   // this sweep's pre-rotation sums of c^2 and a^2 + b^2 over its 66 pairs
-      for (int r = 0; r < 11; ++r) {
-        int p = r, q = 11;
-        if (g > 0) {
-          const int u = (r + g) % 11, w = (r - g + 11) % 11;
-          p = u < w ? u : w;
-          q = u < w ? w : u;
-        }
-        double xp[4] = {0, 0, 0, 0}, xq[4] = {0, 0, 0, 0}, vp[2] = {0, 0}, vq[2] = {0, 0};
-        if (act) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            xp[k] = Mc[p][l + 8 * k];
-            xq[k] = Mc[q][l + 8 * k];
-          }
-#pragma unroll
-          for (int k = 0; k < 2; ++k)
-            if (l + 8 * k < 12) {
-              vp[k] = Vrm[12 * (l + 8 * k) + p];
-              vq[k] = Vrm[12 * (l + 8 * k) + q];
-            }
-        }
-        double a = 0.0, b = 0.0, c = 0.0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          a = fma(xp[k], xp[k], a);
-          b = fma(xq[k], xq[k], b);
-          c = fma(xp[k], xq[k], c);
-        }
-        a = group8_sum(a);
-        b = group8_sum(b);
-        c = group8_sum(c);
-        double cs = 1.0, sn = 0.0;
-        const bool rot = act && fabs(c) >= 1e-300 && c * c > 1e-32 * a * b;
-        if (rot) jacobi_rot(a, b, c, cs, sn);
-        if (act && l == 0) {
-          off = fma(c, c, off);
-          dg = fma(a, a, fma(b, b, dg));
-        }
-        if (rot) {   // (group-uniform: the 8 lanes hold the same sums)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            Mc[p][l + 8 * k] = cs * xp[k] - sn * xq[k];
-            Mc[q][l + 8 * k] = sn * xp[k] + cs * xq[k];
-          }
-#pragma unroll
-          for (int k = 0; k < 2; ++k)
-            if (l + 8 * k < 12) {
-              Vrm[12 * (l + 8 * k) + p] = cs * vp[k] - sn * vq[k];
-              Vrm[12 * (l + 8 * k) + q] = sn * vp[k] + cs * vq[k];
-            }
-        }
-        __asm__ volatile("" ::: "memory");
-      }
-      // every column meets 11 pairs a sweep: dg / 11 = the squared diagonal of M^T M (the two-sided form's measure,
-      // here taken during the sweep, before its rotations); numpy restatement on the reference poses: 6.3 sweeps
-      off = warp_sum_d(off);
-      dg = warp_sum_d(dg);
-      if (off <= SPEF_EPNP_JTOL_OS * dg * (1.0 / 11.0)) break;
-    }
-    if (lane < 12) {   // eigenvalues: squared column norms of M V
-      double ss = 0.0;
-      for (int k = 0; k < 32; ++k) ss = fma(Mc[lane][k], Mc[lane][k], ss);
-      Ev[lane] = ss;
-    }
-  }
-  __syncthreads();
-#else
   // ---- M^T M (M never stored): entry e = (p, q) = thread e, accumulated point by point as r1[p] r1[q] + r2[p] r2[q]
   const int e = tid;
   const bool ent = e < 144;
@@ -454,16 +336,11 @@ __global__ __launch_bounds__(192) SPEF_EPNP_ATTR void epnp_kernel(const float* _
       __syncthreads();
     }
   }
-#endif
   // the 4 eigenvectors of smallest eigenvalue, ascending (ties keep the lower index); static loops only (a
   // dynamically indexed private array would live in scratch)
   double ev[12];
 #pragma unroll
-#if SPEF_EPNP_OSJ
-  for (int i = 0; i < 12; ++i) ev[i] = Ev[i];
-#else
   for (int i = 0; i < 12; ++i) ev[i] = As[cur][13 * i];
-#endif
   int idx[4];
   uint32_t used = 0;
 #pragma unroll

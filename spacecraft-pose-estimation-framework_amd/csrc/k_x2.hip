@@ -129,12 +129,6 @@ struct X2Slab {
 #ifndef SPEF_X2_RES_AHEAD   // persistent tiles: chunks before a tile's end at which its residual is fetched (4: no gain)
 #define SPEF_X2_RES_AHEAD 2
 #endif
-#ifndef SPEF_X2_PPRIO   // three-stage kernels: s_setprio 1 for the VALU (1) or MFMA (2) waves
-#define SPEF_X2_PPRIO 0
-#endif
-#ifndef SPEF_X2_WPRIO   // role-split kernels: s_setprio 1 for the expand waves (1)
-#define SPEF_X2_WPRIO 0
-#endif
 #ifndef SPEF_X2_ROWS0   // slab kernels: input rows shared between a wave's vertically adjacent pixel tiles
 #define SPEF_X2_ROWS0 1   // interleaved A/B, bit-identical: blocks 5-6 117.8 -> 111.0 us per step
 #endif
@@ -737,7 +731,6 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
 
   if (ewave) {
     // ================= expand waves
-    if constexpr (SPEF_X2_WPRIO == 1) __builtin_amdgcn_s_setprio(1);
     const int e = wr;
     // this wave's input-tile pixel tiles pt = e + NE j: B fragments (hi / lo) for every K step, loaded and split once
     // per tile. The fp32 rows are loaded into the fragments' own registers (8 floats of (j, ks) in the bits of
@@ -1317,7 +1310,6 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
   }
 
   if (ewave) {
-    if constexpr (SPEF_X2_PPRIO == 2) __builtin_amdgcn_s_setprio(1);
     // ================= MFMA waves: expand (pixel tiles e + NE j, both hidden halves) and project (output-channel tiles
     // e + NE t, every output pixel tile)
     const int e = wr;
@@ -1570,7 +1562,6 @@ __global__ __launch_bounds__(8 * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) 
     if (wave == 0) stamp(0, 7);
   } else {
     // ================= VALU waves: depthwise of output pixel tiles QPV d .. QPV d + QPV - 1 -> Ds
-    if constexpr (SPEF_X2_PPRIO == 1) __builtin_amdgcn_s_setprio(1);
     const int d = wr;
     int pbase[G::QPV];
 #pragma unroll
