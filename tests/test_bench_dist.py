@@ -63,3 +63,34 @@ def test_headline_line_compact_on_a_full_gpu_record():
     assert 'kernels' not in rec and 'keypoint_mode' not in rec
     assert set(rec['sub_records']) == {'c5', 'fp16x2', 'fp16', 'keypoint_mode', 'epnp'}
     assert rec['pose_err_vs_fp32_sharp_head']['fp16mx']['within_tolerance'] is True
+
+
+def test_roofline_traffic_lookup_by_launched_kernel():
+    """bench.py's PMC-traffic lookup for the roofline kernel: the profiling key names the kernel the library launched
+    (x2_irb / x2_irw / x2_irp, spef_api.cpp); each key must resolve to exactly one profiled instantiation of the
+    committed round-6 fp16mx traffic file, and the dominant kernel's bytes must be the file's entry for it."""
+    import json
+    bench = _bench_module()
+    path = os.path.join(REPO, 'profiles', 'r06_mx_pmc_traffic.json')
+    with open(path) as f:
+        kernels = json.load(f)['kernels']
+    keys = {'x2_irp_kernel<96,576,96,s1>': 'x2_irp_kernel<96,576,96,1,8,16,1,1>',
+            'x2_irw_kernel<64,384,64,s1>': 'x2_irw_kernel<64,384,64,1,8,16,1,1,1,1,1>',
+            'x2_irb_kernel<32,192,32,s1>': 'x2_irb_kernel<32,192,32,1,8,16,1,1,4,1,0>',
+            'x2_irp_kernel<160,960,320,s1>': 'x2_irp_kernel<160,960,320,1,8,8,0,0>',
+            'mx_irb_kernel<24,144,24,s1>': 'mx_irb_kernel<24,144,24,1,16,1,1,1>'}
+    for key, sym in keys.items():
+        assert bench.pmc_traffic(key, path) == kernels[sym]['hbm_bytes_per_launch'], key
+    assert bench.pmc_traffic('x2_irp_kernel<1,2,3,s1>', path) is None     # no such instantiation: no traffic figure
+
+
+def test_plant_keypoint_head_outputs_the_planted_keypoints():
+    """weights.plant_keypoint_head (the bench's keypoint sub-record and the B=64 keypoint test): with zero head weights
+    the sigmoid of the head output is exactly the planted keypoints (float32 logit / sigmoid round trip)."""
+    import numpy as np
+    from spef_amd.arch import mobilenet_v2
+    from spef_amd.weights import plant_keypoint_head, synthetic_state_dict
+    g = np.load(os.path.join(REPO, 'tests', 'golden', 'keypoints.npz'))
+    sd = plant_keypoint_head(synthetic_state_dict(mobilenet_v2('keypoints'), seed=1001, head_std=2e-4), g['kp2d'][7])
+    b = sd['head.layer.1.bias'].astype(np.float64)
+    np.testing.assert_allclose(1.0 / (1.0 + np.exp(-b)), g['kp2d'][7], rtol=0, atol=2e-7)
