@@ -52,7 +52,7 @@ INT8_BOUND = (0.05, 0.030, 0.25)   # logits, position (m), orientation (deg)
 FP16_TRAFFIC = ['r04_pmc_traffic.json', 'r03f_pmc_traffic.json']
 MX_TRAFFIC = ['r06_mx_pmc_traffic.json', 'r05_mx_pmc_traffic.json']
 INT8_TRAFFIC = ['r03_int8_pmc_traffic.json']
-X2_TRAFFIC = ['r05_x2_pmc_traffic.json', 'r04_x2_pmc_traffic.json']
+X2_TRAFFIC = ['r06_x2_pmc_traffic.json', 'r05_x2_pmc_traffic.json', 'r04_x2_pmc_traffic.json']
 TRAFFIC = {'fp16': FP16_TRAFFIC, 'bf16': FP16_TRAFFIC, 'int8': INT8_TRAFFIC, 'fp16x2': X2_TRAFFIC, 'fp16mx': MX_TRAFFIC}
 ARITH = {'fp16': 'fp16 storage, fp16 MFMA operands, fp32 accumulate (packed-fp16 depthwise in blocks 2-7)',
          'bf16': 'bf16 storage, bf16 MFMA operands, fp32 accumulate',
